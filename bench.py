@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Headline benchmark: verified Chaum-Pedersen proofs per second on MI355X.
+
+Workload (BASELINE.json configs[1]): 2^20 ristretto255 Chaum-Pedersen proofs, per-proof
+(non-batched) verification -- the reference's BatchVerifier::verify outcome per entry
+(batch.rs:171-231) -- with inputs resident in HBM.  One step = one pass of the verify
+path over the whole batch: k_challenge (Merlin/STROBE Fiat-Shamir challenges + response
+checks) followed by k_verify_each (4 ristretto decodes + 2 Straus double-scalar
+equations per proof).  Inputs are synthetic: valid proofs from the GPU prover
+(cpz_prove_synthetic_device, ChaCha20-derived witnesses, distinct per rank).
+
+Multi-GPU (torchrun, one process per GPU): each rank verifies its own 2^20 proofs; there
+is no data-path collective (per-proof verification has no exchange step), so scaling
+is weak and value = all ranks' proofs / max-over-ranks time.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "chaum-pedersen-zkp_amd"))
+
+SEED_X = hashlib.sha256(b"cpz-bench-x").digest()
+SEED_K = hashlib.sha256(b"cpz-bench-k").digest()
+
+
+def _load_json(rel):
+    p = os.path.join(ROOT, rel)
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f)
+    return None
+
+
+def cpu_baseline(host_rows, seconds: float, threads: int):
+    """Time the C oracle (reference-semantics per-proof verify, oracle/cpz_oracle.c) on a
+    bounded sample of the same synthetic proofs.  Test/measurement infrastructure only."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import coracle  # noqa: WPS433
+    except Exception as exc:  # pragma: no cover - reported, not fatal
+        return {"value": None, "error": "C oracle unavailable: %s" % exc}
+    return coracle.time_verify(host_rows, seconds=seconds, threads=threads)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=1 << 20, help="proofs per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (rank 0, N=1)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = min(16, cpus))")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    import chaum_pedersen as cp
+
+    gpu = cp.Gpu(local_rank)
+    n = args.n
+    t = {k: torch.empty((n, 32), dtype=torch.uint8, device=dev) for k in ("y1", "y2", "r1", "r2", "s")}
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    gpu.prove_synthetic_device(n, SEED_X, SEED_K, t["y1"], t["y2"], t["r1"], t["r2"], t["s"],
+                               first_index=rank * n, stream=stream)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        gpu.verify_each_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    n_bad = int((status != 0).sum().item())
+    if n_bad:
+        raise SystemExit("bench: %d of %d valid synthetic proofs rejected -- refusing to report" % (n_bad, n))
+
+    gpu.set_timing(True)
+    gpu.stage_times()  # reset
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stages = gpu.stage_times()
+    gpu.set_timing(False)
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    # the timed steps must also have verified everything
+    n_bad = int((status != 0).sum().item())
+    if n_bad:
+        raise SystemExit("bench: %d proofs rejected in the timed region" % n_bad)
+
+    total = world * n * args.steps
+    value = total / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    oc = _load_json("bench/opcount.json") or {}
+    mads = oc.get("verify_each", {}).get("mads_per_proof", 490660)
+    peak_mad = oc.get("peaks", {}).get("v_mad_u64_u32_lane_ops_per_s", 25.35e12)
+    v_ms, v_cnt = stages.get("verify_each", (0.0, 0))
+    c_ms, c_cnt = stages.get("challenge", (0.0, 0))
+    v_avg_s = (v_ms / v_cnt) * 1e-3 if v_cnt else None
+    achieved = (mads * n / v_avg_s) / 1e12 if v_avg_s else None
+    pmc = _load_json("profiles/r01_verify_each_pmc.json") or {}
+    roofline = {
+        "kernel": "k_verify_each",
+        "bound": "valu-int",
+        "achieved": achieved,
+        "peak": peak_mad / 1e12,
+        "unit": "Tmad/s",
+        "frac": (achieved / (peak_mad / 1e12)) if achieved else None,
+        "traffic": pmc.get("hbm_bytes_per_launch"),
+        "algorithmic_mads_per_proof": mads,
+        "kernel_ms": v_ms / v_cnt if v_cnt else None,
+        "challenge_kernel_ms": c_ms / c_cnt if c_cnt else None,
+        "hbm_frac": ((194 * n / v_avg_s) / 8.0e12) if v_avg_s else None,
+    }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        sample = 1 << 14
+        rows = {k: t[k][:sample].cpu().numpy() for k in t}
+        cpu = cpu_baseline(rows, args.cpu_seconds, threads)
+
+    if rank == 0:
+        line = {
+            "metric": "verified proofs/sec (1/2/4/8 MI355X) + % int-VALU roofline vs host-CPU",
+            "value": value,
+            "unit": "proofs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32/int64 limbs (GF(2^255-19), radix 2^25.5)",
+            "data": "synthetic (GPU prover, ChaCha20-derived witnesses; all proofs valid, checked)",
+            "config": {"workload": "configs[1]: 2^20 proofs per GPU, per-proof verification (challenge + 2 equations)",
+                       "proofs_per_gpu": n, "contexts": "none", "generators": "default (g, h)",
+                       "parallelism": "dp%d (independent shards, no collective)" % world},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    gpu.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,105 @@
+"""Build recipes for the in-tree native artefacts (no cmake/ninja needed).
+
+* ``lib/libcpz.so``      -- the product: gfx950 HIP kernels + host runtime + C ABI
+                           (hipcc --offload-arch=gfx950).
+* ``tests/native/libcpz_hosttest.so`` -- CPU build of the device-library headers with
+                           limb-bound assertions, for unit tests only.
+* ``oracle/``            -- delegated to oracle/Makefile (the C oracle: CPU baseline and
+                           at-scale checker; test infrastructure only).
+
+Each target is rebuilt only when one of its sources is newer than the output.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIBDIR = os.path.join(PKG, "lib")
+LIBCPZ = os.path.join(LIBDIR, "libcpz.so")
+HOSTTEST = os.path.join(ROOT, "tests", "native", "libcpz_hosttest.so")
+ARCH = os.environ.get("CPZ_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the gfx950 build needs ROCm")
+
+
+def _newer(out: str, srcs) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > t for s in srcs)
+
+
+def _headers():
+    hdr = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    return hdr + [os.path.join(ROOT, "include", "cpz.h")]
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build step failed: %s\n%s" % (" ".join(cmd), r.stdout[-4000:]))
+    return r.stdout
+
+
+def build_libcpz(force: bool = False, verbose: bool = False) -> str:
+    units = ["kernels.hip", "runtime.hip"]
+    srcs = [os.path.join(CSRC, u) for u in units] + _headers()
+    if not force and not _newer(LIBCPZ, srcs):
+        return LIBCPZ
+    os.makedirs(os.path.join(LIBDIR, "obj"), exist_ok=True)
+    hipcc = _hipcc()
+    common = [hipcc, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-I", CSRC,
+              "-I", os.path.join(ROOT, "include")]
+
+    def compile_one(u):
+        obj = os.path.join(LIBDIR, "obj", u.replace(".hip", ".o"))
+        if force or _newer(obj, [os.path.join(CSRC, u)] + _headers()):
+            _run(common + ["-c", os.path.join(CSRC, u), "-o", obj])
+        return obj
+
+    with ThreadPoolExecutor(max_workers=len(units)) as ex:
+        objs = list(ex.map(compile_one, units))
+    tmp = LIBCPZ + ".tmp"
+    _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs)
+    os.replace(tmp, LIBCPZ)
+    if verbose:
+        print("built", LIBCPZ)
+    return LIBCPZ
+
+
+def build_hosttest(force: bool = False) -> str:
+    src = os.path.join(ROOT, "tests", "native", "hostlib.cpp")
+    if not force and not _newer(HOSTTEST, [src] + _headers()):
+        return HOSTTEST
+    cxx = shutil.which("g++") or "g++"
+    tmp = HOSTTEST + ".tmp"
+    _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-DCPZ_BOUNDS_CHECK", "-DCPZ_COUNT_OPS", "-I", CSRC, src, "-o", tmp])
+    os.replace(tmp, HOSTTEST)
+    return HOSTTEST
+
+
+def build_oracle(force: bool = False) -> None:
+    mk = os.path.join(ROOT, "oracle", "Makefile")
+    if os.path.exists(mk):
+        _run(["make", "-s", "-C", os.path.join(ROOT, "oracle")] + (["-B"] if force else []))
+
+
+def build_all(force: bool = False, verbose: bool = False) -> None:
+    build_hosttest(force)
+    build_oracle(force)
+    build_libcpz(force, verbose)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv, verbose=True)

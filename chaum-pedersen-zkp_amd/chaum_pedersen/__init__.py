@@ -1,0 +1,406 @@
+"""chaum_pedersen -- MI355X-native drop-in for the reference's verify path.
+
+Mirrors the reference crate's public surface for the batch-verification path
+(kobby-pentangeli/chaum-pedersen-zkp: src/verifier/batch.rs, src/primitives/gadgets.rs)
+on top of the C ABI in include/cpz.h:
+
+    Parameters, Statement, Proof       gadgets.rs:25-489 (encodings kept as 32-byte strings)
+    BatchVerifier                      batch.rs:82-324 (same names, cap, errors, ordering)
+    Gpu                                bulk / device-resident entry points (no 1000 cap)
+
+Every verification runs the gfx950 kernels in lib/libcpz.so; nothing here computes a
+verification result on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import struct
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _native
+from ._native import (CpzError, STATUS_BAD_POINT, STATUS_BAD_SCALAR, STATUS_EQ_FAIL,
+                      STATUS_IDENTITY_OR_ZERO, STATUS_OK)
+
+__all__ = [
+    "Error", "InvalidParams", "InvalidScalar", "InvalidGroupElement", "CpzError",
+    "Parameters", "Statement", "Proof", "BatchVerifier", "Gpu", "VerifyResult",
+    "MAX_BATCH_SIZE", "PROTOCOL_VERSION", "STATUS_OK", "STATUS_EQ_FAIL", "STATUS_BAD_POINT",
+    "STATUS_BAD_SCALAR", "STATUS_IDENTITY_OR_ZERO", "default_generators",
+]
+
+MAX_BATCH_SIZE = 1000          # batch.rs:48
+PROTOCOL_VERSION = 1           # gadgets.rs:12
+
+
+# --- error taxonomy (src/error.rs:5-17) -------------------------------------------------
+class Error(Exception):
+    pass
+
+
+class InvalidParams(Error):
+    pass
+
+
+class InvalidScalar(Error):
+    pass
+
+
+class InvalidGroupElement(Error):
+    pass
+
+
+_STATUS_ERR = {
+    STATUS_EQ_FAIL: (InvalidParams, "Proof verification failed"),
+    STATUS_BAD_POINT: (InvalidGroupElement, "Bytes do not represent a valid Ristretto point"),
+    STATUS_BAD_SCALAR: (InvalidScalar, "Bytes do not represent a valid scalar"),
+    STATUS_IDENTITY_OR_ZERO: (InvalidParams, "Commitment contains identity element or response scalar is zero"),
+}
+
+
+class VerifyResult:
+    """Per-entry `Result<()>` of BatchVerifier::verify."""
+
+    __slots__ = ("status",)
+
+    def __init__(self, status: int):
+        self.status = int(status)
+
+    def is_ok(self) -> bool:
+        return self.status == STATUS_OK
+
+    def is_err(self) -> bool:
+        return self.status != STATUS_OK
+
+    def error(self) -> Optional[Error]:
+        if self.status == STATUS_OK:
+            return None
+        cls, msg = _STATUS_ERR[self.status]
+        return cls(msg)
+
+    def __repr__(self) -> str:
+        return "Ok(())" if self.is_ok() else "Err(%r)" % (self.error(),)
+
+
+def default_generators():
+    """(g, h) encodings: basepoint and hash-to-group of the h DST (ristretto.rs:79-91)."""
+    return _native.default_generators()
+
+
+def _b32(x, what: str) -> bytes:
+    b = bytes(x)
+    if len(b) != 32:
+        raise InvalidGroupElement("Expected 32 bytes, got %d (%s)" % (len(b), what))
+    return b
+
+
+class Parameters:
+    """Generators (g, h).  Parameters() gives the defaults (gadgets.rs:43-48)."""
+
+    def __init__(self, g: Optional[bytes] = None, h: Optional[bytes] = None):
+        dg, dh = default_generators()
+        self.g = dg if g is None else _b32(g, "g")
+        self.h = dh if h is None else _b32(h, "h")
+
+    @classmethod
+    def new(cls) -> "Parameters":
+        return cls()
+
+    @classmethod
+    def with_generators(cls, g: bytes, h: bytes) -> "Parameters":
+        """gadgets.rs:77-103: identity / equal generators rejected here; undecodable ones
+        are rejected by the GPU table build (CPZ_EGENERATOR) on first use."""
+        g, h = _b32(g, "g"), _b32(h, "h")
+        if g == bytes(32):
+            raise InvalidParams("Generator g cannot be identity")
+        if h == bytes(32):
+            raise InvalidParams("Generator h cannot be identity")
+        if g == h:
+            raise InvalidParams("Generators g and h must be different")
+        return cls(g, h)
+
+    def generator_g(self) -> bytes:
+        return self.g
+
+    def generator_h(self) -> bytes:
+        return self.h
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, Parameters) and (self.g, self.h) == (other.g, other.h)
+
+    def __hash__(self) -> int:
+        return hash((self.g, self.h))
+
+
+class Statement:
+    """Public values (y1, y2) as 32-byte encodings (gadgets.rs:177-239)."""
+
+    def __init__(self, y1: bytes, y2: bytes):
+        self.y1 = _b32(y1, "y1")
+        self.y2 = _b32(y2, "y2")
+
+
+class Proof:
+    """Commitment (r1, r2) and response s (gadgets.rs:307-489)."""
+
+    def __init__(self, r1: bytes, r2: bytes, s: bytes, version: int = PROTOCOL_VERSION):
+        self.r1 = _b32(r1, "r1")
+        self.r2 = _b32(r2, "r2")
+        self.s = bytes(s)
+        if len(self.s) != 32:
+            raise InvalidScalar("Expected 32 bytes, got %d" % len(self.s))
+        self.version = version
+
+    def to_bytes(self) -> bytes:
+        """gadgets.rs:343-361: [ver][u32be 32][r1][u32be 32][r2][u32be 32][s] = 109 bytes."""
+        out = bytearray([self.version])
+        for part in (self.r1, self.r2, self.s):
+            out += struct.pack(">I", len(part)) + part
+        return bytes(out)
+
+    @classmethod
+    def from_bytes(cls, b: bytes) -> "Proof":
+        """Structural checks of gadgets.rs:364-461 (version, lengths, truncation, trailing
+        bytes).  Whether r1/r2 decode, s is canonical/non-zero and r1/r2 are not the identity
+        is decided on the GPU and reported per entry by the verifiers (status 2/3/4)."""
+        b = bytes(b)
+        if len(b) < 1 + 4 + 1 + 4 + 1 + 4 + 1:
+            raise InvalidParams("Proof too small: %d bytes" % len(b))
+        if b[0] != PROTOCOL_VERSION:
+            raise InvalidParams("Unsupported proof version: %d" % b[0])
+        pos = 1
+        parts = []
+        for name, maxlen, err in (("r1", 4096, InvalidGroupElement), ("r2", 4096, InvalidGroupElement),
+                                  ("s", 512, InvalidScalar)):
+            if pos + 4 > len(b):
+                raise InvalidParams("Truncated proof: missing %s length" % name)
+            ln = struct.unpack(">I", b[pos:pos + 4])[0]
+            pos += 4
+            if ln == 0 or ln > maxlen:
+                raise InvalidParams("Invalid %s length: %d" % (name, ln))
+            if pos + ln > len(b):
+                raise InvalidParams("Truncated proof: incomplete %s data" % name)
+            if ln != 32:
+                raise err("Expected 32 bytes, got %d" % ln)
+            parts.append(b[pos:pos + ln])
+            pos += ln
+        if pos != len(b):
+            raise InvalidParams("Proof has %d trailing bytes" % (len(b) - pos))
+        return cls(*parts)
+
+    def commitment(self):
+        return self.r1, self.r2
+
+    def response(self) -> bytes:
+        return self.s
+
+
+def _rows(data, n: int, name: str) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(data, dtype=np.uint8))
+    if a.shape != (n, 32):
+        a = a.reshape(n, 32)
+    return a
+
+
+def _ctx_arrays(contexts: Optional[Sequence[Optional[bytes]]], n: int):
+    """None -> no contexts.  Otherwise (blob, offsets[n+1], present[n])."""
+    if contexts is None:
+        return None, None, None
+    if len(contexts) != n:
+        raise InvalidParams("contexts length %d != %d" % (len(contexts), n))
+    present = np.array([0 if c is None else 1 for c in contexts], dtype=np.uint8)
+    if not present.any():
+        return None, None, None
+    lens = np.array([0 if c is None else len(c) for c in contexts], dtype=np.uint64)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    blob = np.frombuffer(b"".join(c for c in contexts if c is not None) or b"\0", dtype=np.uint8).copy()
+    return blob, off, present
+
+
+def _ptr(a) -> Optional[int]:
+    return None if a is None else a.ctypes.data
+
+
+class Gpu:
+    """A verifier context on one GPU (cpz_ctx).  Bulk entry points, no batch cap."""
+
+    def __init__(self, device: int = 0):
+        lib = _native.load()
+        ndev = lib.cpz_device_count()
+        if ndev <= 0:
+            raise CpzError(_native.CPZ_EHIP, "no GPU visible to the HIP runtime")
+        h = ctypes.c_void_p()
+        _native.check(lib.cpz_ctx_create(device, ctypes.byref(h)))
+        self._lib = lib
+        self._h = h
+        self.device = device
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.cpz_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- per-kernel timing (HIP events on the launch stream) -------------------------------
+    STAGES = ("challenge", "verify_each", "rlc_prepare", "rlc_msm", "fallback", "s5", "s6", "s7")
+
+    def set_timing(self, enable: bool) -> None:
+        _native.check(self._lib.cpz_ctx_set_timing(self._h, 1 if enable else 0))
+
+    def stage_times(self):
+        """{stage: (total_ms, launches)} since the previous call (synchronises)."""
+        ms = (ctypes.c_double * _native.NUM_STAGES)()
+        cnt = (ctypes.c_int * _native.NUM_STAGES)()
+        _native.check(self._lib.cpz_ctx_stage_times(self._h, ms, cnt))
+        return {self.STAGES[k]: (ms[k], cnt[k]) for k in range(_native.NUM_STAGES) if cnt[k]}
+
+    # -- host-buffer entry points ---------------------------------------------------------
+    def verify_each(self, y1, y2, r1, r2, s, contexts=None, params: Optional[Parameters] = None) -> np.ndarray:
+        """Status per proof (uint8[n]) for (n, 32) byte arrays.  cpz_verify_each."""
+        params = params or Parameters()
+        n = len(y1)
+        arrs = [_rows(a, n, nm) for a, nm in ((y1, "y1"), (y2, "y2"), (r1, "r1"), (r2, "r2"), (s, "s"))]
+        blob, off, present = _ctx_arrays(contexts, n)
+        out = np.empty(n, dtype=np.uint8)
+        _native.check(self._lib.cpz_verify_each(
+            self._h, params.g, params.h, n, *[_ptr(a) for a in arrs], _ptr(blob), _ptr(off), _ptr(present),
+            _ptr(out)))
+        return out
+
+    def challenges(self, y1, y2, r1, r2, contexts=None, params: Optional[Parameters] = None) -> np.ndarray:
+        params = params or Parameters()
+        n = len(y1)
+        arrs = [_rows(a, n, nm) for a, nm in ((y1, "y1"), (y2, "y2"), (r1, "r1"), (r2, "r2"))]
+        blob, off, present = _ctx_arrays(contexts, n)
+        out = np.empty((n, 32), dtype=np.uint8)
+        _native.check(self._lib.cpz_challenges(
+            self._h, params.g, params.h, n, *[_ptr(a) for a in arrs], _ptr(blob), _ptr(off), _ptr(present),
+            _ptr(out)))
+        return out
+
+    def prove_synthetic(self, n: int, seed_x: bytes, seed_k: bytes, first_index: int = 0, contexts=None,
+                        params: Optional[Parameters] = None):
+        """Synthetic proofs from ChaCha20-derived witnesses: dict of (n, 32) arrays."""
+        params = params or Parameters()
+        outs = {k: np.empty((n, 32), dtype=np.uint8) for k in ("y1", "y2", "r1", "r2", "s")}
+        blob, off, present = _ctx_arrays(contexts, n)
+        _native.check(self._lib.cpz_prove_synthetic(
+            self._h, params.g, params.h, n, first_index, bytes(seed_x), bytes(seed_k), _ptr(blob), _ptr(off),
+            _ptr(present), *[_ptr(outs[k]) for k in ("y1", "y2", "r1", "r2", "s")]))
+        return outs
+
+    # -- device-resident entry points (torch tensors on this GPU) ---------------------------
+    def verify_each_device(self, y1, y2, r1, r2, s, status_out, params: Optional[Parameters] = None,
+                           stream: Optional[int] = None, ctx_bytes=None, ctx_off=None, ctx_present=None) -> None:
+        """Enqueue verification of device tensors (uint8, (n, 32), 16-B aligned) on `stream`."""
+        params = params or Parameters()
+        n = int(y1.shape[0])
+        dp = lambda t: None if t is None else t.data_ptr()
+        _native.check(self._lib.cpz_verify_each_device(
+            self._h, params.g, params.h, n, dp(y1), dp(y2), dp(r1), dp(r2), dp(s), dp(ctx_bytes), dp(ctx_off),
+            dp(ctx_present), dp(status_out), stream))
+
+    def prove_synthetic_device(self, n: int, seed_x: bytes, seed_k: bytes, y1, y2, r1, r2, s, first_index: int = 0,
+                               params: Optional[Parameters] = None, stream: Optional[int] = None) -> None:
+        params = params or Parameters()
+        _native.check(self._lib.cpz_prove_synthetic_device(
+            self._h, params.g, params.h, n, first_index, bytes(seed_x), bytes(seed_k), None, None, None,
+            y1.data_ptr(), y2.data_ptr(), r1.data_ptr(), r2.data_ptr(), s.data_ptr(), stream))
+
+
+_default_gpu: Optional[Gpu] = None
+
+
+def _gpu() -> Gpu:
+    global _default_gpu
+    if _default_gpu is None:
+        _default_gpu = Gpu(0)
+    return _default_gpu
+
+
+class _Entry:
+    __slots__ = ("params", "statement", "proof", "context")
+
+    def __init__(self, params, statement, proof, context):
+        self.params, self.statement, self.proof, self.context = params, statement, proof, context
+
+
+class BatchVerifier:
+    """Mirror of `verifier::batch::BatchVerifier` (batch.rs:82-324).
+
+    Same cap (MAX_BATCH_SIZE, batch.rs:48, 151-156), same empty-batch error
+    (batch.rs:172-176), results in entry order.  `verify` returns one VerifyResult per
+    entry: exactly what the reference returns, because its n >= 2 batch equation falls
+    back to per-entry verification and its n == 1 path is verify_one.
+    """
+
+    def __init__(self, gpu: Optional[Gpu] = None):
+        self._entries: List[_Entry] = []
+        self._gpu = gpu
+
+    @classmethod
+    def new(cls) -> "BatchVerifier":
+        return cls()
+
+    @classmethod
+    def with_capacity(cls, capacity: int) -> "BatchVerifier":
+        return cls()
+
+    def len(self) -> int:
+        return len(self._entries)
+
+    __len__ = len
+
+    def is_empty(self) -> bool:
+        return not self._entries
+
+    def remaining_capacity(self) -> int:
+        return max(0, MAX_BATCH_SIZE - len(self._entries))
+
+    def add(self, params: Parameters, statement: Statement, proof: Proof) -> None:
+        self.add_with_context(params, statement, proof, None)
+
+    def add_with_context(self, params: Parameters, statement: Statement, proof: Proof,
+                         context: Optional[bytes]) -> None:
+        if len(self._entries) >= MAX_BATCH_SIZE:
+            raise InvalidParams("Batch size limit exceeded (max %d)" % MAX_BATCH_SIZE)
+        self._entries.append(_Entry(params, statement, proof, None if context is None else bytes(context)))
+
+    def clear(self) -> None:
+        self._entries.clear()
+
+    def verify(self, rng=None) -> List[VerifyResult]:
+        """batch.rs:171-183.  `rng` is accepted for signature parity; per-entry
+        verification consumes no randomness."""
+        if not self._entries:
+            raise InvalidParams("Cannot verify empty batch")
+        gpu = self._gpu or _gpu()
+        status = np.empty(len(self._entries), dtype=np.uint8)
+        # One bulk call per distinct Parameters (normally a single group).
+        groups = {}
+        for i, e in enumerate(self._entries):
+            groups.setdefault((e.params.g, e.params.h), []).append(i)
+        for (g, h), idx in groups.items():
+            ents = [self._entries[i] for i in idx]
+            st = gpu.verify_each(
+                np.frombuffer(b"".join(e.statement.y1 for e in ents), np.uint8).reshape(-1, 32),
+                np.frombuffer(b"".join(e.statement.y2 for e in ents), np.uint8).reshape(-1, 32),
+                np.frombuffer(b"".join(e.proof.r1 for e in ents), np.uint8).reshape(-1, 32),
+                np.frombuffer(b"".join(e.proof.r2 for e in ents), np.uint8).reshape(-1, 32),
+                np.frombuffer(b"".join(e.proof.s for e in ents), np.uint8).reshape(-1, 32),
+                contexts=[e.context for e in ents], params=Parameters(g, h))
+            status[np.array(idx)] = st
+        return [VerifyResult(s) for s in status]

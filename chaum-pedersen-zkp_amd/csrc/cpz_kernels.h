@@ -1,0 +1,79 @@
+// Kernel argument blocks and launchers shared by kernels.hip and the host runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "scalarmul.h"
+
+namespace cpz {
+
+constexpr uint8_t kStatusOk = 0;
+constexpr uint8_t kStatusEqFail = 1;
+constexpr uint8_t kStatusBadPoint = 2;
+constexpr uint8_t kStatusBadScalar = 3;
+constexpr uint8_t kStatusIdentityOrZero = 4;
+
+constexpr int kNielsEntries = kTableB;   // radix-256 signed digits: |d| <= 128
+constexpr int kCachedEntries = kTableV;   // radix-16 signed digits: |d| <= 8
+constexpr int kVerifyBlock = 256;
+
+// Merlin/STROBE sponge snapshot.
+struct StrobeSnap {
+  uint8_t state[200];
+  int32_t pos;
+  int32_t pos_begin;
+  int32_t flags;
+  int32_t pad;
+};
+
+struct ChallengeArgs {
+  int64_t n;
+  uint32_t gh_words[16];         // encodings of g and h
+  const uint32_t* y1;            // n x 8 words each (SoA rows of 32 bytes)
+  const uint32_t* y2;
+  const uint32_t* r1;
+  const uint32_t* r2;
+  const uint32_t* s;             // may be null (prover)
+  const uint8_t* ctx_bytes;      // concatenated contexts
+  const uint64_t* ctx_off;       // n + 1 offsets, or null: no contexts
+  const uint8_t* ctx_present;    // n flags (Some/None), or null: all Some when ctx_off set
+  const StrobeSnap* prefix;      // [0] after Transcript::new(), [1] after append_parameters
+  uint32_t* c_out;               // n x 8 words
+  uint8_t* status_out;           // n (written when s != null)
+};
+
+struct VerifyArgs {
+  int64_t n;
+  const uint32_t* y1;
+  const uint32_t* y2;
+  const uint32_t* r1;
+  const uint32_t* r2;
+  const uint32_t* s;
+  const uint32_t* c;
+  uint8_t* status;               // in: response-scalar status; out: final status
+  const ge_niels* tab;           // [0, 128): g, [128, 256): h
+  ge_cached* scratch;            // grid * kVerifyBlock * kCachedEntries entries
+};
+
+struct ProveArgs {
+  int64_t n;
+  uint64_t first_index;
+  uint32_t seed_x[8];
+  uint32_t seed_k[8];
+  const ge_niels* tab;
+  uint32_t* y1;
+  uint32_t* y2;
+  uint32_t* r1;
+  uint32_t* r2;
+  const uint32_t* c;
+  uint32_t* s_out;
+};
+
+hipError_t launch_transcript_prefix(const uint32_t* gh_words, StrobeSnap* out, hipStream_t st);
+hipError_t launch_challenge(const ChallengeArgs& a, hipStream_t st);
+hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, hipStream_t st);
+hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st);
+hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st);
+hipError_t launch_prove_response(const ProveArgs& a, hipStream_t st);
+
+}  // namespace cpz

@@ -1,0 +1,262 @@
+// gfx950 kernels for the Chaum-Pedersen verify path.
+//
+//   k_transcript_prefix  one thread: Merlin state after Transcript::new() (S0) and after
+//                        append_parameters(g, h) (S1)          transcript.rs:29-50
+//   k_challenge          1 thread / proof: Fiat-Shamir challenge c (bit-exact merlin),
+//                        response-scalar checks (from_canonical_bytes, zero)
+//                        batch.rs:188-206, gadgets.rs:466-482
+//   k_build_niels        (k * B) for k = 1..128, B in {g, h}: affine Niels tables
+//   k_verify_each        1 thread / proof: 4 ristretto decodes, then
+//                        [s]g - [c]y1 == r1 and [s]h - [c]y2 == r2 (ristretto equality)
+//                        by a Straus loop: radix-16 signed digits of c against a per-proof
+//                        table of 8 multiples of -y (HBM-backed scratch), radix-256 signed
+//                        digits of s against the shared 128-entry LDS table of g (h).
+//                        batch.rs:185-231, verifier/mod.rs:144-171
+//   k_prove_points /     synthetic-input generator: Prover::prove_with_transcript
+//   k_prove_response     (prover/mod.rs:86-131) with ChaCha20-derived witnesses/nonces
+//
+// Status codes (uint8 per proof): 0 valid, 1 equation failed, 2 undecodable point,
+// 3 non-canonical s, 4 identity commitment or zero s.
+#include <hip/hip_runtime.h>
+
+#include "cpz_kernels.h"
+#include "ristretto.h"
+#include "scalar25519.h"
+#include "transcript.h"
+#include "scalarmul.h"
+#include "verify.h"
+
+namespace cpz {
+
+// ---------------------------------------------------------------------------------------
+// Loads
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void load_words8(uint32_t w[8], const uint32_t* base, int64_t i) {
+  const uint4* p = reinterpret_cast<const uint4*>(base + 8 * i);
+  const uint4 a = p[0], b = p[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+  w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+
+__device__ __forceinline__ bool words_zero(const uint32_t w[8]) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) acc |= w[k];
+  return acc == 0;
+}
+
+__device__ __forceinline__ void store_words8(uint32_t* base, int64_t i, const uint32_t w[8]) {
+  uint4* p = reinterpret_cast<uint4*>(base + 8 * i);
+  p[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  p[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Transcript: per-thread STROBE image in LDS, dword-interleaved across the block so the
+// Keccak load/store of all threads is bank-conflict free.
+// ---------------------------------------------------------------------------------------
+struct LdsState {
+  uint32_t* base;  // __shared__ uint32_t[50 * T]
+  int tid;
+  int T;
+  __device__ __forceinline__ uint8_t* byte_ptr(int i) const {
+    return reinterpret_cast<uint8_t*>(base + (i >> 2) * T + tid) + (i & 3);
+  }
+  __device__ __forceinline__ uint8_t get(int i) const { return *byte_ptr(i); }
+  __device__ __forceinline__ void put(int i, uint8_t v) { *byte_ptr(i) = v; }
+  __device__ __forceinline__ void xor_(int i, uint8_t v) { *byte_ptr(i) ^= v; }
+  __device__ __forceinline__ void permute() {
+    uint64_t a[25];
+#pragma unroll
+    for (int l = 0; l < 25; l++)
+      a[l] = (uint64_t)base[(2 * l) * T + tid] | ((uint64_t)base[(2 * l + 1) * T + tid] << 32);
+    keccak_f1600(a);
+#pragma unroll
+    for (int l = 0; l < 25; l++) {
+      base[(2 * l) * T + tid] = (uint32_t)a[l];
+      base[(2 * l + 1) * T + tid] = (uint32_t)(a[l] >> 32);
+    }
+  }
+};
+
+__global__ void k_transcript_prefix(const uint32_t* __restrict__ gh_words, StrobeSnap* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  ArrayState st;
+  Strobe<ArrayState> s = transcript_new(st);
+  for (int i = 0; i < 200; i++) out[0].state[i] = st.b[i];
+  out[0].pos = s.pos; out[0].pos_begin = s.pos_begin; out[0].flags = s.cur_flags;
+  transcript_parameters(s, gh_words, gh_words + 8);
+  for (int i = 0; i < 200; i++) out[1].state[i] = st.b[i];
+  out[1].pos = s.pos; out[1].pos_begin = s.pos_begin; out[1].flags = s.cur_flags;
+}
+
+constexpr int kChallengeBlock = 128;
+
+__global__ void __launch_bounds__(kChallengeBlock) k_challenge(ChallengeArgs a) {
+  __shared__ uint32_t lds[50 * kChallengeBlock];
+  const int64_t i = (int64_t)blockIdx.x * kChallengeBlock + threadIdx.x;
+  if (i >= a.n) return;
+  LdsState st{lds, (int)threadIdx.x, kChallengeBlock};
+  const bool has_ctx = a.ctx_off != nullptr && (a.ctx_present == nullptr || a.ctx_present[i] != 0);
+  const StrobeSnap& snap = a.prefix[has_ctx ? 0 : 1];
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(snap.state);
+#pragma unroll
+    for (int w = 0; w < 50; w++) lds[w * kChallengeBlock + threadIdx.x] = src[w];
+  }
+  Strobe<LdsState> s(st, snap.pos, snap.pos_begin, (uint8_t)snap.flags);
+  if (has_ctx) {
+    const uint64_t b0 = a.ctx_off[i], b1 = a.ctx_off[i + 1];
+    transcript_context(s, a.ctx_bytes + b0, (uint32_t)(b1 - b0));
+    transcript_parameters(s, a.gh_words, a.gh_words + 8);
+  }
+  uint32_t y1[8], y2[8], r1[8], r2[8];
+  load_words8(y1, a.y1, i);
+  load_words8(y2, a.y2, i);
+  load_words8(r1, a.r1, i);
+  load_words8(r2, a.r2, i);
+  const sc c = transcript_challenge(s, y1, y2, r1, r2);
+  store_words8(a.c_out, i, c.w);
+  if (a.s != nullptr) {
+    uint32_t w[8];
+    load_words8(w, a.s, i);
+    a.status_out[i] = response_status(w);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Fixed-base tables: tab[b * 128 + (k - 1)] = k * base_b in affine Niels form.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_build_niels(const uint32_t* __restrict__ base_words, int nbases, ge_niels* __restrict__ tab,
+                              int* __restrict__ ok) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nbases * kNielsEntries) return;
+  const int b = t / kNielsEntries;
+  const int k = t % kNielsEntries + 1;
+  ge_p3 B;
+  const bool dec = ristretto_decode(B, base_words + 8 * b);
+  if (k == 1) ok[b] = dec ? 1 : 0;
+  tab[t] = p3_to_niels(small_mul(B, k));
+}
+
+// ---------------------------------------------------------------------------------------
+// Per-proof verification
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void copy_niels_to_lds(ge_niels* dst, const ge_niels* src, int count) {
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  const int nvec = count * (int)sizeof(ge_niels) / 16;
+  for (int v = threadIdx.x; v < nvec; v += blockDim.x) d[v] = s[v];
+}
+
+__global__ void __launch_bounds__(kVerifyBlock, 2) k_verify_each(VerifyArgs a) {
+  __shared__ ge_niels tab_g[kNielsEntries];
+  __shared__ ge_niels tab_h[kNielsEntries];
+  copy_niels_to_lds(tab_g, a.tab, kNielsEntries);
+  copy_niels_to_lds(tab_h, a.tab + kNielsEntries, kNielsEntries);
+  __syncthreads();
+  const int64_t gtid = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * kVerifyBlock;
+  ge_cached* tab_v = a.scratch + gtid * kCachedEntries;
+  for (int64_t i = gtid; i < a.n; i += stride) {
+    // Rows are read where they are consumed (decode just before each equation) so
+    // only one decoded point is live at a time.
+    uint32_t sw[8], cw[8];
+    load_words8(sw, a.s, i);
+    load_words8(cw, a.c, i);
+    a.status[i] = verify_proof(a.y1 + 8 * i, a.y2 + 8 * i, a.r1 + 8 * i, a.r2 + 8 * i, sw, cw, a.status[i],
+                               tab_g, tab_h, tab_v);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Synthetic prover (input generator): x_i, k_i = wide(ChaCha20(seed_x / seed_k, block i)).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ sc chacha_scalar(const uint32_t key[8], uint64_t counter) {
+  uint32_t blk[16];
+  chacha20_block(blk, key, counter, 0);
+  return sc_reduce_wide(blk);
+}
+
+__global__ void __launch_bounds__(kVerifyBlock, 2) k_prove_points(ProveArgs a) {
+  __shared__ ge_niels tab_g[kNielsEntries];
+  __shared__ ge_niels tab_h[kNielsEntries];
+  copy_niels_to_lds(tab_g, a.tab, kNielsEntries);
+  copy_niels_to_lds(tab_h, a.tab + kNielsEntries, kNielsEntries);
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
+  if (i >= a.n) return;
+  const uint64_t idx = a.first_index + (uint64_t)i;
+  uint32_t d[8], w[8];
+  {
+    const sc x = chacha_scalar(a.seed_x, idx);
+    sc_recode_radix256(d, x.w);
+  }
+  ristretto_encode(w, fixed_base_mul(tab_g, d));
+  store_words8(a.y1, i, w);
+  ristretto_encode(w, fixed_base_mul(tab_h, d));
+  store_words8(a.y2, i, w);
+  {
+    const sc k = chacha_scalar(a.seed_k, idx);
+    sc_recode_radix256(d, k.w);
+  }
+  ristretto_encode(w, fixed_base_mul(tab_g, d));
+  store_words8(a.r1, i, w);
+  ristretto_encode(w, fixed_base_mul(tab_h, d));
+  store_words8(a.r2, i, w);
+}
+
+__global__ void k_prove_response(ProveArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const uint64_t idx = a.first_index + (uint64_t)i;
+  const sc x = chacha_scalar(a.seed_x, idx);
+  const sc k = chacha_scalar(a.seed_k, idx);
+  sc c;
+  load_words8(c.w, a.c, i);
+  const sc s = sc_add(k, sc_mul(c, x));  // s = k + c x   (prover/mod.rs:126-131)
+  store_words8(a.s_out, i, s.w);
+}
+
+// ---------------------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------------------
+hipError_t launch_transcript_prefix(const uint32_t* gh_words, StrobeSnap* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_transcript_prefix, dim3(1), dim3(64), 0, st, gh_words, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_challenge(const ChallengeArgs& a, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  const int64_t blocks = (a.n + kChallengeBlock - 1) / kChallengeBlock;
+  hipLaunchKernelGGL(k_challenge, dim3((unsigned)blocks), dim3(kChallengeBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, hipStream_t st) {
+  const int total = nbases * kNielsEntries;
+  hipLaunchKernelGGL(k_build_niels, dim3((total + 63) / 64), dim3(64), 0, st, base_words, nbases, tab, ok);
+  return hipGetLastError();
+}
+
+hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_verify_each, dim3(grid), dim3(kVerifyBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  const int64_t blocks = (a.n + kVerifyBlock - 1) / kVerifyBlock;
+  hipLaunchKernelGGL(k_prove_points, dim3((unsigned)blocks), dim3(kVerifyBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_prove_response(const ProveArgs& a, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  const int64_t blocks = (a.n + 255) / 256;
+  hipLaunchKernelGGL(k_prove_response, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace cpz

@@ -1,0 +1,519 @@
+// Host runtime behind the C ABI (include/cpz.h): device context, generator-table cache,
+// reusable device buffers, kernel sequencing.  One HIP stream per context.
+//
+// Call sequence for cpz_verify_each (replaces BatchVerifier::verify, batch.rs:171-231):
+//   [cache miss on (g, h)]  k_build_niels(g, h) + k_transcript_prefix(g, h)
+//   k_challenge   -> c_i, response-scalar status          (transcript + gadgets checks)
+//   k_verify_each -> final status                         (decode + two equations)
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/cpz.h"
+#include "cpz_kernels.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define CPZ_HIP(expr)                                                                     \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(CPZ_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));           \
+  } while (0)
+
+const uint8_t kDefaultG[32] = {0xe2, 0xf2, 0xae, 0x0a, 0x6a, 0xbc, 0x4e, 0x71, 0xa8, 0x84, 0xa9,
+                               0x61, 0xc5, 0x00, 0x51, 0x5f, 0x58, 0xe3, 0x0b, 0x6a, 0xa5, 0x82,
+                               0xdd, 0x8d, 0xb6, 0xa6, 0x59, 0x45, 0xe0, 0x8d, 0x2d, 0x76};
+const uint8_t kDefaultH[32] = {0xc8, 0xdb, 0x6f, 0x46, 0xe1, 0xb9, 0x1e, 0x7e, 0x93, 0xac, 0xe6,
+                               0x9e, 0xab, 0x46, 0x97, 0x6e, 0xfe, 0xbe, 0x07, 0xde, 0xaf, 0x5b,
+                               0x9a, 0x2a, 0x74, 0x42, 0xfd, 0x02, 0x36, 0x40, 0x16, 0x23};
+
+// Device buffer that only grows.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) {
+      hipError_t e = hipFree(p);
+      p = nullptr;
+      cap = 0;
+      if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace
+
+struct cpz_ctx {
+  int device = 0;
+  int cus = 0;
+  int verify_blocks_per_cu = 2;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  // (g, h) cache
+  bool have_gh = false;
+  uint8_t gh[64];
+  DevBuf tab;       // 256 ge_niels
+  DevBuf prefix;    // 2 StrobeSnap
+  DevBuf gh_words;  // 16 words
+  DevBuf ok_flags;  // 2 ints
+  // work buffers
+  DevBuf c;         // n x 32
+  DevBuf st;        // n
+  DevBuf scratch;   // grid x 256 x 8 ge_cached
+  // host-API staging
+  DevBuf in[5];
+  DevBuf ctxb, ctxo, ctxp;
+  // optional per-kernel timing
+  bool timing = false;
+  struct Mark { int stage; hipEvent_t a, b; };
+  std::vector<Mark> marks;
+  std::vector<hipEvent_t> free_events;
+};
+
+namespace {
+
+hipEvent_t take_event(cpz_ctx* ctx) {
+  if (!ctx->free_events.empty()) {
+    hipEvent_t e = ctx->free_events.back();
+    ctx->free_events.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// RAII bracket: records events around one kernel launch on `st` when timing is enabled.
+struct StageTimer {
+  cpz_ctx* ctx;
+  int stage;
+  hipStream_t st;
+  hipEvent_t a = nullptr, b = nullptr;
+  StageTimer(cpz_ctx* c, int s, hipStream_t stream) : ctx(c), stage(s), st(stream) {
+    if (ctx->timing) {
+      a = take_event(ctx);
+      b = take_event(ctx);
+      if (a) (void)hipEventRecord(a, st);
+    }
+  }
+  ~StageTimer() {
+    if (a && b) {
+      (void)hipEventRecord(b, st);
+      ctx->marks.push_back({stage, a, b});
+    }
+  }
+};
+
+// Build (or reuse) the fixed-base tables and transcript prefix for (g, h).
+int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32]) {
+  if (ctx->have_gh && std::memcmp(ctx->gh, g, 32) == 0 && std::memcmp(ctx->gh + 32, h, 32) == 0) return CPZ_OK;
+  // Parameters::with_generators (gadgets.rs:77-103): valid, non-identity, distinct.
+  static const uint8_t zero[32] = {0};
+  if (std::memcmp(g, zero, 32) == 0 || std::memcmp(h, zero, 32) == 0)
+    return fail(CPZ_EGENERATOR, "generator cannot be identity");
+  if (std::memcmp(g, h, 32) == 0) return fail(CPZ_EGENERATOR, "generators g and h must be different");
+  CPZ_HIP(ctx->tab.ensure(2 * cpz::kNielsEntries * sizeof(cpz::ge_niels)));
+  CPZ_HIP(ctx->prefix.ensure(2 * sizeof(cpz::StrobeSnap)));
+  CPZ_HIP(ctx->gh_words.ensure(64));
+  CPZ_HIP(ctx->ok_flags.ensure(2 * sizeof(int)));
+  uint8_t both[64];
+  std::memcpy(both, g, 32);
+  std::memcpy(both + 32, h, 32);
+  CPZ_HIP(hipMemcpyAsync(ctx->gh_words.p, both, 64, hipMemcpyHostToDevice, ctx->stream));
+  CPZ_HIP(cpz::launch_build_niels(static_cast<const uint32_t*>(ctx->gh_words.p), 2,
+                                  static_cast<cpz::ge_niels*>(ctx->tab.p), static_cast<int*>(ctx->ok_flags.p),
+                                  ctx->stream));
+  CPZ_HIP(cpz::launch_transcript_prefix(static_cast<const uint32_t*>(ctx->gh_words.p),
+                                        static_cast<cpz::StrobeSnap*>(ctx->prefix.p), ctx->stream));
+  int ok[2] = {0, 0};
+  CPZ_HIP(hipMemcpyAsync(ok, ctx->ok_flags.p, sizeof(ok), hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipStreamSynchronize(ctx->stream));
+  if (!ok[0] || !ok[1]) {
+    ctx->have_gh = false;
+    return fail(CPZ_EGENERATOR, "generator encoding does not decode to a ristretto255 point");
+  }
+  std::memcpy(ctx->gh, both, 64);
+  ctx->have_gh = true;
+  return CPZ_OK;
+}
+
+void words_from_bytes(uint32_t w[16], const uint8_t g[32], const uint8_t h[32]) {
+  std::memcpy(w, g, 32);
+  std::memcpy(w + 8, h, 32);
+}
+
+int verify_grid(cpz_ctx* ctx, size_t n) {
+  const size_t want = (n + cpz::kVerifyBlock - 1) / cpz::kVerifyBlock;
+  const size_t cap = (size_t)ctx->cus * (size_t)ctx->verify_blocks_per_cu;
+  return (int)(want < cap ? want : cap);
+}
+
+int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
+                   const void* s, const void* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
+                   uint8_t* status, hipStream_t st) {
+  CPZ_HIP(ctx->c.ensure(n * 32));
+  const int grid = verify_grid(ctx, n);
+  CPZ_HIP(ctx->scratch.ensure((size_t)grid * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached)));
+  cpz::ChallengeArgs ca;
+  ca.n = (int64_t)n;
+  words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
+  ca.y1 = static_cast<const uint32_t*>(y1);
+  ca.y2 = static_cast<const uint32_t*>(y2);
+  ca.r1 = static_cast<const uint32_t*>(r1);
+  ca.r2 = static_cast<const uint32_t*>(r2);
+  ca.s = static_cast<const uint32_t*>(s);
+  ca.ctx_bytes = static_cast<const uint8_t*>(ctx_bytes);
+  ca.ctx_off = ctx_off;
+  ca.ctx_present = ctx_present;
+  ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->prefix.p);
+  ca.c_out = static_cast<uint32_t*>(ctx->c.p);
+  ca.status_out = status;
+  {
+    StageTimer t(ctx, 0, st);
+    CPZ_HIP(cpz::launch_challenge(ca, st));
+  }
+  cpz::VerifyArgs va;
+  va.n = (int64_t)n;
+  va.y1 = ca.y1;
+  va.y2 = ca.y2;
+  va.r1 = ca.r1;
+  va.r2 = ca.r2;
+  va.s = ca.s;
+  va.c = ca.c_out;
+  va.status = status;
+  va.tab = static_cast<const cpz::ge_niels*>(ctx->tab.p);
+  va.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p);
+  {
+    StageTimer t(ctx, 1, st);
+    CPZ_HIP(cpz::launch_verify_each(va, grid, st));
+  }
+  return CPZ_OK;
+}
+
+// Stage host inputs on the device.  Returns device pointers through out[].
+int stage_inputs(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], int count, const uint8_t* ctx_bytes,
+                 const uint64_t* ctx_off, const uint8_t* ctx_present, const void* dev[5], const void** dcb,
+                 const uint64_t** dco, const uint8_t** dcp) {
+  for (int k = 0; k < count; k++) {
+    CPZ_HIP(ctx->in[k].ensure(n * 32));
+    CPZ_HIP(hipMemcpyAsync(ctx->in[k].p, host[k], n * 32, hipMemcpyHostToDevice, ctx->stream));
+    dev[k] = ctx->in[k].p;
+  }
+  *dcb = nullptr;
+  *dco = nullptr;
+  *dcp = nullptr;
+  if (ctx_off) {
+    const size_t nbytes = ctx_off[n] - ctx_off[0];
+    for (size_t i = 0; i < n; i++)
+      if (ctx_off[i + 1] < ctx_off[i]) return fail(CPZ_EINVAL, "ctx_off must be non-decreasing");
+    std::vector<uint64_t> rel(n + 1);
+    for (size_t i = 0; i <= n; i++) rel[i] = ctx_off[i] - ctx_off[0];
+    CPZ_HIP(ctx->ctxb.ensure(nbytes ? nbytes : 1));
+    CPZ_HIP(ctx->ctxo.ensure((n + 1) * sizeof(uint64_t)));
+    if (nbytes)
+      CPZ_HIP(hipMemcpyAsync(ctx->ctxb.p, ctx_bytes + ctx_off[0], nbytes, hipMemcpyHostToDevice, ctx->stream));
+    CPZ_HIP(hipMemcpyAsync(ctx->ctxo.p, rel.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->stream));
+    // The copies above read pageable host memory synchronously, so rel may be freed.
+    CPZ_HIP(hipStreamSynchronize(ctx->stream));
+    *dcb = ctx->ctxb.p;
+    *dco = static_cast<const uint64_t*>(ctx->ctxo.p);
+    if (ctx_present) {
+      CPZ_HIP(ctx->ctxp.ensure(n));
+      CPZ_HIP(hipMemcpyAsync(ctx->ctxp.p, ctx_present, n, hipMemcpyHostToDevice, ctx->stream));
+      *dcp = static_cast<const uint8_t*>(ctx->ctxp.p);
+    }
+  }
+  return CPZ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cpz_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+const char* cpz_last_error(void) { return g_last_error.c_str(); }
+
+void cpz_default_generators(uint8_t g[32], uint8_t h[32]) {
+  if (g) std::memcpy(g, kDefaultG, 32);
+  if (h) std::memcpy(h, kDefaultH, 32);
+}
+
+int cpz_ctx_create(int device_ordinal, cpz_ctx** out) {
+  if (!out) return fail(CPZ_EINVAL, "out is null");
+  *out = nullptr;
+  int ndev = 0;
+  CPZ_HIP(hipGetDeviceCount(&ndev));
+  if (device_ordinal < 0 || device_ordinal >= ndev) return fail(CPZ_EINVAL, "device ordinal out of range");
+  CPZ_HIP(hipSetDevice(device_ordinal));
+  cpz_ctx* ctx = new (std::nothrow) cpz_ctx();
+  if (!ctx) return fail(CPZ_ENOMEM, "host allocation failed");
+  ctx->device = device_ordinal;
+  hipDeviceProp_t prop;
+  hipError_t e = hipGetDeviceProperties(&prop, device_ordinal);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete ctx;
+    return fail(CPZ_EHIP, std::string("context setup: ") + hipGetErrorString(e));
+  }
+  ctx->cus = prop.multiProcessorCount;
+  *out = ctx;
+  return CPZ_OK;
+}
+
+int cpz_ctx_set_timing(cpz_ctx* ctx, int enable) {
+  if (!ctx) return fail(CPZ_EINVAL, "null context");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  ctx->timing = enable != 0;
+  return CPZ_OK;
+}
+
+int cpz_ctx_stage_times(cpz_ctx* ctx, double ms_out[CPZ_NUM_STAGES], int launches_out[CPZ_NUM_STAGES]) {
+  if (!ctx || !ms_out) return fail(CPZ_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  for (int k = 0; k < CPZ_NUM_STAGES; k++) {
+    ms_out[k] = 0.0;
+    if (launches_out) launches_out[k] = 0;
+  }
+  for (auto& m : ctx->marks) {
+    CPZ_HIP(hipEventSynchronize(m.b));
+    float ms = 0.f;
+    CPZ_HIP(hipEventElapsedTime(&ms, m.a, m.b));
+    if (m.stage >= 0 && m.stage < CPZ_NUM_STAGES) {
+      ms_out[m.stage] += ms;
+      if (launches_out) launches_out[m.stage] += 1;
+    }
+    ctx->free_events.push_back(m.a);
+    ctx->free_events.push_back(m.b);
+  }
+  ctx->marks.clear();
+  return CPZ_OK;
+}
+
+void cpz_ctx_destroy(cpz_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (auto& m : ctx->marks) {
+    (void)hipEventDestroy(m.a);
+    (void)hipEventDestroy(m.b);
+  }
+  for (auto e : ctx->free_events) (void)hipEventDestroy(e);
+  ctx->tab.release();
+  ctx->prefix.release();
+  ctx->gh_words.release();
+  ctx->ok_flags.release();
+  ctx->c.release();
+  ctx->st.release();
+  ctx->scratch.release();
+  for (auto& b : ctx->in) b.release();
+  ctx->ctxb.release();
+  ctx->ctxo.release();
+  ctx->ctxp.release();
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int cpz_verify_each_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, const void* d_y1,
+                           const void* d_y2, const void* d_r1, const void* d_r2, const void* d_s,
+                           const void* d_ctx_bytes, const uint64_t* d_ctx_off, const uint8_t* d_ctx_present,
+                           void* d_status_out, void* stream) {
+  if (!ctx || !g || !h) return fail(CPZ_EINVAL, "null context or generators");
+  if (n == 0) return fail(CPZ_EEMPTY, "Cannot verify empty batch");
+  if (!d_y1 || !d_y2 || !d_r1 || !d_r2 || !d_s || !d_status_out) return fail(CPZ_EINVAL, "null input pointer");
+  if (!aligned16(d_y1) || !aligned16(d_y2) || !aligned16(d_r1) || !aligned16(d_r2) || !aligned16(d_s))
+    return fail(CPZ_EINVAL, "device inputs must be 16-byte aligned");
+  if (d_ctx_off && !d_ctx_bytes) return fail(CPZ_EINVAL, "ctx_off given without ctx_bytes");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  int rc = ensure_generators(ctx, g, h);
+  if (rc) return rc;
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  return enqueue_verify(ctx, n, d_y1, d_y2, d_r1, d_r2, d_s, d_ctx_bytes, d_ctx_off, d_ctx_present,
+                        static_cast<uint8_t*>(d_status_out), st);
+}
+
+int cpz_verify_each(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, const uint8_t* y1,
+                    const uint8_t* y2, const uint8_t* r1, const uint8_t* r2, const uint8_t* s,
+                    const uint8_t* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
+                    uint8_t* status_out) {
+  if (!ctx || !g || !h) return fail(CPZ_EINVAL, "null context or generators");
+  if (n == 0) return fail(CPZ_EEMPTY, "Cannot verify empty batch");
+  if (!y1 || !y2 || !r1 || !r2 || !s || !status_out) return fail(CPZ_EINVAL, "null input pointer");
+  if (ctx_off && !ctx_bytes && ctx_off[n] != ctx_off[0]) return fail(CPZ_EINVAL, "ctx_off given without ctx_bytes");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  int rc = ensure_generators(ctx, g, h);
+  if (rc) return rc;
+  const uint8_t* host[5] = {y1, y2, r1, r2, s};
+  const void* dev[5];
+  const void* dcb;
+  const uint64_t* dco;
+  const uint8_t* dcp;
+  rc = stage_inputs(ctx, n, host, 5, ctx_bytes, ctx_off, ctx_present, dev, &dcb, &dco, &dcp);
+  if (rc) return rc;
+  CPZ_HIP(ctx->st.ensure(n));
+  rc = enqueue_verify(ctx, n, dev[0], dev[1], dev[2], dev[3], dev[4], dcb, dco, dcp,
+                      static_cast<uint8_t*>(ctx->st.p), ctx->stream);
+  if (rc) return rc;
+  CPZ_HIP(hipMemcpyAsync(status_out, ctx->st.p, n, hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipStreamSynchronize(ctx->stream));
+  return CPZ_OK;
+}
+
+int cpz_challenges(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, const uint8_t* y1,
+                   const uint8_t* y2, const uint8_t* r1, const uint8_t* r2, const uint8_t* ctx_bytes,
+                   const uint64_t* ctx_off, const uint8_t* ctx_present, uint8_t* c_out) {
+  if (!ctx || !g || !h) return fail(CPZ_EINVAL, "null context or generators");
+  if (n == 0) return fail(CPZ_EEMPTY, "empty input");
+  if (!y1 || !y2 || !r1 || !r2 || !c_out) return fail(CPZ_EINVAL, "null input pointer");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  int rc = ensure_generators(ctx, g, h);
+  if (rc) return rc;
+  const uint8_t* host[5] = {y1, y2, r1, r2, nullptr};
+  const void* dev[5];
+  const void* dcb;
+  const uint64_t* dco;
+  const uint8_t* dcp;
+  rc = stage_inputs(ctx, n, host, 4, ctx_bytes, ctx_off, ctx_present, dev, &dcb, &dco, &dcp);
+  if (rc) return rc;
+  CPZ_HIP(ctx->c.ensure(n * 32));
+  cpz::ChallengeArgs ca;
+  ca.n = (int64_t)n;
+  words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
+  ca.y1 = static_cast<const uint32_t*>(dev[0]);
+  ca.y2 = static_cast<const uint32_t*>(dev[1]);
+  ca.r1 = static_cast<const uint32_t*>(dev[2]);
+  ca.r2 = static_cast<const uint32_t*>(dev[3]);
+  ca.s = nullptr;
+  ca.ctx_bytes = static_cast<const uint8_t*>(dcb);
+  ca.ctx_off = dco;
+  ca.ctx_present = dcp;
+  ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->prefix.p);
+  ca.c_out = static_cast<uint32_t*>(ctx->c.p);
+  ca.status_out = nullptr;
+  CPZ_HIP(cpz::launch_challenge(ca, ctx->stream));
+  CPZ_HIP(hipMemcpyAsync(c_out, ctx->c.p, n * 32, hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipStreamSynchronize(ctx->stream));
+  return CPZ_OK;
+}
+
+int cpz_prove_synthetic_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                               uint64_t first_index, const uint8_t seed_x[32], const uint8_t seed_k[32],
+                               const void* d_ctx_bytes, const uint64_t* d_ctx_off, const uint8_t* d_ctx_present,
+                               void* d_y1, void* d_y2, void* d_r1, void* d_r2, void* d_s, void* stream) {
+  if (!ctx || !g || !h || !seed_x || !seed_k) return fail(CPZ_EINVAL, "null argument");
+  if (n == 0) return fail(CPZ_EEMPTY, "empty input");
+  if (!d_y1 || !d_y2 || !d_r1 || !d_r2 || !d_s) return fail(CPZ_EINVAL, "null output pointer");
+  if (!aligned16(d_y1) || !aligned16(d_y2) || !aligned16(d_r1) || !aligned16(d_r2) || !aligned16(d_s))
+    return fail(CPZ_EINVAL, "device outputs must be 16-byte aligned");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  int rc = ensure_generators(ctx, g, h);
+  if (rc) return rc;
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  CPZ_HIP(ctx->c.ensure(n * 32));
+  cpz::ProveArgs pa;
+  pa.n = (int64_t)n;
+  pa.first_index = first_index;
+  std::memcpy(pa.seed_x, seed_x, 32);
+  std::memcpy(pa.seed_k, seed_k, 32);
+  pa.tab = static_cast<const cpz::ge_niels*>(ctx->tab.p);
+  pa.y1 = static_cast<uint32_t*>(d_y1);
+  pa.y2 = static_cast<uint32_t*>(d_y2);
+  pa.r1 = static_cast<uint32_t*>(d_r1);
+  pa.r2 = static_cast<uint32_t*>(d_r2);
+  pa.c = static_cast<const uint32_t*>(ctx->c.p);
+  pa.s_out = static_cast<uint32_t*>(d_s);
+  CPZ_HIP(cpz::launch_prove_points(pa, st));
+  cpz::ChallengeArgs ca;
+  ca.n = (int64_t)n;
+  words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
+  ca.y1 = pa.y1;
+  ca.y2 = pa.y2;
+  ca.r1 = pa.r1;
+  ca.r2 = pa.r2;
+  ca.s = nullptr;
+  ca.ctx_bytes = static_cast<const uint8_t*>(d_ctx_bytes);
+  ca.ctx_off = d_ctx_off;
+  ca.ctx_present = d_ctx_present;
+  ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->prefix.p);
+  ca.c_out = static_cast<uint32_t*>(ctx->c.p);
+  ca.status_out = nullptr;
+  CPZ_HIP(cpz::launch_challenge(ca, st));
+  CPZ_HIP(cpz::launch_prove_response(pa, st));
+  return CPZ_OK;
+}
+
+int cpz_prove_synthetic(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, uint64_t first_index,
+                        const uint8_t seed_x[32], const uint8_t seed_k[32], const uint8_t* ctx_bytes,
+                        const uint64_t* ctx_off, const uint8_t* ctx_present, uint8_t* y1, uint8_t* y2,
+                        uint8_t* r1, uint8_t* r2, uint8_t* s) {
+  if (!ctx) return fail(CPZ_EINVAL, "null context");
+  if (n == 0) return fail(CPZ_EEMPTY, "empty input");
+  if (!y1 || !y2 || !r1 || !r2 || !s) return fail(CPZ_EINVAL, "null output pointer");
+  void* outs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  for (int k = 0; k < 5; k++) {
+    hipError_t e = hipMalloc(&outs[k], n * 32);
+    if (e != hipSuccess) {
+      for (int j = 0; j < k; j++) (void)hipFree(outs[j]);
+      return fail(CPZ_ENOMEM, "device allocation failed");
+    }
+  }
+  const void* dcb = nullptr;
+  const uint64_t* dco = nullptr;
+  const uint8_t* dcp = nullptr;
+  int rc = CPZ_OK;
+  {
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    (void)hipSetDevice(ctx->device);
+    const uint8_t* host[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    const void* dev[5];
+    rc = stage_inputs(ctx, n, host, 0, ctx_bytes, ctx_off, ctx_present, dev, &dcb, &dco, &dcp);
+  }
+  if (rc == CPZ_OK)
+    rc = cpz_prove_synthetic_device(ctx, g, h, n, first_index, seed_x, seed_k, dcb, dco, dcp, outs[0], outs[1],
+                                    outs[2], outs[3], outs[4], nullptr);
+  if (rc == CPZ_OK) {
+    uint8_t* hosts[5] = {y1, y2, r1, r2, s};
+    for (int k = 0; k < 5 && rc == CPZ_OK; k++) {
+      hipError_t e = hipMemcpyAsync(hosts[k], outs[k], n * 32, hipMemcpyDeviceToHost, ctx->stream);
+      if (e != hipSuccess) rc = fail(CPZ_EHIP, hipGetErrorString(e));
+    }
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (rc == CPZ_OK && e != hipSuccess) rc = fail(CPZ_EHIP, hipGetErrorString(e));
+  }
+  for (int k = 0; k < 5; k++) (void)hipFree(outs[k]);
+  return rc;
+}
+
+}  // extern "C"

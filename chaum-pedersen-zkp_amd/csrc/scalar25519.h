@@ -1,0 +1,208 @@
+// Scalars modulo l = 2^252 + 27742317777372353535851937790883648493 (8 x u32, little-endian).
+//
+// Replaces curve25519-dalek 4.1.3's Scalar as reached from the reference:
+//   Scalar::from_canonical_bytes   (ristretto.rs:94-112)  -> sc_is_canonical
+//   from_bytes_mod_order_wide      (ristretto.rs:146-150, transcript.rs:67-71) -> sc_reduce_wide
+//   scalar_mul_scalar / scalar_add (ristretto.rs:198-200, prover/mod.rs:126-131) -> sc_mul / sc_add
+//   scalar_is_zero                 (ristretto.rs:219-221) -> sc_is_zero
+// plus the signed-digit recodings the scalar-multiplication loops consume.
+// Reduction is Barrett (HAC 14.42, b = 2^32, k = 8, mu = floor(2^512 / l)); every
+// 32x32 partial product is one v_mad_u64_u32.
+#pragma once
+#include "fe25519.h"
+
+namespace cpz {
+
+struct sc {
+  uint32_t w[8];
+};
+
+CPZ_HD uint32_t SC_L(int i) {
+  const uint32_t l[8] = {0x5cf5d3edu, 0x5812631au, 0xa2f79cd6u, 0x14def9deu,
+                         0x00000000u, 0x00000000u, 0x00000000u, 0x10000000u};
+  return l[i];
+}
+
+CPZ_HD uint32_t SC_MU(int i) {
+  const uint32_t mu[9] = {0x0a2c131bu, 0xed9ce5a3u, 0x086329a7u, 0x2106215du, 0xffffffebu,
+                          0xffffffffu, 0xffffffffu, 0xffffffffu, 0x0000000fu};
+  return mu[i];
+}
+
+// a >= l ?
+CPZ_HD bool sc_geq_l9(const uint32_t a[9]) {
+  if (a[8] != 0) return true;
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t d = (uint64_t)a[i] - SC_L(i) - borrow;
+    borrow = (uint32_t)(d >> 63);
+  }
+  return borrow == 0;
+}
+
+CPZ_HD void sc_sub_l9(uint32_t a[9]) {
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint64_t d = (uint64_t)a[i] - (i < 8 ? SC_L(i) : 0u) - borrow;
+    a[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+}
+
+// s < l ?  (Scalar::from_canonical_bytes accepts exactly these.)
+CPZ_HD bool sc_is_canonical(const uint32_t s[8]) {
+  uint32_t t[9];
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = s[i];
+  t[8] = 0;
+  return !sc_geq_l9(t);
+}
+
+CPZ_HD bool sc_is_zero(const uint32_t s[8]) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) acc |= s[i];
+  return acc == 0;
+}
+
+// r = x mod l for a 512-bit x (16 words).
+CPZ_HD sc sc_reduce_wide(const uint32_t x[16]) {
+  // q1 = x >> 224 (9 words); q3 = (q1 * mu) >> 288.
+  uint32_t q2[18];
+#pragma unroll
+  for (int i = 0; i < 18; i++) q2[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+      const uint64_t t = (uint64_t)x[7 + i] * SC_MU(j) + q2[i + j] + carry;
+      q2[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    q2[i + 9] = (uint32_t)carry;
+  }
+  // r2 = (q3 * l) mod 2^288.
+  uint32_t r2[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) r2[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if (i + j < 9) {
+        const uint64_t t = (uint64_t)q2[9 + i] * SC_L(j) + r2[i + j] + carry;
+        r2[i + j] = (uint32_t)t;
+        carry = t >> 32;
+      }
+    }
+    if (i + 8 < 9) r2[i + 8] = (uint32_t)(r2[i + 8] + carry);
+  }
+  // r = (x mod 2^288) - r2 (mod 2^288); then at most two subtractions of l.
+  uint32_t r[9];
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint64_t d = (uint64_t)x[i] - r2[i] - borrow;
+    r[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  if (sc_geq_l9(r)) sc_sub_l9(r);
+  if (sc_geq_l9(r)) sc_sub_l9(r);
+  sc out;
+#pragma unroll
+  for (int i = 0; i < 8; i++) out.w[i] = r[i];
+  return out;
+}
+
+// (a * b) mod l.
+CPZ_HD sc sc_mul(const sc& a, const sc& b) {
+  uint32_t p[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) p[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint64_t t = (uint64_t)a.w[i] * b.w[j] + p[i + j] + carry;
+      p[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    p[i + 8] = (uint32_t)carry;
+  }
+  return sc_reduce_wide(p);
+}
+
+// (a + b) mod l, a and b canonical.
+CPZ_HD sc sc_add(const sc& a, const sc& b) {
+  uint32_t t[9];
+  uint64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t s = (uint64_t)a.w[i] + b.w[i] + carry;
+    t[i] = (uint32_t)s;
+    carry = s >> 32;
+  }
+  t[8] = (uint32_t)carry;
+  if (sc_geq_l9(t)) sc_sub_l9(t);
+  sc out;
+#pragma unroll
+  for (int i = 0; i < 8; i++) out.w[i] = t[i];
+  return out;
+}
+
+// (l - a) mod l.
+CPZ_HD sc sc_neg(const sc& a) {
+  if (sc_is_zero(a.w)) return a;
+  sc out;
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t d = (uint64_t)SC_L(i) - a.w[i] - borrow;
+    out.w[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  return out;
+}
+
+// Signed radix-16 recoding of a scalar < 2^255: 64 digits in [-8, 7], packed as 4-bit
+// two's-complement nibbles, digit i in bits 4(i%8) of word i/8.
+CPZ_HD void sc_recode_radix16(uint32_t out[8], const uint32_t s[8]) {
+  int32_t carry = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+      const int32_t n = (int32_t)((s[j] >> (4 * m)) & 15u) + carry;
+      carry = (n + 8) >> 4;
+      const int32_t d = n - (carry << 4);
+      packed |= ((uint32_t)d & 15u) << (4 * m);
+    }
+    out[j] = packed;
+  }
+}
+
+// Signed radix-256 recoding of a scalar < 2^253: 32 digits in [-128, 127] packed as
+// bytes, digit i in byte i%4 of word i/4.
+CPZ_HD void sc_recode_radix256(uint32_t out[8], const uint32_t s[8]) {
+  int32_t carry = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      const int32_t n = (int32_t)((s[j] >> (8 * m)) & 255u) + carry;
+      carry = (n + 128) >> 8;
+      const int32_t d = n - (carry << 8);
+      packed |= ((uint32_t)d & 255u) << (8 * m);
+    }
+    out[j] = packed;
+  }
+}
+
+}  // namespace cpz

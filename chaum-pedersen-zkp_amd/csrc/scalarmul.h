@@ -1,0 +1,147 @@
+// Variable-time scalar multiplication loops (verification inputs are public, so
+// data-dependent digits are allowed; SIMT divergence is avoided by using fixed windows:
+// every lane adds at every window, digit 0 adds the identity).
+//
+// Replaces the reference's Ristretto255::scalar_mul (ristretto.rs:153-155) as used in
+// verify_one (batch.rs:216-222): instead of four independent constant-time
+// multiplications, each equation is one Straus double-scalar loop
+//     Q = [s] B + [c] V        (B = g or h fixed, V = -y1 or -y2 per proof)
+// whose result is compared with r by ristretto equality.
+#pragma once
+#include "ristretto.h"
+
+namespace cpz {
+
+constexpr int kTableV = 8;     // cached multiples 1..8 of a variable base (radix-16 digits)
+constexpr int kTableB = 128;   // Niels multiples 1..128 of a fixed base (radix-256 digits)
+
+CPZ_HD ge_cached cached_load(const ge_cached* p) {
+  ge_cached r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint4* s = reinterpret_cast<const uint4*>(p);
+  uint4* d = reinterpret_cast<uint4*>(&r);
+#pragma unroll
+  for (int v = 0; v < (int)(sizeof(ge_cached) / 16); v++) d[v] = s[v];
+#else
+  r = *p;
+#endif
+  return r;
+}
+
+CPZ_HD void cached_store(ge_cached* p, const ge_cached& c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint4* s = reinterpret_cast<const uint4*>(&c);
+  uint4* d = reinterpret_cast<uint4*>(p);
+#pragma unroll
+  for (int v = 0; v < (int)(sizeof(ge_cached) / 16); v++) d[v] = s[v];
+#else
+  *p = c;
+#endif
+}
+
+CPZ_HD ge_niels niels_lookup(const ge_niels* tab, int digit) {
+  const int mag = digit < 0 ? -digit : digit;
+  const ge_niels e = tab[(mag == 0 ? 1 : mag) - 1];
+  const ge_niels r = mag == 0 ? ge_niels_identity() : e;
+  return ge_niels_cneg(r, digit < 0);
+}
+
+CPZ_HD ge_cached cached_lookup(const ge_cached* tab, int digit) {
+  const int mag = digit < 0 ? -digit : digit;
+  const ge_cached e = cached_load(tab + (mag == 0 ? 1 : mag) - 1);
+  const ge_cached r = mag == 0 ? ge_cached_identity() : e;
+  return ge_cached_cneg(r, digit < 0);
+}
+
+// Four doublings of a pending completed point.
+CPZ_HD ge_p1p1 dbl4(const ge_p1p1& cur) {
+  ge_p1p1 t = cur;
+#pragma unroll 1
+  for (int d = 0; d < 4; d++) t = p2_dbl(p1p1_to_p2(t));
+  return t;
+}
+
+CPZ_HD ge_p1p1 p1p1_identity() {
+  ge_p1p1 cur;
+  cur.X = fe_zero(); cur.Y = fe_one(); cur.Z = fe_one(); cur.T = fe_one();
+  return cur;
+}
+
+// Writes the cached multiples 1..8 of P (1 doubling + 6 additions).
+CPZ_HD void build_cached_table(ge_cached* tab, const ge_p3& P) {
+  const ge_cached c1 = p3_to_cached(P);
+  cached_store(tab, c1);
+  ge_p3 acc = p1p1_to_p3(p3_dbl(P));
+  cached_store(tab + 1, p3_to_cached(acc));
+#pragma unroll 1
+  for (int k = 2; k < kTableV; k++) {
+    acc = p1p1_to_p3(ge_add_cached(acc, c1));
+    cached_store(tab + k, p3_to_cached(acc));
+  }
+}
+
+// Q = [s] B + [c] V.  tab_v: cached multiples 1..8 of V; tab_b: Niels multiples 1..128
+// of B; cdig: radix-16 signed digits of c; sdig: radix-256 signed digits of s.
+// 63 x 4 doublings, 64 cached additions, 32 Niels additions.
+CPZ_HD ge_p3 straus_vartime(const ge_cached* tab_v, const ge_niels* tab_b, const uint32_t cdig_in[8],
+                            const uint32_t sdig_in[8]) {
+  uint32_t cdig[8], sdig[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) { cdig[j] = cdig_in[j]; sdig[j] = sdig_in[j]; }
+  ge_p1p1 cur = p1p1_identity();
+#pragma unroll 1
+  for (int j = 7; j >= 0; j--) {
+    const uint32_t wc = cdig[7], wg = sdig[7];
+#pragma unroll
+    for (int t = 7; t > 0; t--) { cdig[t] = cdig[t - 1]; sdig[t] = sdig[t - 1]; }
+#pragma unroll 1
+    for (int m = 7; m >= 0; m--) {
+      const int dc = ((int32_t)(wc << (28 - 4 * m))) >> 28;
+      const ge_cached ev = cached_lookup(tab_v, dc);
+      if (j != 7 || m != 7) cur = dbl4(cur);
+      cur = ge_add_cached(p1p1_to_p3(cur), ev);
+      if ((m & 1) == 0) {
+        const int dg = ((int32_t)(wg << (24 - 8 * (m >> 1)))) >> 24;
+        cur = ge_add_niels(p1p1_to_p3(cur), niels_lookup(tab_b, dg));
+      }
+    }
+  }
+  return p1p1_to_p3(cur);
+}
+
+// [s] B by Horner over radix-256 signed digits (prover path).
+CPZ_HD ge_p3 fixed_base_mul(const ge_niels* tab_b, const uint32_t sdig_in[8]) {
+  uint32_t sdig[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) sdig[j] = sdig_in[j];
+  ge_p1p1 cur = p1p1_identity();
+#pragma unroll 1
+  for (int j = 7; j >= 0; j--) {
+    const uint32_t wg = sdig[7];
+#pragma unroll
+    for (int t = 7; t > 0; t--) sdig[t] = sdig[t - 1];
+#pragma unroll 1
+    for (int m = 3; m >= 0; m--) {
+      if (j != 7 || m != 3) {
+        cur = dbl4(cur);
+        cur = dbl4(cur);
+      }
+      const int dg = ((int32_t)(wg << (24 - 8 * m))) >> 24;
+      cur = ge_add_niels(p1p1_to_p3(cur), niels_lookup(tab_b, dg));
+    }
+  }
+  return p1p1_to_p3(cur);
+}
+
+// k * B for 1 <= k <= 255 by double-and-add (table construction).
+CPZ_HD ge_p3 small_mul(const ge_p3& B, int k) {
+  ge_p3 acc = ge_identity();
+#pragma unroll 1
+  for (int bit = 7; bit >= 0; bit--) {
+    acc = p1p1_to_p3(p3_dbl(acc));
+    if ((k >> bit) & 1) acc = ge_add(acc, B);
+  }
+  return acc;
+}
+
+}  // namespace cpz

@@ -1,0 +1,116 @@
+/*
+ * cpz.h -- C ABI of the MI355X-native Chaum-Pedersen / ristretto255 batch verifier.
+ *
+ * Drop-in boundary for the reference's `verifier::batch::BatchVerifier`
+ * (kobby-pentangeli/chaum-pedersen-zkp, src/verifier/batch.rs).  Plain C: caller-owned
+ * buffers, structure-of-arrays inputs, no callbacks, no torch/HIP types in signatures.
+ * Every entry point returns an int status (CPZ_OK = 0, < 0 on error) and never aborts;
+ * cpz_last_error() describes the most recent failure on the calling thread.
+ *
+ * Input layout (per proof i, each field a 32-byte little-endian encoding):
+ *   y1[i], y2[i]  Statement (gadgets.rs:177-239), compressed ristretto255 points
+ *   r1[i], r2[i]  Commitment (gadgets.rs:245-265), compressed ristretto255 points
+ *   s[i]          Response (gadgets.rs:272-286), canonical scalar bytes
+ * i.e. the bytes [5..37), [41..73), [77..109) of `Proof::to_bytes` (gadgets.rs:343-361)
+ * plus the statement encodings.  Optional per-proof transcript contexts
+ * (`add_with_context`, batch.rs:144-168) are given as one byte blob plus n + 1 offsets;
+ * ctx_present distinguishes Some(b"") from None (NULL = every entry Some).
+ *
+ * Per-proof status codes (uint8):
+ *   CPZ_STATUS_OK               Ok(())
+ *   CPZ_STATUS_EQ_FAIL          Err(InvalidParams("Proof verification failed"))  batch.rs:224-228
+ *   CPZ_STATUS_BAD_POINT        a point fails to decode (InvalidGroupElement)    ristretto.rs:120-138
+ *   CPZ_STATUS_BAD_SCALAR       s is not canonical (InvalidScalar)                ristretto.rs:94-112
+ *   CPZ_STATUS_IDENTITY_OR_ZERO identity commitment or zero s (InvalidParams)     gadgets.rs:474-482
+ * Codes 2-4 are rejected by the reference before an entry can reach the batch
+ * (`Proof::from_bytes`, service.rs:501-507); the bulk path reports them per entry.
+ */
+#ifndef CPZ_H_
+#define CPZ_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CPZ_OK 0
+#define CPZ_EINVAL (-1)     /* bad argument (null pointer, n == 0 where forbidden, misalignment) */
+#define CPZ_EHIP (-2)       /* HIP runtime / kernel failure */
+#define CPZ_ENOMEM (-3)     /* device or host allocation failed */
+#define CPZ_EGENERATOR (-4) /* g or h does not decode to a valid, non-identity, distinct pair */
+#define CPZ_EEMPTY (-5)     /* "Cannot verify empty batch" (batch.rs:172-176) */
+
+#define CPZ_STATUS_OK 0
+#define CPZ_STATUS_EQ_FAIL 1
+#define CPZ_STATUS_BAD_POINT 2
+#define CPZ_STATUS_BAD_SCALAR 3
+#define CPZ_STATUS_IDENTITY_OR_ZERO 4
+
+typedef struct cpz_ctx cpz_ctx;
+
+/* Number of visible GPUs (0 when none / no HIP runtime). */
+int cpz_device_count(void);
+
+/* Create a verifier context bound to one GPU (one HIP stream, cached generator tables,
+ * reusable device buffers).  Contexts serialise concurrent calls internally. */
+int cpz_ctx_create(int device_ordinal, cpz_ctx **out);
+void cpz_ctx_destroy(cpz_ctx *ctx);
+
+/* Thread-local description of the last error returned on this thread. */
+const char *cpz_last_error(void);
+
+/* Encodings of the default generators: g = ristretto255 basepoint, h = hash-to-group of
+ * SHA-512("chaum-pedersen-zkp-v1.0.0-generator-h")   (ristretto.rs:27, 79-91). */
+void cpz_default_generators(uint8_t g[32], uint8_t h[32]);
+
+/* Per-proof verification of n proofs under generators (g, h).
+ * Replaces BatchVerifier::verify (batch.rs:171-183) / verify_one (batch.rs:185-231):
+ * status_out[i] is the outcome the reference reports for entry i.  Host buffers.
+ * n == 0 -> CPZ_EEMPTY. */
+int cpz_verify_each(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                    const uint8_t *y1, const uint8_t *y2, const uint8_t *r1, const uint8_t *r2,
+                    const uint8_t *s, const uint8_t *ctx_bytes, const uint64_t *ctx_off,
+                    const uint8_t *ctx_present, uint8_t *status_out);
+
+/* Same with device-resident, 16-byte aligned inputs/outputs, enqueued on `stream`
+ * (a hipStream_t, or NULL for the context's own stream).  Does not synchronise. */
+int cpz_verify_each_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                           const void *d_y1, const void *d_y2, const void *d_r1, const void *d_r2,
+                           const void *d_s, const void *d_ctx_bytes, const uint64_t *d_ctx_off,
+                           const uint8_t *d_ctx_present, void *d_status_out, void *stream);
+
+/* Fiat-Shamir challenges c_i (32-byte canonical scalars), bit-exact with
+ * Transcript::challenge_scalar (transcript.rs:67-71) as built by batch.rs:188-206. */
+int cpz_challenges(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                   const uint8_t *y1, const uint8_t *y2, const uint8_t *r1, const uint8_t *r2,
+                   const uint8_t *ctx_bytes, const uint64_t *ctx_off, const uint8_t *ctx_present,
+                   uint8_t *c_out);
+
+/* Synthetic input generator (Prover::prove_with_transcript, prover/mod.rs:86-131):
+ * witness x_i and nonce k_i = from_bytes_mod_order_wide(ChaCha20(seed_x / seed_k, block
+ * first_index + i)); writes y1 = x g, y2 = x h, r1 = k g, r2 = k h, s = k + c x. */
+int cpz_prove_synthetic(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                        uint64_t first_index, const uint8_t seed_x[32], const uint8_t seed_k[32],
+                        const uint8_t *ctx_bytes, const uint64_t *ctx_off, const uint8_t *ctx_present,
+                        uint8_t *y1, uint8_t *y2, uint8_t *r1, uint8_t *r2, uint8_t *s);
+int cpz_prove_synthetic_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                               uint64_t first_index, const uint8_t seed_x[32], const uint8_t seed_k[32],
+                               const void *d_ctx_bytes, const uint64_t *d_ctx_off,
+                               const uint8_t *d_ctx_present, void *d_y1, void *d_y2, void *d_r1,
+                               void *d_r2, void *d_s, void *stream);
+
+/* Per-kernel timing (HIP events recorded on the launch stream around every kernel).
+ * Stages: 0 = k_challenge, 1 = k_verify_each, 2 = RLC decode/weights, 3 = RLC MSM,
+ * 4 = fallback.  cpz_ctx_stage_times synchronises, writes the summed milliseconds and
+ * launch counts per stage since the last call, and resets them. */
+#define CPZ_NUM_STAGES 8
+int cpz_ctx_set_timing(cpz_ctx *ctx, int enable);
+int cpz_ctx_stage_times(cpz_ctx *ctx, double ms_out[CPZ_NUM_STAGES], int launches_out[CPZ_NUM_STAGES]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CPZ_H_ */

@@ -1,0 +1,178 @@
+"""CPU unit tests of the device library (csrc/*.h) compiled for the host with limb-bound
+assertions (tests/native/hostlib.cpp), against the Python oracle and the golden fixtures.
+
+This exercises the exact arithmetic the gfx950 kernels run (same source), so a failure
+here localises a bug before any GPU time is spent.  Test infrastructure only.
+"""
+import ctypes
+import os
+import random
+
+import pytest
+
+import pyoracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P, L = O.P, O.L
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("build_native", os.path.join(ROOT, "chaum-pedersen-zkp_amd", "build_native.py"))
+    bn = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bn)
+    return ctypes.CDLL(bn.build_hosttest())
+
+
+def fb(x):
+    return (x % P).to_bytes(32, "little")
+
+
+def fi(b):
+    return int.from_bytes(b, "little")
+
+
+def buf(n=32):
+    return ctypes.create_string_buffer(n)
+
+
+EDGE = [0, 1, 2, 19, P - 1, P - 2, 2**255 - 20, 2**254, 2**26, 2**25 - 1, (2**255 - 19) // 2]
+
+
+def test_field_ops_random_and_edges(lib):
+    rnd = random.Random(1)
+    out = buf()
+    vals = EDGE + [rnd.randrange(P) for _ in range(1500)]
+    for i, a in enumerate(vals):
+        b = vals[(i * 7 + 3) % len(vals)]
+        lib.cpzt_fe_mul(out, fb(a), fb(b)); assert fi(out.raw) == a * b % P
+        lib.cpzt_fe_sq(out, fb(a)); assert fi(out.raw) == a * a % P
+        lib.cpzt_fe_sq2(out, fb(a)); assert fi(out.raw) == 2 * a * a % P
+        lib.cpzt_fe_sub(out, fb(a), fb(b)); assert fi(out.raw) == (a - b) % P
+        lib.cpzt_fe_add(out, fb(a), fb(b)); assert fi(out.raw) == (a + b) % P
+
+
+def test_field_unreduced_inputs(lib):
+    # fe_fromwords ignores bit 255 and accepts values in [p, 2^255): tobytes must reduce.
+    out = buf()
+    for a in [P, P + 1, P + 18, 2**255 - 1, 2**256 - 1]:
+        lib.cpzt_fe_mul(out, a.to_bytes(32, "little"), fb(1))
+        assert fi(out.raw) == (a & (2**255 - 1)) % P
+
+
+def test_invert_pow_sqrt_ratio(lib):
+    rnd = random.Random(2)
+    out = buf()
+    for _ in range(40):
+        a = rnd.randrange(1, P)
+        lib.cpzt_fe_invert(out, fb(a)); assert fi(out.raw) == pow(a, P - 2, P)
+        lib.cpzt_fe_pow22523(out, fb(a)); assert fi(out.raw) == pow(a, (P - 5) // 8, P)
+        u, v = rnd.randrange(P), rnd.randrange(1, P)
+        sq = lib.cpzt_fe_sqrt_ratio(out, fb(u), fb(v))
+        assert (bool(sq), fi(out.raw)) == O.sqrt_ratio_m1(u, v)
+    # u = 0, v = 0 edge cases (RFC 9496: (True, 0) and (False, 0))
+    assert lib.cpzt_fe_sqrt_ratio(out, fb(0), fb(5)) == 1 and fi(out.raw) == 0
+    assert lib.cpzt_fe_sqrt_ratio(out, fb(3), fb(0)) == 0 and fi(out.raw) == 0
+
+
+def test_ristretto_decode_encode(lib, golden):
+    rnd = random.Random(3)
+    out = buf()
+    for enc in golden["rfc9496_multiples"]:
+        b = bytes.fromhex(enc)
+        assert lib.cpzt_decode_encode(out, b) == 1 and out.raw == b
+    for enc in golden["rfc9496_bad"]:
+        assert lib.cpzt_decode_encode(out, bytes.fromhex(enc)) == 0
+    for _ in range(400):
+        b = bytes(rnd.getrandbits(8) for _ in range(32))
+        ok = lib.cpzt_decode_encode(out, b)
+        assert (ok == 1) == (O.ristretto_decode(b) is not None)
+        if ok:
+            assert out.raw == b
+
+
+def test_point_ops(lib):
+    rnd = random.Random(4)
+    s_, d_, n_ = buf(), buf(), buf()
+    for _ in range(25):
+        A = O.pt_mul(O.BASEPOINT, rnd.randrange(L))
+        B = O.pt_mul(O.generator_h(), rnd.randrange(L))
+        ea, eb = O.ristretto_encode(A), O.ristretto_encode(B)
+        assert lib.cpzt_point_ops(s_, d_, n_, ea, eb) == 1
+        assert s_.raw == O.ristretto_encode(O.pt_add(A, B))
+        assert d_.raw == O.ristretto_encode(O.pt_add(A, A))
+        assert n_.raw == O.ristretto_encode(O.pt_neg(A))
+        assert lib.cpzt_points_equal(ea, ea) == 1 and lib.cpzt_points_equal(ea, eb) == 0
+
+
+def test_straus_and_fixed_base(lib):
+    rnd = random.Random(5)
+    out, out2 = buf(), buf()
+    scal = [(0, 0), (L - 1, L - 1), (1, 0), (0, 1), (2**252, 2**252 - 1), (128, 8), (L - 128, L - 8)]
+    scal += [(rnd.randrange(L), rnd.randrange(L)) for _ in range(12)]
+    for i, (s, c) in enumerate(scal):
+        base = O.generator_h() if i % 2 else O.BASEPOINT
+        V = O.pt_mul(O.BASEPOINT, rnd.randrange(1, L))
+        assert lib.cpzt_straus(out, out2, O.ristretto_encode(base), O.ristretto_encode(V), s.to_bytes(32, "little"),
+                               c.to_bytes(32, "little"))
+        assert out.raw == O.ristretto_encode(O.pt_add(O.pt_mul(base, s), O.pt_mul(V, c)))
+        assert out2.raw == O.ristretto_encode(O.pt_mul(base, s))
+
+
+def test_scalars(lib):
+    rnd = random.Random(6)
+    out = buf()
+    for i in range(400):
+        x = bytes(rnd.getrandbits(8) for _ in range(64)) if i else b"\xff" * 64
+        lib.cpzt_sc_reduce_wide(out, x); assert fi(out.raw) == fi(x) % L
+        a, b = rnd.randrange(L), rnd.randrange(L)
+        lib.cpzt_sc_mul(out, a.to_bytes(32, "little"), b.to_bytes(32, "little")); assert fi(out.raw) == a * b % L
+        lib.cpzt_sc_add(out, a.to_bytes(32, "little"), b.to_bytes(32, "little")); assert fi(out.raw) == (a + b) % L
+    for v in [0, 1, L - 1, L, L + 1, 2**253, 2**255, 2**256 - 1]:
+        assert lib.cpzt_sc_canonical(v.to_bytes(32, "little")) == (1 if v < L else 0)
+
+
+def test_hashes(lib, golden):
+    rnd = random.Random(7)
+    o64 = buf(64)
+    key = bytes(range(32))
+    for ctr, stream in [(0, 0), (5, 1), (2**32 + 3, 0), (2**64 - 1, 7)]:
+        lib.cpzt_chacha20_block(o64, key, ctypes.c_uint64(ctr), ctypes.c_uint64(stream))
+        assert o64.raw == O.chacha20_block(key, ctr, stream)
+    st = bytearray(rnd.getrandbits(8) for _ in range(200))
+    st2 = ctypes.create_string_buffer(bytes(st), 200)
+    lib.cpzt_keccak_f1600(st2)
+    O.keccak_f1600(st)
+    assert st2.raw == bytes(st)
+    k = golden["merlin_kat"]
+    out = buf()
+    lib.cpzt_merlin_kat(out, k["protocol"].encode(), len(k["protocol"]), k["label"].encode(), len(k["label"]),
+                        k["message"].encode(), len(k["message"]), k["challenge_label"].encode(),
+                        len(k["challenge_label"]), k["n"])
+    assert out.raw.hex() == k["out"]
+
+
+def _ctx(p):
+    return None if p["ctx"] is None else bytes.fromhex(p["ctx"])
+
+
+def test_golden_proofs_host_build(lib, golden):
+    g, h = bytes.fromhex(golden["g"]), bytes.fromhex(golden["h"])
+    out = buf()
+    for p in golden["proofs"]:
+        f = {k: bytes.fromhex(p[k]) for k in ("y1", "y2", "r1", "r2", "s")}
+        ctx = _ctx(p)
+        cb = ctx or b""
+        if "c" in p:
+            lib.cpzt_challenge(out, g, h, f["y1"], f["y2"], f["r1"], f["r2"], cb, len(cb), ctx is not None)
+            assert out.raw.hex() == p["c"], p["kind"]
+        st = lib.cpzt_verify(g, h, f["y1"], f["y2"], f["r1"], f["r2"], f["s"], cb, len(cb), ctx is not None)
+        assert st == p["status"], (p["kind"], st, p["status"])
+    cg = golden["custom_generators"]
+    g2, h2 = bytes.fromhex(cg["g"]), bytes.fromhex(cg["h"])
+    for p in cg["proofs"]:
+        f = {k: bytes.fromhex(p[k]) for k in ("y1", "y2", "r1", "r2", "s")}
+        cb = _ctx(p) or b""
+        assert lib.cpzt_verify(g2, h2, f["y1"], f["y2"], f["r1"], f["r2"], f["s"], cb, len(cb), 1) == 0
+        assert lib.cpzt_verify(g, h, f["y1"], f["y2"], f["r1"], f["r2"], f["s"], cb, len(cb), 1) == 1

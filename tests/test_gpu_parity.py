@@ -1,0 +1,196 @@
+"""GPU parity tests: the HIP path (lib/libcpz.so via the C ABI) against the oracle's
+golden fixtures and against size-independent properties at scale.
+
+Reference behaviour pinned (batch.rs:337-511, verifier/mod.rs:179-229,
+tests/security_tests.rs): valid accepted, forged / wrong-statement / wrong-context
+rejected, decode rejections (gadgets.rs:364-489), empty batch and 1000-entry cap.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _arr(proofs, key):
+    return np.frombuffer(b"".join(bytes.fromhex(p[key]) for p in proofs), np.uint8).reshape(-1, 32)
+
+
+def _ctxs(proofs):
+    return [None if p["ctx"] is None else bytes.fromhex(p["ctx"]) for p in proofs]
+
+
+def test_golden_status_and_challenges(gpu, golden):
+    import chaum_pedersen as cp
+    ps = golden["proofs"]
+    st = gpu.verify_each(_arr(ps, "y1"), _arr(ps, "y2"), _arr(ps, "r1"), _arr(ps, "r2"), _arr(ps, "s"),
+                         contexts=_ctxs(ps))
+    exp = np.array([p["status"] for p in ps], np.uint8)
+    bad = [(p["kind"], int(a), int(b)) for p, a, b in zip(ps, st, exp) if a != b]
+    assert not bad, bad
+    with_c = [p for p in ps if "c" in p]
+    c = gpu.challenges(_arr(with_c, "y1"), _arr(with_c, "y2"), _arr(with_c, "r1"), _arr(with_c, "r2"),
+                       contexts=_ctxs(with_c))
+    assert [bytes(r).hex() for r in c] == [p["c"] for p in with_c]
+    # each proof alone (n == 1 path, batch.rs:178-180) gives the same answer
+    for p in ps[:6] + ps[-12:]:
+        one = gpu.verify_each(_arr([p], "y1"), _arr([p], "y2"), _arr([p], "r1"), _arr([p], "r2"), _arr([p], "s"),
+                              contexts=_ctxs([p]))
+        assert int(one[0]) == p["status"], p["kind"]
+
+
+def test_custom_generators(gpu, golden):
+    import chaum_pedersen as cp
+    cg = golden["custom_generators"]
+    params = cp.Parameters.with_generators(bytes.fromhex(cg["g"]), bytes.fromhex(cg["h"]))
+    ps = cg["proofs"]
+    args = [_arr(ps, k) for k in ("y1", "y2", "r1", "r2", "s")]
+    assert list(gpu.verify_each(*args, contexts=_ctxs(ps), params=params)) == [0] * len(ps)
+    assert list(gpu.verify_each(*args, contexts=_ctxs(ps))) == [1] * len(ps)
+    # undecodable generator -> CPZ_EGENERATOR
+    bad = cp.Parameters(bytes.fromhex(golden["rfc9496_bad"][4]), bytes.fromhex(cg["h"]))
+    with pytest.raises(cp.CpzError) as ei:
+        gpu.verify_each(*args, contexts=_ctxs(ps), params=bad)
+    assert ei.value.code == -4
+
+
+def test_synthetic_prover_matches_oracle(gpu, golden):
+    sx, sk = bytes.fromhex(golden["seed_x"]), bytes.fromhex(golden["seed_k"])
+    syn = golden["synthetic"]
+    first8 = gpu.prove_synthetic(8, sx, sk)
+    for i in range(8):
+        for k in ("y1", "y2", "r1", "r2", "s"):
+            assert bytes(first8[k][i]).hex() == syn[i][k], (i, k)
+    for d in syn[8:]:
+        one = gpu.prove_synthetic(1, sx, sk, first_index=d["index"])
+        for k in ("y1", "y2", "r1", "r2", "s"):
+            assert bytes(one[k][0]).hex() == d[k], (d["index"], k)
+
+
+def _prove_oracle(i, ctx=None):
+    return O.prove(O.bench_scalar(b"x", 1000 + i), O.bench_scalar(b"k", 1000 + i), ctx)
+
+
+def _rec_args(recs):
+    return [np.frombuffer(b"".join(getattr(r, k) for r in recs), np.uint8).reshape(-1, 32)
+            for k in ("y1", "y2", "r1", "r2", "s")]
+
+
+# ---- BatchVerifier mirror: the reference's batch.rs unit tests ---------------------------
+def _entry(i, ctx=None, wrong_statement=False):
+    import chaum_pedersen as cp
+    rec = _prove_oracle(i, ctx)
+    if wrong_statement:
+        other = _prove_oracle(i + 500)
+        st = cp.Statement(other.y1, other.y2)
+    else:
+        st = cp.Statement(rec.y1, rec.y2)
+    return cp.Parameters(), st, cp.Proof(rec.r1, rec.r2, rec.s)
+
+
+def test_batch_empty_fails(gpu):
+    import chaum_pedersen as cp
+    with pytest.raises(cp.InvalidParams):
+        cp.BatchVerifier(gpu).verify()
+
+
+def test_batch_single_valid_and_invalid(gpu):
+    import chaum_pedersen as cp
+    b = cp.BatchVerifier(gpu)
+    b.add(*_entry(0))
+    r = b.verify()
+    assert len(r) == 1 and r[0].is_ok()
+    b = cp.BatchVerifier(gpu)
+    b.add(*_entry(1, wrong_statement=True))
+    r = b.verify()
+    assert len(r) == 1 and r[0].is_err() and isinstance(r[0].error(), cp.InvalidParams)
+
+
+def test_batch_multiple_valid_and_mixed(gpu):
+    import chaum_pedersen as cp
+    b = cp.BatchVerifier(gpu)
+    for i in range(10):
+        b.add(*_entry(i))
+    assert all(r.is_ok() for r in b.verify())
+    b = cp.BatchVerifier(gpu)
+    for i in range(10):
+        b.add(*_entry(i, wrong_statement=(i % 2 == 1)))
+    res = b.verify()
+    assert [r.is_ok() for r in res] == [i % 2 == 0 for i in range(10)]
+
+
+def test_batch_with_transcript_context_and_replay(gpu):
+    import chaum_pedersen as cp
+    params, st, proof = _entry(3, ctx=b"challenge-12345")
+    b = cp.BatchVerifier(gpu)
+    b.add_with_context(params, st, proof, b"challenge-12345")
+    assert b.verify()[0].is_ok()
+    b = cp.BatchVerifier(gpu)
+    b.add_with_context(params, st, proof, b"challenge-99999")   # replayed into another session
+    b.add(params, st, proof)                                    # context dropped
+    assert [r.is_ok() for r in b.verify()] == [False, False]
+
+
+def test_batch_size_limit_capacity_clear(gpu):
+    import chaum_pedersen as cp
+    b = cp.BatchVerifier(gpu)
+    assert b.len() == 0 and b.is_empty() and b.remaining_capacity() == cp.MAX_BATCH_SIZE
+    e = _entry(7)
+    for _ in range(cp.MAX_BATCH_SIZE):
+        b.add(*e)
+    with pytest.raises(cp.InvalidParams):
+        b.add(*e)
+    res = b.verify()
+    assert len(res) == cp.MAX_BATCH_SIZE and all(r.is_ok() for r in res)
+    b.clear()
+    assert b.is_empty()
+
+
+def test_security_corrupted_bytes(gpu):
+    """security_tests.rs:42-105: corrupt byte 6 (commitment) or len-10 (response)."""
+    import chaum_pedersen as cp
+    rec = _prove_oracle(11)
+    st = cp.Statement(rec.y1, rec.y2)
+    wire = cp.Proof(rec.r1, rec.r2, rec.s).to_bytes()
+    assert len(wire) == 109
+    for pos in (1 + 5, len(wire) - 10):
+        w = bytearray(wire)
+        w[pos] ^= 0xFF
+        b = cp.BatchVerifier(gpu)
+        b.add(cp.Parameters(), st, cp.Proof.from_bytes(bytes(w)))
+        assert b.verify()[0].is_err()
+
+
+# ---- at scale: size-independent properties ----------------------------------------------
+def test_scale_synthetic_all_valid_and_forged_exact(gpu, golden):
+    torch = pytest.importorskip("torch")
+    n = 1 << 17
+    sx, sk = bytes.fromhex(golden["seed_x"]), bytes.fromhex(golden["seed_k"])
+    dev = torch.device("cuda:0")
+    t = {k: torch.empty((n, 32), dtype=torch.uint8, device=dev) for k in ("y1", "y2", "r1", "r2", "s")}
+    gpu.prove_synthetic_device(n, sx, sk, t["y1"], t["y2"], t["r1"], t["r2"], t["s"])
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    gpu.verify_each_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status)
+    torch.cuda.synchronize()
+    assert int(status.sum().item()) == 0 and int((status == 0).sum().item()) == n
+    # forge 1%: s := s + 1 (mod l) at seeded indices -> exactly those fail with status 1
+    rng = np.random.default_rng(1234)
+    idx = np.sort(rng.choice(n, size=n // 100, replace=False))
+    s_host = t["s"].cpu().numpy().copy()
+    for i in idx:
+        v = (int.from_bytes(s_host[i].tobytes(), "little") + 1) % O.L
+        s_host[i] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)
+    t["s"].copy_(torch.from_numpy(s_host))
+    gpu.verify_each_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status)
+    torch.cuda.synchronize()
+    got = np.nonzero(status.cpu().numpy())[0]
+    assert np.array_equal(got, idx)
+    assert set(np.unique(status.cpu().numpy()[idx]).tolist()) == {1}
+    # spot-check a sample against the oracle's per-proof verify
+    host = {k: t[k].cpu().numpy() for k in t}
+    for i in list(idx[:4]) + [0, n - 1, 77777]:
+        rec = O.ProofRecord(*(host[k][i].tobytes() for k in ("y1", "y2", "r1", "r2", "s")))
+        assert O.verify_one(rec) == int(status[i].item())
