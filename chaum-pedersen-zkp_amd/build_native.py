@@ -89,6 +89,22 @@ def build_hosttest(force: bool = False) -> str:
     return HOSTTEST
 
 
+CPP_TEST = os.path.join(ROOT, "tests", "cpp", "batch_verifier_test")
+
+
+def build_cpp_test(force: bool = False) -> str:
+    """C++ mirror of batch.rs's unit tests over include/cpz_batch.hpp (links libcpz.so)."""
+    src = os.path.join(ROOT, "tests", "cpp", "batch_verifier_test.cpp")
+    hdrs = [os.path.join(ROOT, "include", "cpz.h"), os.path.join(ROOT, "include", "cpz_batch.hpp")]
+    if not force and not _newer(CPP_TEST, [src, LIBCPZ] + hdrs):
+        return CPP_TEST
+    cxx = shutil.which("g++") or "g++"
+    _run([cxx, "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), src, "-o", CPP_TEST + ".tmp",
+          "-L", LIBDIR, "-lcpz", "-Wl,-rpath,$ORIGIN/../../chaum-pedersen-zkp_amd/lib"])
+    os.replace(CPP_TEST + ".tmp", CPP_TEST)
+    return CPP_TEST
+
+
 def build_oracle(force: bool = False) -> None:
     mk = os.path.join(ROOT, "oracle", "Makefile")
     if os.path.exists(mk):
@@ -99,6 +115,7 @@ def build_all(force: bool = False, verbose: bool = False) -> None:
     build_hosttest(force)
     build_oracle(force)
     build_libcpz(force, verbose)
+    build_cpp_test(force)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,133 @@
+// C++ mirror of the reference's BatchVerifier unit tests (src/verifier/batch.rs:337-511),
+// run against the GPU through include/cpz_batch.hpp -> include/cpz.h -> lib/libcpz.so.
+// Proofs come from the GPU prover (cpz_prove_synthetic); contexts follow
+// examples/batch_verification.rs ("user-{i}-session").  Exit status 0 = all passed.
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "cpz_batch.hpp"
+
+using namespace chaum_pedersen;
+
+static int failures = 0;
+#define CHECK(cond)                                                   \
+  do {                                                                \
+    if (!(cond)) {                                                    \
+      std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+      failures++;                                                     \
+    }                                                                 \
+  } while (0)
+
+struct Set {
+  std::vector<Statement> st;
+  std::vector<Proof> pr;
+};
+
+static Set prove(Device& dev, std::size_t n, uint64_t first, const std::vector<std::string>* ctxs = nullptr) {
+  Set s;
+  Parameters p;
+  std::vector<uint8_t> y1(32 * n), y2(32 * n), r1(32 * n), r2(32 * n), sc(32 * n), blob;
+  std::vector<uint64_t> off(n + 1, 0);
+  if (ctxs)
+    for (std::size_t i = 0; i < n; i++) {
+      blob.insert(blob.end(), (*ctxs)[i].begin(), (*ctxs)[i].end());
+      off[i + 1] = blob.size();
+    }
+  if (blob.empty()) blob.push_back(0);
+  uint8_t sx[32], sk[32];
+  for (int i = 0; i < 32; i++) { sx[i] = (uint8_t)(i * 13 + 1); sk[i] = (uint8_t)(i * 7 + 3); }
+  const int rc = cpz_prove_synthetic(dev.get(), p.g.data(), p.h.data(), n, first, sx, sk, ctxs ? blob.data() : nullptr,
+                                     ctxs ? off.data() : nullptr, nullptr, y1.data(), y2.data(), r1.data(), r2.data(),
+                                     sc.data());
+  if (rc != CPZ_OK) {
+    std::fprintf(stderr, "prove failed: %s\n", cpz_last_error());
+    std::exit(2);
+  }
+  for (std::size_t i = 0; i < n; i++) {
+    Statement st;
+    Proof pr;
+    std::memcpy(st.y1.data(), &y1[32 * i], 32);
+    std::memcpy(st.y2.data(), &y2[32 * i], 32);
+    std::memcpy(pr.r1.data(), &r1[32 * i], 32);
+    std::memcpy(pr.r2.data(), &r2[32 * i], 32);
+    std::memcpy(pr.s.data(), &sc[32 * i], 32);
+    s.st.push_back(st);
+    s.pr.push_back(pr);
+  }
+  return s;
+}
+
+int main() {
+  Device dev(0);
+  if (!dev.ok()) {
+    std::fprintf(stderr, "no device: %s\n", cpz_last_error());
+    return 2;
+  }
+  Parameters params;
+  Set base = prove(dev, 32, 7000);
+  {  // empty_batch_fails
+    BatchVerifier b(dev);
+    Result overall;
+    auto r = b.verify(&overall);
+    CHECK(overall.is_err() && r.empty());
+  }
+  {  // single_valid_proof
+    BatchVerifier b(dev);
+    CHECK(b.add(params, base.st[0], base.pr[0]).is_ok());
+    auto r = b.verify();
+    CHECK(r.size() == 1 && r[0].is_ok());
+  }
+  {  // single_invalid_proof (wrong statement)
+    BatchVerifier b(dev);
+    b.add(params, base.st[1], base.pr[0]);
+    auto r = b.verify();
+    CHECK(r.size() == 1 && r[0].is_err() && r[0].kind == ErrorKind::InvalidParams);
+  }
+  {  // multiple_valid_proofs
+    BatchVerifier b(dev);
+    for (int i = 0; i < 10; i++) b.add(params, base.st[i], base.pr[i]);
+    auto r = b.verify();
+    CHECK(r.size() == 10);
+    for (auto& x : r) CHECK(x.is_ok());
+  }
+  {  // mixed_valid_invalid_proofs
+    BatchVerifier b(dev);
+    for (int i = 0; i < 10; i++) b.add(params, (i % 2 == 0) ? base.st[i] : base.st[i + 10], base.pr[i]);
+    auto r = b.verify();
+    CHECK(r.size() == 10);
+    for (int i = 0; i < 10; i++) CHECK(r[i].is_ok() == (i % 2 == 0));
+  }
+  {  // batch_with_transcript_context (+ examples/batch_verification.rs contexts)
+    std::vector<std::string> ctxs;
+    for (int i = 0; i < 10; i++) ctxs.push_back("user-" + std::to_string(i) + "-session");
+    Set c = prove(dev, 10, 9000, &ctxs);
+    BatchVerifier b(dev);
+    for (int i = 0; i < 10; i++)
+      b.add_with_context(params, c.st[i], c.pr[i], std::vector<uint8_t>(ctxs[i].begin(), ctxs[i].end()));
+    b.add(params, c.st[0], c.pr[0]);  // context dropped -> must fail
+    auto r = b.verify();
+    CHECK(r.size() == 11);
+    for (int i = 0; i < 10; i++) CHECK(r[i].is_ok());
+    CHECK(r[10].is_err());
+  }
+  {  // batch_size_limit / batch_capacity_tracking / batch_clear
+    BatchVerifier b(dev);
+    CHECK(b.len() == 0 && b.is_empty() && b.remaining_capacity() == MAX_BATCH_SIZE);
+    for (std::size_t i = 0; i < MAX_BATCH_SIZE; i++) CHECK(b.add(params, base.st[i % 32], base.pr[i % 32]).is_ok());
+    CHECK(b.add(params, base.st[0], base.pr[0]).is_err());
+    CHECK(b.remaining_capacity() == 0);
+    auto r = b.verify();
+    CHECK(r.size() == MAX_BATCH_SIZE);
+    for (auto& x : r) CHECK(x.is_ok());
+    b.clear();
+    CHECK(b.is_empty());
+  }
+  if (failures) {
+    std::fprintf(stderr, "%d failures\n", failures);
+    return 1;
+  }
+  std::printf("batch_verifier_test: all passed\n");
+  return 0;
+}

@@ -194,3 +194,14 @@ def test_scale_synthetic_all_valid_and_forged_exact(gpu, golden):
     for i in list(idx[:4]) + [0, n - 1, 77777]:
         rec = O.ProofRecord(*(host[k][i].tobytes() for k in ("y1", "y2", "r1", "r2", "s")))
         assert O.verify_one(rec) == int(status[i].item())
+
+
+def test_cpp_batch_verifier_mirror():
+    """The C++ mirror (include/cpz_batch.hpp) of batch.rs's unit tests, through the C ABI."""
+    import os
+    import subprocess
+    import build_native
+    exe = build_native.build_cpp_test()
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "all passed" in r.stdout

@@ -1,0 +1,22 @@
+"""bench/opcount.json (the algorithmic work the roofline divides by) must match what the
+device code actually executes per proof, counted on the host build of csrc/verify.h."""
+import ctypes
+import json
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_verify_each_opcount(golden):
+    import build_native
+    lib = ctypes.CDLL(build_native.build_hosttest())
+    oc = json.load(open(os.path.join(ROOT, "bench", "opcount.json")))["verify_each"]
+    g, h = bytes.fromhex(golden["g"]), bytes.fromhex(golden["h"])
+    for p in [q for q in golden["proofs"] if "c" in q][:5]:
+        f = {k: bytes.fromhex(p[k]) for k in ("y1", "y2", "r1", "r2", "s", "c")}
+        m, s = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        lib.cpzt_verify_opcount(ctypes.byref(m), ctypes.byref(s), g, h, f["y1"], f["y2"], f["r1"], f["r2"], f["s"],
+                                f["c"])
+        # fixed windows: the work does not depend on the data
+        assert (m.value, s.value) == (oc["fe_mul"], oc["fe_sq"])
+    assert oc["mads_per_proof"] == oc["fe_mul"] * oc["mads_per_fe_mul"] + oc["fe_sq"] * oc["mads_per_fe_sq"]

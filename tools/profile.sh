@@ -1,0 +1,19 @@
+#!/bin/bash
+# rocprofv3 passes for the bench workload (run on the GPU box from the repo root):
+#   A: kernel trace + stats (per-kernel durations)      -> gpurun_out/prof_trace
+#   B/C: HBM traffic counters, one per pass (FETCH_SIZE, WRITE_SIZE)
+#   D: SQ instruction / wave counters
+# Each GPU step has its own time limit; steps are chained with && so a failure stops the script.
+set -o pipefail
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p $OUT
+ARGS="--steps ${STEPS:-3} --warmup 1 --no-cpu-baseline ${BENCH_ARGS}"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_trace -o run -- python3 bench.py $ARGS > $OUT/prof_trace.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_fetch -o run -- python3 bench.py $ARGS > $OUT/prof_fetch.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_write -o run -- python3 bench.py $ARGS > $OUT/prof_write.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $OUT/prof_sq -o run -- python3 bench.py $ARGS > $OUT/prof_sq.log 2>&1
+rc=$?
+echo "profile rc=$rc"
+find $OUT -name "*.csv" | head -50
+exit $rc
