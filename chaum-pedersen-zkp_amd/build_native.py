@@ -53,7 +53,7 @@ def _run(cmd):
 
 
 def build_libcpz(force: bool = False, verbose: bool = False) -> str:
-    units = ["kernels.hip", "runtime.hip"]
+    units = ["kernels.hip", "rlc.hip", "runtime.hip"]
     srcs = [os.path.join(CSRC, u) for u in units] + _headers()
     if not force and not _newer(LIBCPZ, srcs):
         return LIBCPZ

@@ -291,6 +291,44 @@ class Gpu:
             _ptr(out)))
         return out
 
+    def verify_batch(self, y1, y2, r1, r2, s, seed: bytes, first_index: int = 0, contexts=None,
+                     params: Optional[Parameters] = None, statuses: bool = True):
+        """RLC batch check (cpz_verify_batch).  Returns (partial: bytes, batch_ok: bool,
+        status: uint8[n] or None).  With statuses=True a failing batch runs the fallback
+        search and status holds the exact per-entry outcome."""
+        params = params or Parameters()
+        n = len(y1)
+        arrs = [_rows(a, n, nm) for a, nm in ((y1, "y1"), (y2, "y2"), (r1, "r1"), (r2, "r2"), (s, "s"))]
+        blob, off, present = _ctx_arrays(contexts, n)
+        partial = ctypes.create_string_buffer(32)
+        ok = ctypes.c_int(0)
+        out = np.empty(n, dtype=np.uint8) if statuses else None
+        _native.check(self._lib.cpz_verify_batch(
+            self._h, params.g, params.h, n, *[_ptr(a) for a in arrs], _ptr(blob), _ptr(off), _ptr(present),
+            bytes(seed), first_index, partial, ctypes.byref(ok), _ptr(out)))
+        return partial.raw, bool(ok.value), out
+
+    def verify_batch_device(self, y1, y2, r1, r2, s, status_out, seed: bytes, first_index: int = 0,
+                            fallback: bool = False, params: Optional[Parameters] = None,
+                            stream: Optional[int] = None):
+        """Device-resident RLC batch check; returns (partial, batch_ok); fills status_out."""
+        params = params or Parameters()
+        partial = ctypes.create_string_buffer(32)
+        ok = ctypes.c_int(0)
+        _native.check(self._lib.cpz_verify_batch_device(
+            self._h, params.g, params.h, int(y1.shape[0]), y1.data_ptr(), y2.data_ptr(), r1.data_ptr(),
+            r2.data_ptr(), s.data_ptr(), None, None, None, bytes(seed), first_index, partial, ctypes.byref(ok),
+            status_out.data_ptr(), 1 if fallback else 0, stream))
+        return partial.raw, bool(ok.value)
+
+    def combine_partials(self, partials: Sequence[bytes]):
+        """(sum encoding, is_identity) of per-shard partials (cpz_combine_partials)."""
+        blob = b"".join(bytes(p) for p in partials)
+        out = ctypes.create_string_buffer(32)
+        ident = ctypes.c_int(0)
+        _native.check(self._lib.cpz_combine_partials(self._h, len(partials), blob, out, ctypes.byref(ident)))
+        return out.raw, bool(ident.value)
+
     def prove_synthetic(self, n: int, seed_x: bytes, seed_k: bytes, first_index: int = 0, contexts=None,
                         params: Optional[Parameters] = None):
         """Synthetic proofs from ChaCha20-derived witnesses: dict of (n, 32) arrays."""

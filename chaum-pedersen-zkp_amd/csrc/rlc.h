@@ -1,0 +1,59 @@
+// Argument blocks and launchers of the RLC / Pippenger path (rlc.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "scalar25519.h"
+#include "scalarmul.h"
+
+namespace cpz {
+
+constexpr int kRlcWindows = 16;          // 16-bit signed windows cover scalars < 2^255
+constexpr int kRlcBuckets = 1 << 15;     // |digit| in [1, 2^15]
+constexpr int kRlcSegLen = 32;           // buckets per reduction segment
+constexpr int kRlcPrepBlock = 256;       // proofs per prepare block (= block_sums granule)
+constexpr int kRlcSortBlock = 1024;
+constexpr int kNielsEntriesRlc = kTableB;
+
+struct RlcPrepArgs {
+  int64_t n;
+  uint64_t first_index;          // global index of proof 0 (weights are keyed by it)
+  uint32_t seed[8];
+  const uint32_t* y1;
+  const uint32_t* y2;
+  const uint32_t* r1;
+  const uint32_t* r2;
+  const uint32_t* s;
+  const uint32_t* c;             // challenges from k_challenge
+  uint8_t* status;               // in: response status; out: decode-level status (0/2/3/4)
+  ge_niels* pts;                 // 4 n (+2 extra) negated affine points
+  int16_t* digits;               // [16][dstride] signed radix-2^16 digits
+  int64_t dstride;
+  sc* block_sums;                // [ceil(n/256)][2]
+};
+
+struct RlcMsmArgs {
+  int64_t p0, p1;                // point range [p0, p1)
+  int64_t e0;                    // the two extra points (g, h) live at e0, e0 + 1
+  ge_niels* pts;
+  int16_t* digits;
+  int64_t dstride;
+  uint32_t* counts;              // [16][2^15]
+  uint32_t* offsets;             // [16][2^15 + 1]
+  uint32_t* cursor;              // [16][2^15]
+  uint32_t* idx;                 // [16][istride]
+  int64_t istride;
+  ge_p3* buckets;                // [16][2^15]
+  ge_p3* seg_s;                  // [16][1024]
+  ge_p3* seg_w;                  // [16][1024]
+  ge_p3* win;                    // [16]
+  uint32_t* partial_out;         // 8 words
+  int* identity_out;             // 1
+};
+
+hipError_t launch_rlc_prepare(const RlcPrepArgs& a, hipStream_t st);
+hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0, int64_t b1, const ge_niels* tab,
+                          int sort_blocks, hipStream_t st);
+hipError_t launch_rlc_combine(const uint32_t* parts, int k, uint32_t* out, int* flags, hipStream_t st);
+
+}  // namespace cpz

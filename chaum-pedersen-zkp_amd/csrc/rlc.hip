@@ -1,0 +1,474 @@
+// Random-linear-combination batch verification on gfx950: one Pippenger multi-scalar
+// multiplication per batch (or per shard / per sub-range during fallback).
+//
+// Replaces the reference's batch check (verify_batch / verify_batch_equations,
+// batch.rs:233-312) with the CORRECT equation (the reference omits alpha on y*c,
+// batch.rs:297-300):
+//   P = sum_i  [a_i s_i] g - [a_i] r1_i - [a_i c_i] y1_i + [b_i s_i] h - [b_i] r2_i - [b_i c_i] y2_i
+// with a_i = wide(ChaCha20(seed, block first+i, stream 0)), b_i = stream 1 (the i-th
+// `random_scalar` of ChaCha20Rng::from_seed(seed), batch.rs:240).  P is the identity iff
+// every weighted proof satisfies both equations (w.o.p.).  Proofs whose decode-level
+// status is non-zero carry zero weight and are reported individually.
+//
+// Pipeline (all on one stream):
+//   k_rlc_prepare   1 thread / proof: 4 decodes, weights, 4 scalar products, negated
+//                   affine-Niels points, signed radix-2^16 digits (16 windows), per-block
+//                   sums of a_i s_i and b_i s_i.
+//   k_rlc_extra     g and h as two more MSM points with the summed scalars.
+//   k_rlc_hist      per-window bucket histogram (LDS-privatised, 32768 buckets).
+//   k_rlc_scan      exclusive scan -> bucket offsets.
+//   k_rlc_scatter   point ids sorted by bucket (counting sort).
+//   k_rlc_bucket    1 thread / (window, bucket): mixed additions over its list.
+//   k_rlc_segment   1 thread / (window, 32-bucket segment): running sums.
+//   k_rlc_window    1 block / window: sum_b b * B_b from the segments (LDS tree).
+//   k_rlc_final     2^(16w) combine, encode -> 32-byte partial + identity flag.
+#include <hip/hip_runtime.h>
+
+#include "rlc.h"
+#include "verify.h"
+
+namespace cpz {
+
+__device__ __forceinline__ void rlc_load8(uint32_t w[8], const uint32_t* base, int64_t i) {
+  const uint4* p = reinterpret_cast<const uint4*>(base + 8 * i);
+  const uint4 a = p[0], b = p[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+  w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+
+// Signed radix-2^16 digits of a scalar < 2^253 (16 windows, digit in [-2^15, 2^15)).
+__device__ __forceinline__ void recode16(int16_t d[kRlcWindows], const uint32_t s[8]) {
+  int32_t carry = 0;
+#pragma unroll
+  for (int w = 0; w < kRlcWindows; w++) {
+    const int32_t chunk = (int32_t)((s[w >> 1] >> (16 * (w & 1))) & 0xffffu) + carry;
+    carry = (chunk + 0x8000) >> 16;
+    d[w] = (int16_t)(chunk - (carry << 16));
+  }
+}
+
+__device__ __forceinline__ ge_niels niels_from_p3_affine(const ge_p3& P, bool neg) {
+  // P has Z = 1 (decoded): (y + x, y - x, 2d x y), negated by swapping and negating.
+  ge_niels r;
+  r.ypx = fe_add(P.Y, P.X);
+  r.ymx = fe_sub(P.Y, P.X);
+  r.xy2d = fe_mul(P.T, FE_D2());
+  return ge_niels_cneg(r, neg);
+}
+
+__device__ __forceinline__ void store_niels(ge_niels* dst, const ge_niels& v) {
+  const uint4* s = reinterpret_cast<const uint4*>(&v);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(ge_niels) / 16); k++) d[k] = s[k];
+}
+
+__device__ __forceinline__ ge_niels load_niels(const ge_niels* src) {
+  ge_niels v;
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint4* d = reinterpret_cast<uint4*>(&v);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(ge_niels) / 16); k++) d[k] = s[k];
+  return v;
+}
+
+__device__ __forceinline__ void store_p3(ge_p3* dst, const ge_p3& v) {
+  const uint4* s = reinterpret_cast<const uint4*>(&v);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(ge_p3) / 16); k++) d[k] = s[k];
+}
+
+__device__ __forceinline__ ge_p3 load_p3(const ge_p3* src) {
+  ge_p3 v;
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint4* d = reinterpret_cast<uint4*>(&v);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(ge_p3) / 16); k++) d[k] = s[k];
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// k_rlc_prepare
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kRlcPrepBlock) k_rlc_prepare(RlcPrepArgs a) {
+  __shared__ sc red_a[kRlcPrepBlock];
+  __shared__ sc red_b[kRlcPrepBlock];
+  const int64_t i = (int64_t)blockIdx.x * kRlcPrepBlock + threadIdx.x;
+  sc as, bs;
+#pragma unroll
+  for (int k = 0; k < 8; k++) { as.w[k] = 0; bs.w[k] = 0; }
+  if (i < a.n) {
+    uint32_t w[8];
+    ge_p3 Y1, Y2, R1, R2;
+    rlc_load8(w, a.y1, i);
+    bool ok = ristretto_decode(Y1, w);
+    rlc_load8(w, a.y2, i);
+    ok = ristretto_decode(Y2, w) && ok;
+    rlc_load8(w, a.r1, i);
+    bool ident = words8_zero(w);
+    ok = ristretto_decode(R1, w) && ok;
+    rlc_load8(w, a.r2, i);
+    ident = words8_zero(w) || ident;
+    ok = ristretto_decode(R2, w) && ok;
+    const uint8_t st_s = a.status[i];
+    uint8_t st;
+    if (!ok) st = kStBadPoint;
+    else if (st_s == kStBadScalar) st = kStBadScalar;
+    else if (ident || st_s == kStIdentityOrZero) st = kStIdentityOrZero;
+    else st = kStOk;
+    a.status[i] = st;
+    const bool live = (st == kStOk);
+
+    // weights (batch.rs:240 random_scalar, here ChaCha20Rng-keyed by the seed)
+    uint32_t blk[16];
+    chacha20_block(blk, a.seed, a.first_index + (uint64_t)i, 0);
+    const sc wa = sc_reduce_wide(blk);
+    chacha20_block(blk, a.seed, a.first_index + (uint64_t)i, 1);
+    const sc wb = sc_reduce_wide(blk);
+    sc c, s;
+    rlc_load8(c.w, a.c, i);
+    rlc_load8(s.w, a.s, i);
+    sc k[4];
+    k[0] = wa;              // -r1
+    k[1] = sc_mul(wa, c);   // -y1
+    k[2] = wb;              // -r2
+    k[3] = sc_mul(wb, c);   // -y2
+    if (live) {
+      as = sc_mul(wa, s);
+      bs = sc_mul(wb, s);
+    }
+    const ge_p3* P[4] = {&R1, &Y1, &R2, &Y2};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int64_t j = 4 * i + q;
+      store_niels(a.pts + j, live ? niels_from_p3_affine(*P[q], true) : ge_niels_identity());
+      int16_t d[kRlcWindows];
+      recode16(d, k[q].w);
+#pragma unroll
+      for (int wv = 0; wv < kRlcWindows; wv++) a.digits[(int64_t)wv * a.dstride + j] = live ? d[wv] : (int16_t)0;
+    }
+  }
+  // block sums of a_i s_i, b_i s_i (mod l)
+  red_a[threadIdx.x] = as;
+  red_b[threadIdx.x] = bs;
+  __syncthreads();
+  for (int off = kRlcPrepBlock / 2; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+      red_a[threadIdx.x] = sc_add(red_a[threadIdx.x], red_a[threadIdx.x + off]);
+      red_b[threadIdx.x] = sc_add(red_b[threadIdx.x], red_b[threadIdx.x + off]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    a.block_sums[2 * blockIdx.x] = red_a[0];
+    a.block_sums[2 * blockIdx.x + 1] = red_b[0];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_rlc_extra: g and h with scalars sum_{blocks in [b0, b1)} (a s), (b s).
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_rlc_extra(RlcMsmArgs a, const sc* __restrict__ block_sums, int64_t b0,
+                                                   int64_t b1, const ge_niels* __restrict__ tab) {
+  __shared__ sc red_a[256];
+  __shared__ sc red_b[256];
+  sc sa, sb;
+#pragma unroll
+  for (int k = 0; k < 8; k++) { sa.w[k] = 0; sb.w[k] = 0; }
+  for (int64_t b = b0 + threadIdx.x; b < b1; b += 256) {
+    sa = sc_add(sa, block_sums[2 * b]);
+    sb = sc_add(sb, block_sums[2 * b + 1]);
+  }
+  red_a[threadIdx.x] = sa;
+  red_b[threadIdx.x] = sb;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+      red_a[threadIdx.x] = sc_add(red_a[threadIdx.x], red_a[threadIdx.x + off]);
+      red_b[threadIdx.x] = sc_add(red_b[threadIdx.x], red_b[threadIdx.x + off]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 2) {
+    const sc s = threadIdx.x == 0 ? red_a[0] : red_b[0];
+    const int64_t j = a.e0 + threadIdx.x;
+    store_niels(a.pts + j, tab[threadIdx.x * kNielsEntriesRlc]);  // entry k = 1: g, h
+    int16_t d[kRlcWindows];
+    recode16(d, s.w);
+#pragma unroll
+    for (int wv = 0; wv < kRlcWindows; wv++) a.digits[(int64_t)wv * a.dstride + j] = d[wv];
+  }
+}
+
+// point index for flat position t over [p0, p1) U [e0, e0 + 2)
+__device__ __forceinline__ int64_t msm_point(const RlcMsmArgs& a, int64_t t) {
+  const int64_t np = a.p1 - a.p0;
+  return t < np ? a.p0 + t : a.e0 + (t - np);
+}
+
+// ---------------------------------------------------------------------------------------
+// Counting sort by bucket, per window.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kRlcSortBlock) k_rlc_hist(RlcMsmArgs a) {
+  extern __shared__ uint32_t hist[];  // kRlcBuckets counters
+  const int w = blockIdx.y;
+  for (int b = threadIdx.x; b < kRlcBuckets; b += kRlcSortBlock) hist[b] = 0;
+  __syncthreads();
+  const int64_t total = (a.p1 - a.p0) + 2;
+  const int16_t* dig = a.digits + (int64_t)w * a.dstride;
+  for (int64_t t = (int64_t)blockIdx.x * kRlcSortBlock + threadIdx.x; t < total; t += (int64_t)gridDim.x * kRlcSortBlock) {
+    const int d = dig[msm_point(a, t)];
+    if (d != 0) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
+  }
+  __syncthreads();
+  uint32_t* g = a.counts + (int64_t)w * kRlcBuckets;
+  for (int b = threadIdx.x; b < kRlcBuckets; b += kRlcSortBlock)
+    if (hist[b]) atomicAdd(&g[b], hist[b]);
+}
+
+// One block per window: exclusive scan of kRlcBuckets counts -> offsets (and cursors).
+__global__ void __launch_bounds__(1024) k_rlc_scan(RlcMsmArgs a) {
+  __shared__ uint32_t part[1024];
+  const int w = blockIdx.x;
+  constexpr int per = kRlcBuckets / 1024;
+  const uint32_t* cnt = a.counts + (int64_t)w * kRlcBuckets;
+  uint32_t local[per];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < per; k++) {
+    local[k] = cnt[threadIdx.x * per + k];
+    sum += local[k];
+  }
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  // Hillis-Steele inclusive scan over the 1024 partial sums
+  for (int off = 1; off < 1024; off <<= 1) {
+    const uint32_t v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[threadIdx.x] - sum;  // exclusive
+  uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
+  uint32_t* cur = a.cursor + (int64_t)w * kRlcBuckets;
+#pragma unroll
+  for (int k = 0; k < per; k++) {
+    off[threadIdx.x * per + k] = run;
+    cur[threadIdx.x * per + k] = run;
+    run += local[k];
+  }
+  if (threadIdx.x == 1023) off[kRlcBuckets] = run;
+}
+
+__global__ void __launch_bounds__(kRlcSortBlock) k_rlc_scatter(RlcMsmArgs a) {
+  const int w = blockIdx.y;
+  const int64_t total = (a.p1 - a.p0) + 2;
+  const int16_t* dig = a.digits + (int64_t)w * a.dstride;
+  uint32_t* cur = a.cursor + (int64_t)w * kRlcBuckets;
+  uint32_t* idx = a.idx + (int64_t)w * a.istride;
+  for (int64_t t = (int64_t)blockIdx.x * kRlcSortBlock + threadIdx.x; t < total; t += (int64_t)gridDim.x * kRlcSortBlock) {
+    const int64_t j = msm_point(a, t);
+    const int d = dig[j];
+    if (d != 0) {
+      const uint32_t pos = atomicAdd(&cur[(d < 0 ? -d : d) - 1], 1u);
+      idx[pos] = (uint32_t)j | (d < 0 ? 0x80000000u : 0u);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Bucket accumulation: B[w][b] = sum of (+/-) points in bucket b of window w.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)kRlcWindows * kRlcBuckets) return;
+  const int w = (int)(t / kRlcBuckets);
+  const int b = (int)(t % kRlcBuckets);
+  const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
+  const uint32_t* idx = a.idx + (int64_t)w * a.istride;
+  const uint32_t e0 = off[b], e1 = off[b + 1];
+  ge_p3 acc = ge_identity();
+  for (uint32_t e = e0; e < e1; e++) {
+    const uint32_t id = idx[e];
+    const ge_niels p = ge_niels_cneg(load_niels(a.pts + (id & 0x7fffffffu)), (id >> 31) != 0);
+    acc = p1p1_to_p3(ge_add_niels(acc, p));
+  }
+  store_p3(a.buckets + t, acc);
+}
+
+// One thread per (window, segment of kRlcSegLen buckets):
+//   S = sum_{b in seg} B_b,   W = sum_{b in seg} (b - lo + 1) B_b   (lo = first bucket value)
+__global__ void __launch_bounds__(256) k_rlc_segment(RlcMsmArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  constexpr int nseg = kRlcBuckets / kRlcSegLen;
+  if (t >= (int64_t)kRlcWindows * nseg) return;
+  const int w = (int)(t / nseg);
+  const int sg = (int)(t % nseg);
+  const ge_p3* B = a.buckets + (int64_t)w * kRlcBuckets + (int64_t)sg * kRlcSegLen;
+  ge_p3 run = ge_identity(), acc = ge_identity();
+  for (int k = kRlcSegLen - 1; k >= 0; k--) {
+    run = ge_add(run, load_p3(B + k));
+    acc = ge_add(acc, run);
+  }
+  store_p3(a.seg_s + t, run);
+  store_p3(a.seg_w + t, acc);
+}
+
+// One block (256 threads) per window.  Segment t covers bucket values 32t+1..32t+32:
+//   T_w = sum_t W_t + 32 * sum_t t S_t.
+// Thread u owns segments 4u..4u+3: A_u = sum_j S_{4u+j}, M_u = sum_j j S_{4u+j},
+//   sum_t t S_t = 4 sum_u u A_u + sum_u M_u,   sum_u u A_u = sum_{k>=1} suffix_k(A).
+__global__ void __launch_bounds__(256) k_rlc_window(RlcMsmArgs a) {
+  __shared__ ge_p3 lds[256];
+  const int w = blockIdx.x;
+  const int u = threadIdx.x;
+  constexpr int nseg = kRlcBuckets / kRlcSegLen;
+  static_assert(nseg == 4 * 256, "window kernel assumes 1024 segments");
+  const ge_p3* S = a.seg_s + (int64_t)w * nseg;
+  const ge_p3* Wt = a.seg_w + (int64_t)w * nseg;
+  ge_p3 A = ge_identity(), M = ge_identity(), Wsum = ge_identity();
+  {
+    ge_p3 run = ge_identity();
+    for (int j = 3; j >= 1; j--) {   // M = sum_j j S_j = sum_{j>=1} suffix_j
+      run = ge_add(run, load_p3(S + 4 * u + j));
+      M = ge_add(M, run);
+    }
+    A = ge_add(run, load_p3(S + 4 * u));
+    for (int j = 0; j < 4; j++) Wsum = ge_add(Wsum, load_p3(Wt + 4 * u + j));
+  }
+  // suffix scan of A over u (inclusive): suf_u = sum_{v >= u} A_v
+  lds[u] = A;
+  __syncthreads();
+  ge_p3 suf = A;
+  for (int off = 1; off < 256; off <<= 1) {
+    ge_p3 other = ge_identity();
+    const bool has = u + off < 256;
+    if (has) other = lds[u + off];
+    __syncthreads();
+    if (has) suf = ge_add(suf, other);
+    lds[u] = suf;
+    __syncthreads();
+  }
+  // X_u = [u >= 1] suf_u  + 4^-1 ... combine: total = sum W + 32 * (4 * sum_{u>=1} suf_u + sum M)
+  ge_p3 x = (u >= 1) ? suf : ge_identity();
+  // tree-sum three quantities: x, M, Wsum
+  ge_p3 vals[3] = {x, M, Wsum};
+  ge_p3 tot[3];
+  for (int q = 0; q < 3; q++) {
+    lds[u] = vals[q];
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+      if (u < off) lds[u] = ge_add(lds[u], lds[u + off]);
+      __syncthreads();
+    }
+    tot[q] = lds[0];
+    __syncthreads();
+  }
+  if (u == 0) {
+    ge_p3 r = tot[0];
+    r = p1p1_to_p3(p3_dbl(r));
+    r = p1p1_to_p3(p3_dbl(r));  // 4 * sum suf
+    r = ge_add(r, tot[1]);
+#pragma unroll 1
+    for (int k = 0; k < 5; k++) r = p1p1_to_p3(p3_dbl(r));  // * 32
+    r = ge_add(r, tot[2]);
+    store_p3(a.win + w, r);
+  }
+}
+
+// Single block: P = sum_w 2^(16 w) T_w (tree), encode.
+__global__ void __launch_bounds__(64) k_rlc_final(RlcMsmArgs a) {
+  __shared__ ge_p3 lds[kRlcWindows];
+  const int w = threadIdx.x;
+  if (w < kRlcWindows) lds[w] = load_p3(a.win + w);
+  __syncthreads();
+  // level L: pairs (2k, 2k+1) at stride 2^L windows: T = T_2k + 2^(16 * 2^L) T_2k+1
+  for (int span = 1; span < kRlcWindows; span <<= 1) {
+    const bool active = (w < kRlcWindows) && (w % (2 * span) == 0);
+    ge_p3 hi = ge_identity(), lo = ge_identity();
+    if (active) {
+      lo = lds[w];
+      hi = lds[w + span];
+#pragma unroll 1
+      for (int k = 0; k < 16 * span; k++) hi = p1p1_to_p3(p3_dbl(hi));
+      lo = ge_add(lo, hi);
+    }
+    __syncthreads();
+    if (active) lds[w] = lo;
+    __syncthreads();
+  }
+  if (w == 0) {
+    const ge_p3 P = lds[0];
+    uint32_t enc[8];
+    ristretto_encode(enc, P);
+    for (int k = 0; k < 8; k++) a.partial_out[k] = enc[k];
+    a.identity_out[0] = ristretto_is_identity(P) ? 1 : 0;
+  }
+}
+
+// Sum of k encoded partials (multi-GPU / fallback combine).
+__global__ void k_rlc_combine(const uint32_t* __restrict__ parts, int k, uint32_t* __restrict__ out,
+                              int* __restrict__ flags) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  ge_p3 acc = ge_identity();
+  int ok = 1;
+  for (int j = 0; j < k; j++) {
+    ge_p3 P;
+    ok = ristretto_decode(P, parts + 8 * j) && ok;
+    acc = ge_add(acc, P);
+  }
+  uint32_t enc[8];
+  ristretto_encode(enc, acc);
+  for (int q = 0; q < 8; q++) out[q] = enc[q];
+  flags[0] = ok;
+  flags[1] = ristretto_is_identity(acc) ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------------------
+hipError_t launch_rlc_prepare(const RlcPrepArgs& a, hipStream_t st) {
+  const int64_t blocks = (a.n + kRlcPrepBlock - 1) / kRlcPrepBlock;
+  hipLaunchKernelGGL(k_rlc_prepare, dim3((unsigned)blocks), dim3(kRlcPrepBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0, int64_t b1, const ge_niels* tab,
+                          int sort_blocks, hipStream_t st) {
+  hipError_t e;
+  hipLaunchKernelGGL(k_rlc_extra, dim3(1), dim3(256), 0, st, a, block_sums, b0, b1, tab);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(a.counts, 0, sizeof(uint32_t) * kRlcWindows * kRlcBuckets, st)) != hipSuccess) return e;
+  const size_t lds = sizeof(uint32_t) * kRlcBuckets;  // 128 KB of the 160 KB LDS
+  static bool attr_set = false;
+  if (!attr_set) {
+    if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rlc_hist),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
+      return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k_rlc_hist, dim3(sort_blocks, kRlcWindows), dim3(kRlcSortBlock), lds, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rlc_scan, dim3(kRlcWindows), dim3(1024), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rlc_scatter, dim3(sort_blocks, kRlcWindows), dim3(kRlcSortBlock), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const int64_t nb = (int64_t)kRlcWindows * kRlcBuckets;
+  hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const int64_t ns = (int64_t)kRlcWindows * (kRlcBuckets / kRlcSegLen);
+  hipLaunchKernelGGL(k_rlc_segment, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rlc_window, dim3(kRlcWindows), dim3(256), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rlc_final, dim3(1), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_rlc_combine(const uint32_t* parts, int k, uint32_t* out, int* flags, hipStream_t st) {
+  hipLaunchKernelGGL(k_rlc_combine, dim3(1), dim3(64), 0, st, parts, k, out, flags);
+  return hipGetLastError();
+}
+
+}  // namespace cpz

@@ -15,6 +15,7 @@
 
 #include "../../include/cpz.h"
 #include "cpz_kernels.h"
+#include "rlc.h"
 
 namespace {
 
@@ -86,6 +87,11 @@ struct cpz_ctx {
   // host-API staging
   DevBuf in[5];
   DevBuf ctxb, ctxo, ctxp;
+  // RLC / Pippenger buffers (sized for the largest batch seen)
+  DevBuf rl_pts, rl_dig, rl_bsum, rl_counts, rl_offsets, rl_cursor, rl_idx, rl_buckets, rl_segs, rl_segw, rl_win,
+      rl_partial, rl_flags, rl_parts;
+  int64_t rl_cap = 0;  // proofs
+  int sort_blocks = 0;
   // optional per-kernel timing
   bool timing = false;
   struct Mark { int stage; hipEvent_t a, b; };
@@ -249,6 +255,206 @@ int stage_inputs(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], int count
   return CPZ_OK;
 }
 
+// ---- RLC batch path --------------------------------------------------------------------
+int rlc_reserve(cpz_ctx* ctx, int64_t n) {
+  if (n <= ctx->rl_cap) return CPZ_OK;
+  const int64_t npts = 4 * n + 2;
+  const int64_t nblk = (n + cpz::kRlcPrepBlock - 1) / cpz::kRlcPrepBlock;
+  CPZ_HIP(ctx->rl_pts.ensure((size_t)npts * sizeof(cpz::ge_niels)));
+  CPZ_HIP(ctx->rl_dig.ensure((size_t)npts * cpz::kRlcWindows * sizeof(int16_t)));
+  CPZ_HIP(ctx->rl_bsum.ensure((size_t)nblk * 2 * sizeof(cpz::sc)));
+  CPZ_HIP(ctx->rl_counts.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcBuckets));
+  CPZ_HIP(ctx->rl_offsets.ensure(sizeof(uint32_t) * cpz::kRlcWindows * (cpz::kRlcBuckets + 1)));
+  CPZ_HIP(ctx->rl_cursor.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcBuckets));
+  CPZ_HIP(ctx->rl_idx.ensure((size_t)npts * cpz::kRlcWindows * sizeof(uint32_t)));
+  CPZ_HIP(ctx->rl_buckets.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * cpz::kRlcBuckets));
+  const size_t nseg = (size_t)cpz::kRlcWindows * (cpz::kRlcBuckets / cpz::kRlcSegLen);
+  CPZ_HIP(ctx->rl_segs.ensure(sizeof(cpz::ge_p3) * nseg));
+  CPZ_HIP(ctx->rl_segw.ensure(sizeof(cpz::ge_p3) * nseg));
+  CPZ_HIP(ctx->rl_win.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows));
+  CPZ_HIP(ctx->rl_partial.ensure(64));
+  CPZ_HIP(ctx->rl_flags.ensure(4 * sizeof(int)));
+  ctx->rl_cap = n;
+  return CPZ_OK;
+}
+
+cpz::RlcMsmArgs rlc_msm_args(cpz_ctx* ctx, int64_t lo, int64_t hi) {
+  cpz::RlcMsmArgs m;
+  m.p0 = 4 * lo;
+  m.p1 = 4 * hi;
+  m.e0 = 4 * ctx->rl_cap;
+  m.pts = static_cast<cpz::ge_niels*>(ctx->rl_pts.p);
+  m.digits = static_cast<int16_t*>(ctx->rl_dig.p);
+  m.dstride = 4 * ctx->rl_cap + 2;
+  m.counts = static_cast<uint32_t*>(ctx->rl_counts.p);
+  m.offsets = static_cast<uint32_t*>(ctx->rl_offsets.p);
+  m.cursor = static_cast<uint32_t*>(ctx->rl_cursor.p);
+  m.idx = static_cast<uint32_t*>(ctx->rl_idx.p);
+  m.istride = 4 * ctx->rl_cap + 2;
+  m.buckets = static_cast<cpz::ge_p3*>(ctx->rl_buckets.p);
+  m.seg_s = static_cast<cpz::ge_p3*>(ctx->rl_segs.p);
+  m.seg_w = static_cast<cpz::ge_p3*>(ctx->rl_segw.p);
+  m.win = static_cast<cpz::ge_p3*>(ctx->rl_win.p);
+  m.partial_out = static_cast<uint32_t*>(ctx->rl_partial.p);
+  m.identity_out = static_cast<int*>(ctx->rl_flags.p);
+  return m;
+}
+
+// MSM over proofs [lo, hi) (lo a multiple of kRlcPrepBlock) of the prepared batch.
+// Synchronises; returns the partial encoding and identity flag.
+int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t partial[32], int* identity) {
+  cpz::RlcMsmArgs m = rlc_msm_args(ctx, lo, hi);
+  const int64_t b0 = lo / cpz::kRlcPrepBlock;
+  const int64_t b1 = (hi + cpz::kRlcPrepBlock - 1) / cpz::kRlcPrepBlock;
+  const int64_t npts = 4 * (hi - lo) + 2;
+  int sort_blocks = (int)((npts + cpz::kRlcSortBlock * 64 - 1) / (cpz::kRlcSortBlock * 64));
+  if (sort_blocks > ctx->cus / 8) sort_blocks = ctx->cus / 8 > 0 ? ctx->cus / 8 : 1;
+  if (sort_blocks < 1) sort_blocks = 1;
+  {
+    StageTimer t(ctx, 3, st);
+    CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_bsum.p), b0, b1,
+                                static_cast<const cpz::ge_niels*>(ctx->tab.p), sort_blocks, st));
+  }
+  int flags[1];
+  CPZ_HIP(hipMemcpyAsync(partial, ctx->rl_partial.p, 32, hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipMemcpyAsync(flags, ctx->rl_flags.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipStreamSynchronize(st));
+  *identity = flags[0];
+  return CPZ_OK;
+}
+
+// Prepare (challenge + decode + weights + points/digits) for the whole batch.
+int rlc_prepare(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
+                const void* s, const void* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
+                uint8_t* status, const uint8_t seed[32], uint64_t first_index, hipStream_t st) {
+  int rc = rlc_reserve(ctx, (int64_t)n);
+  if (rc) return rc;
+  CPZ_HIP(ctx->c.ensure(n * 32));
+  cpz::ChallengeArgs ca;
+  ca.n = (int64_t)n;
+  words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
+  ca.y1 = static_cast<const uint32_t*>(y1);
+  ca.y2 = static_cast<const uint32_t*>(y2);
+  ca.r1 = static_cast<const uint32_t*>(r1);
+  ca.r2 = static_cast<const uint32_t*>(r2);
+  ca.s = static_cast<const uint32_t*>(s);
+  ca.ctx_bytes = static_cast<const uint8_t*>(ctx_bytes);
+  ca.ctx_off = ctx_off;
+  ca.ctx_present = ctx_present;
+  ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->prefix.p);
+  ca.c_out = static_cast<uint32_t*>(ctx->c.p);
+  ca.status_out = status;
+  {
+    StageTimer t(ctx, 0, st);
+    CPZ_HIP(cpz::launch_challenge(ca, st));
+  }
+  cpz::RlcPrepArgs pa;
+  pa.n = (int64_t)n;
+  pa.first_index = first_index;
+  std::memcpy(pa.seed, seed, 32);
+  pa.y1 = ca.y1;
+  pa.y2 = ca.y2;
+  pa.r1 = ca.r1;
+  pa.r2 = ca.r2;
+  pa.s = ca.s;
+  pa.c = ca.c_out;
+  pa.status = status;
+  pa.pts = static_cast<cpz::ge_niels*>(ctx->rl_pts.p);
+  pa.digits = static_cast<int16_t*>(ctx->rl_dig.p);
+  pa.dstride = 4 * ctx->rl_cap + 2;
+  pa.block_sums = static_cast<cpz::sc*>(ctx->rl_bsum.p);
+  {
+    StageTimer t(ctx, 2, st);
+    CPZ_HIP(cpz::launch_rlc_prepare(pa, st));
+  }
+  return CPZ_OK;
+}
+
+// Batch-fail fallback: locate the invalid entries of [lo, hi) exactly.  Sub-ranges whose
+// partial is the identity are accepted (their decode-level statuses are final);
+// failing ones are split in kFanout parts, and a range is verified per proof
+// (k_verify_each) once it is small or most of its parts fail.
+constexpr int64_t kLeaf = 1 << 16;
+constexpr int kFanout = 8;
+
+int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const void* y2, const void* r1, const void* r2,
+                 const void* s, uint8_t* status, hipStream_t st, int depth) {
+  auto per_proof = [&](int64_t a, int64_t b) -> int {
+    cpz::VerifyArgs va;
+    va.n = b - a;
+    va.y1 = static_cast<const uint32_t*>(y1) + 8 * a;
+    va.y2 = static_cast<const uint32_t*>(y2) + 8 * a;
+    va.r1 = static_cast<const uint32_t*>(r1) + 8 * a;
+    va.r2 = static_cast<const uint32_t*>(r2) + 8 * a;
+    va.s = static_cast<const uint32_t*>(s) + 8 * a;
+    va.c = static_cast<const uint32_t*>(ctx->c.p) + 8 * a;
+    va.status = status + a;  // decode-level status in, final status out
+    va.tab = static_cast<const cpz::ge_niels*>(ctx->tab.p);
+    va.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p);
+    const int grid = verify_grid(ctx, (size_t)(b - a));
+    CPZ_HIP(ctx->scratch.ensure((size_t)grid * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached)));
+    va.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p);
+    StageTimer t(ctx, 4, st);
+    CPZ_HIP(cpz::launch_verify_each(va, grid, st));
+    return CPZ_OK;
+  };
+  if (hi - lo <= kLeaf || depth > 12) return per_proof(lo, hi);
+  int64_t cuts[kFanout + 1];
+  for (int k = 0; k <= kFanout; k++) {
+    int64_t c = lo + ((hi - lo) * k) / kFanout;
+    c = (c / cpz::kRlcPrepBlock) * cpz::kRlcPrepBlock;
+    cuts[k] = k == 0 ? lo : (k == kFanout ? hi : (c < lo ? lo : c));
+  }
+  bool fail[kFanout];
+  int nfail = 0;
+  for (int k = 0; k < kFanout; k++) {
+    fail[k] = false;
+    if (cuts[k + 1] <= cuts[k]) continue;
+    uint8_t part[32];
+    int ident = 0;
+    int rc = rlc_range(ctx, cuts[k], cuts[k + 1], st, part, &ident);
+    if (rc) return rc;
+    fail[k] = !ident;
+    nfail += fail[k] ? 1 : 0;
+  }
+  if (2 * nfail > kFanout) return per_proof(lo, hi);  // dense failures: no pruning left
+  for (int k = 0; k < kFanout; k++) {
+    if (!fail[k]) continue;
+    int rc = rlc_fallback(ctx, cuts[k], cuts[k + 1], y1, y2, r1, r2, s, status, st, depth + 1);
+    if (rc) return rc;
+  }
+  return CPZ_OK;
+}
+
+int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
+                      const void* s, const void* cb, const uint64_t* co, const uint8_t* cp, uint8_t* d_status,
+                      const uint8_t seed[32], uint64_t first_index, uint8_t partial_out[32], int* batch_ok,
+                      int fallback, uint8_t* host_status, hipStream_t st) {
+  int rc = rlc_prepare(ctx, n, y1, y2, r1, r2, s, cb, co, cp, d_status, seed, first_index, st);
+  if (rc) return rc;
+  uint8_t part[32];
+  int ident = 0;
+  rc = rlc_range(ctx, 0, (int64_t)n, st, part, &ident);
+  if (rc) return rc;
+  if (partial_out) std::memcpy(partial_out, part, 32);
+  // every entry must also have decoded (zero-weight entries are not "verified")
+  std::vector<uint8_t> hs(n);
+  CPZ_HIP(hipMemcpyAsync(hs.data(), d_status, n, hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipStreamSynchronize(st));
+  bool all_live = true;
+  for (size_t i = 0; i < n; i++) all_live = all_live && hs[i] == 0;
+  if (batch_ok) *batch_ok = (ident && all_live) ? 1 : 0;
+  if (!ident && fallback) {
+    rc = rlc_fallback(ctx, 0, (int64_t)n, y1, y2, r1, r2, s, d_status, st, 0);
+    if (rc) return rc;
+  }
+  if (host_status) {
+    CPZ_HIP(hipMemcpyAsync(host_status, d_status, n, hipMemcpyDeviceToHost, st));
+    CPZ_HIP(hipStreamSynchronize(st));
+  }
+  return CPZ_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -285,6 +491,70 @@ int cpz_ctx_create(int device_ordinal, cpz_ctx** out) {
   }
   ctx->cus = prop.multiProcessorCount;
   *out = ctx;
+  return CPZ_OK;
+}
+
+int cpz_verify_batch(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, const uint8_t* y1,
+                     const uint8_t* y2, const uint8_t* r1, const uint8_t* r2, const uint8_t* s,
+                     const uint8_t* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
+                     const uint8_t seed[32], uint64_t first_index, uint8_t partial_out[32], int* batch_ok,
+                     uint8_t* status_out) {
+  if (!ctx || !g || !h || !seed) return fail(CPZ_EINVAL, "null context, generators or seed");
+  if (n == 0) return fail(CPZ_EEMPTY, "Cannot verify empty batch");
+  if (!y1 || !y2 || !r1 || !r2 || !s) return fail(CPZ_EINVAL, "null input pointer");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  int rc = ensure_generators(ctx, g, h);
+  if (rc) return rc;
+  const uint8_t* host[5] = {y1, y2, r1, r2, s};
+  const void* dev[5];
+  const void* dcb;
+  const uint64_t* dco;
+  const uint8_t* dcp;
+  rc = stage_inputs(ctx, n, host, 5, ctx_bytes, ctx_off, ctx_present, dev, &dcb, &dco, &dcp);
+  if (rc) return rc;
+  CPZ_HIP(ctx->st.ensure(n));
+  return verify_batch_impl(ctx, n, dev[0], dev[1], dev[2], dev[3], dev[4], dcb, dco, dcp,
+                           static_cast<uint8_t*>(ctx->st.p), seed, first_index, partial_out, batch_ok,
+                           status_out != nullptr, status_out, ctx->stream);
+}
+
+int cpz_verify_batch_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, const void* d_y1,
+                            const void* d_y2, const void* d_r1, const void* d_r2, const void* d_s,
+                            const void* d_ctx_bytes, const uint64_t* d_ctx_off, const uint8_t* d_ctx_present,
+                            const uint8_t seed[32], uint64_t first_index, uint8_t partial_out[32], int* batch_ok,
+                            void* d_status_out, int fallback, void* stream) {
+  if (!ctx || !g || !h || !seed) return fail(CPZ_EINVAL, "null context, generators or seed");
+  if (n == 0) return fail(CPZ_EEMPTY, "Cannot verify empty batch");
+  if (!d_y1 || !d_y2 || !d_r1 || !d_r2 || !d_s || !d_status_out) return fail(CPZ_EINVAL, "null input pointer");
+  if (!aligned16(d_y1) || !aligned16(d_y2) || !aligned16(d_r1) || !aligned16(d_r2) || !aligned16(d_s))
+    return fail(CPZ_EINVAL, "device inputs must be 16-byte aligned");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  int rc = ensure_generators(ctx, g, h);
+  if (rc) return rc;
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  return verify_batch_impl(ctx, n, d_y1, d_y2, d_r1, d_r2, d_s, d_ctx_bytes, d_ctx_off, d_ctx_present,
+                           static_cast<uint8_t*>(d_status_out), seed, first_index, partial_out, batch_ok, fallback,
+                           nullptr, st);
+}
+
+int cpz_combine_partials(cpz_ctx* ctx, size_t k, const uint8_t* partials, uint8_t out[32], int* is_identity) {
+  if (!ctx || !partials || !out || k == 0 || k > 4096) return fail(CPZ_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  CPZ_HIP(ctx->rl_parts.ensure(k * 32 + 64));
+  CPZ_HIP(ctx->rl_flags.ensure(4 * sizeof(int)));
+  CPZ_HIP(hipMemcpyAsync(ctx->rl_parts.p, partials, k * 32, hipMemcpyHostToDevice, ctx->stream));
+  uint32_t* outw = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ctx->rl_parts.p) + k * 32);
+  CPZ_HIP(cpz::launch_rlc_combine(static_cast<const uint32_t*>(ctx->rl_parts.p), (int)k, outw,
+                                  static_cast<int*>(ctx->rl_flags.p), ctx->stream));
+  int flags[2];
+  CPZ_HIP(hipMemcpyAsync(out, outw, 32, hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipMemcpyAsync(flags, ctx->rl_flags.p, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipStreamSynchronize(ctx->stream));
+  if (!flags[0]) return fail(CPZ_EINVAL, "a partial does not decode");
+  if (is_identity) *is_identity = flags[1];
   return CPZ_OK;
 }
 
@@ -338,6 +608,10 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->ctxb.release();
   ctx->ctxo.release();
   ctx->ctxp.release();
+  for (DevBuf* b : {&ctx->rl_pts, &ctx->rl_dig, &ctx->rl_bsum, &ctx->rl_counts, &ctx->rl_offsets, &ctx->rl_cursor,
+                    &ctx->rl_idx, &ctx->rl_buckets, &ctx->rl_segs, &ctx->rl_segw, &ctx->rl_win, &ctx->rl_partial,
+                    &ctx->rl_flags, &ctx->rl_parts})
+    b->release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

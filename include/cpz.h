@@ -101,6 +101,36 @@ int cpz_prove_synthetic_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t 
                                const uint8_t *d_ctx_present, void *d_y1, void *d_y2, void *d_r1,
                                void *d_r2, void *d_s, void *stream);
 
+/* Random-linear-combination batch verification (configs C3-C5): one Pippenger MSM checks
+ *   P = sum_i [a_i s_i] g - [a_i] r1_i - [a_i c_i] y1_i + [b_i s_i] h - [b_i] r2_i - [b_i c_i] y2_i == O
+ * -- the reference's verify_batch_equations (batch.rs:271-312) with the equation corrected
+ * (the reference omits alpha on y*c, batch.rs:297-300).  Weights a_i / b_i are the
+ * (first_index + i)-th ChaCha20 keystream blocks of `seed`, stream 0 / 1, reduced wide mod l
+ * (random_scalar, batch.rs:240, ristretto.rs:146-150).
+ *   partial_out  32-byte encoding of P for this batch / shard (identity = 32 zero bytes);
+ *                shards with global first_index values sum to the single-GPU P.
+ *   batch_ok     1 iff every entry decodes and P is the identity.
+ *   status_out   optional (n): exact per-entry statuses.  When the batch fails, a fallback
+ *                search (sub-range RLC partials, per-proof verification at the leaves)
+ *                locates the invalid entries (verify_individually, batch.rs:314-318).
+ * The _device form takes device-resident inputs and always needs d_status_out (decode-level
+ * statuses, or exact ones when fallback != 0); it synchronises `stream`. */
+int cpz_verify_batch(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                     const uint8_t *y1, const uint8_t *y2, const uint8_t *r1, const uint8_t *r2,
+                     const uint8_t *s, const uint8_t *ctx_bytes, const uint64_t *ctx_off,
+                     const uint8_t *ctx_present, const uint8_t seed[32], uint64_t first_index,
+                     uint8_t partial_out[32], int *batch_ok, uint8_t *status_out);
+int cpz_verify_batch_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                            const void *d_y1, const void *d_y2, const void *d_r1, const void *d_r2,
+                            const void *d_s, const void *d_ctx_bytes, const uint64_t *d_ctx_off,
+                            const uint8_t *d_ctx_present, const uint8_t seed[32], uint64_t first_index,
+                            uint8_t partial_out[32], int *batch_ok, void *d_status_out, int fallback,
+                            void *stream);
+
+/* Sum k 32-byte partials (per-GPU shards) on the device: out = encoding of the sum,
+ * *is_identity = 1 iff the combined batch equation holds. */
+int cpz_combine_partials(cpz_ctx *ctx, size_t k, const uint8_t *partials, uint8_t out[32], int *is_identity);
+
 /* Per-kernel timing (HIP events recorded on the launch stream around every kernel).
  * Stages: 0 = k_challenge, 1 = k_verify_each, 2 = RLC decode/weights, 3 = RLC MSM,
  * 4 = fallback.  cpz_ctx_stage_times synchronises, writes the summed milliseconds and

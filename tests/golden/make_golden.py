@@ -210,6 +210,34 @@ def main():
     out["weights"] = [{"index": i, "alpha": O.scalar_bytes(O.batch_weight(wseed, i)).hex(),
                        "gamma": O.scalar_bytes(O.batch_weight2(wseed, i)).hex()} for i in (0, 1, 2, 63, 1 << 20)]
 
+    # 7. RLC partials (corrected batch equation, the MSM the GPU runs) for fixed seeds:
+    #    all-valid batches are the identity; forged / malformed entries make a specific point;
+    #    shards keyed by global index sum to the whole.
+    rseed = hashlib.sha256(b"cpz-rlc-golden").digest()
+    valid = [r for r, p in zip(recs, proofs[:48]) if r.ctx is None][:12]
+    def prs(rs):
+        return [rec_json(r, 0) for r in rs]
+    rlc = []
+    P = O.rlc_partial(valid, rseed)
+    assert O.pt_is_identity(P)
+    rlc.append({"name": "valid12", "seed": rseed.hex(), "first_index": 0, "proofs": prs(valid),
+                "partial": O.ristretto_encode(P).hex(), "identity": True})
+    forged_set = list(valid)
+    forged_set[3] = O.ProofRecord(valid[3].y1, valid[3].y2, valid[3].r1, valid[3].r2,
+                                  O.scalar_bytes(int.from_bytes(valid[3].s, "little") + 1))
+    forged_set[7] = O.ProofRecord(valid[8].y1, valid[8].y2, valid[7].r1, valid[7].r2, valid[7].s)
+    forged_set[9] = O.ProofRecord(valid[9].y1, valid[9].y2, bytes.fromhex(RFC_BAD[5]), valid[9].r2, valid[9].s)
+    P = O.rlc_partial(forged_set, rseed, 5)
+    P0 = O.rlc_partial(forged_set[:6], rseed, 5)
+    P1 = O.rlc_partial(forged_set[6:], rseed, 11)
+    assert O.pt_eq(O.pt_add(P0, P1), P) and not O.pt_is_identity(P)
+    rlc.append({"name": "forged12", "seed": rseed.hex(), "first_index": 5, "proofs": prs(forged_set),
+                "partial": O.ristretto_encode(P).hex(), "identity": False,
+                "shards": [{"lo": 0, "hi": 6, "first_index": 5, "partial": O.ristretto_encode(P0).hex()},
+                           {"lo": 6, "hi": 12, "first_index": 11, "partial": O.ristretto_encode(P1).hex()}],
+                "statuses": [O.verify_one(r) for r in forged_set]})
+    out["rlc"] = rlc
+
     path = os.path.join(HERE, "golden.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)

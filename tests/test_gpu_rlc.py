@@ -1,0 +1,127 @@
+"""GPU parity for the random-linear-combination batch path (configs C3-C5):
+Pippenger partials bit-exact against the oracle's corrected RLC (pyoracle.rlc_partial),
+shard partials keyed by global index summing to the whole (the multi-GPU invariant),
+and the batch-fail fallback locating exactly the invalid entries (verify_individually,
+batch.rs:314-318)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _arr(ps, k):
+    return np.frombuffer(b"".join(bytes.fromhex(p[k]) for p in ps), np.uint8).reshape(-1, 32)
+
+
+def test_rlc_golden_partials_and_statuses(gpu, golden):
+    for case in golden["rlc"]:
+        ps = case["proofs"]
+        args = [_arr(ps, k) for k in ("y1", "y2", "r1", "r2", "s")]
+        seed = bytes.fromhex(case["seed"])
+        partial, ok, st = gpu.verify_batch(*args, seed=seed, first_index=case["first_index"])
+        assert partial.hex() == case["partial"], case["name"]
+        assert ok == case["identity"]
+        if "statuses" in case:
+            assert list(st) == case["statuses"]
+        else:
+            assert not st.any()
+        parts = []
+        for sh in case.get("shards", []):
+            sub = [a[sh["lo"]:sh["hi"]] for a in args]
+            p, _, _ = gpu.verify_batch(*sub, seed=seed, first_index=sh["first_index"], statuses=False)
+            assert p.hex() == sh["partial"]
+            parts.append(p)
+        if parts:
+            total, ident = gpu.combine_partials(parts)
+            assert total.hex() == case["partial"] and ident == case["identity"]
+
+
+def _synthetic(gpu, torch, n, first=0):
+    sx = hashlib.sha256(b"cpz-bench-x").digest()
+    sk = hashlib.sha256(b"cpz-bench-k").digest()
+    dev = torch.device("cuda:0")
+    t = {k: torch.empty((n, 32), dtype=torch.uint8, device=dev) for k in ("y1", "y2", "r1", "r2", "s")}
+    gpu.prove_synthetic_device(n, sx, sk, t["y1"], t["y2"], t["r1"], t["r2"], t["s"], first_index=first)
+    return t
+
+
+def _bump_s(t, torch, idx):
+    s_host = t["s"].cpu().numpy().copy()
+    for i in idx:
+        v = (int.from_bytes(s_host[i].tobytes(), "little") + 1) % O.L
+        s_host[i] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)
+    t["s"].copy_(torch.from_numpy(s_host))
+
+
+def test_rlc_scale_valid_forged_fallback_and_shards(gpu):
+    torch = pytest.importorskip("torch")
+    n = 1 << 17
+    seed = hashlib.sha256(b"cpz-weights-v1").digest()
+    t = _synthetic(gpu, torch, n)
+    st = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    partial, ok = gpu.verify_batch_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], st, seed)
+    assert ok and partial == bytes(32) and int(st.sum().item()) == 0
+    # shard invariant: halves keyed by global index sum to the whole (identity here)
+    h = n // 2
+    halves = []
+    for lo, hi in ((0, h), (h, n)):
+        sub = {k: v[lo:hi] for k, v in t.items()}
+        p, okh = gpu.verify_batch_device(sub["y1"], sub["y2"], sub["r1"], sub["r2"], sub["s"], st[lo:hi], seed,
+                                         first_index=lo)
+        assert okh
+        halves.append(p)
+    assert gpu.combine_partials(halves) == (bytes(32), True)
+    # 0.5 % forged: batch fails, fallback returns exactly the forged set
+    rng = np.random.default_rng(99)
+    idx = np.sort(rng.choice(n, size=n // 200, replace=False))
+    _bump_s(t, torch, idx)
+    partial, ok = gpu.verify_batch_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], st, seed, fallback=True)
+    assert not ok and partial != bytes(32)
+    got = np.nonzero(st.cpu().numpy())[0]
+    assert np.array_equal(got, idx) and set(st.cpu().numpy()[idx].tolist()) == {1}
+    # forged shards: partials still sum to the whole-batch partial
+    halves = []
+    for lo, hi in ((0, h), (h, n)):
+        sub = {k: v[lo:hi] for k, v in t.items()}
+        p, _ = gpu.verify_batch_device(sub["y1"], sub["y2"], sub["r1"], sub["r2"], sub["s"], st[lo:hi], seed,
+                                       first_index=lo)
+        halves.append(p)
+    total, ident = gpu.combine_partials(halves)
+    assert total == partial and not ident
+
+
+def test_rlc_single_forgery_bisection(gpu):
+    """One bad proof in 2^18: the fallback must prune with sub-range partials (bisection)
+    and still return exactly that index."""
+    torch = pytest.importorskip("torch")
+    n = 1 << 18
+    seed = hashlib.sha256(b"cpz-weights-v1").digest()
+    t = _synthetic(gpu, torch, n, first=1 << 20)
+    bad = 200_003
+    _bump_s(t, torch, [bad])
+    st = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    gpu.set_timing(True)
+    gpu.stage_times()
+    partial, ok = gpu.verify_batch_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], st, seed, fallback=True)
+    stages = gpu.stage_times()
+    gpu.set_timing(False)
+    assert not ok
+    assert np.nonzero(st.cpu().numpy())[0].tolist() == [bad]
+    # bisection ran several sub-range MSMs and verified only a leaf per proof
+    assert stages["rlc_msm"][1] > 1
+    assert stages.get("fallback", (0, 0))[1] >= 1
+
+
+def test_rlc_decode_failures_zero_weight(gpu, golden):
+    ps = [p for p in golden["proofs"] if p["kind"] == "valid"][:6]
+    ps = ps + [p for p in golden["proofs"] if p["kind"].startswith("bad_r1")][:1]
+    args = [_arr(ps, k) for k in ("y1", "y2", "r1", "r2", "s")]
+    ctxs = [None if p["ctx"] is None else bytes.fromhex(p["ctx"]) for p in ps]
+    partial, ok, st = gpu.verify_batch(*args, seed=b"\x01" * 32, contexts=ctxs)
+    assert partial == bytes(32)          # the undecodable entry carries zero weight
+    assert not ok                         # ... but the batch is not "all verified"
+    assert list(st) == [p["status"] for p in ps]
