@@ -59,6 +59,13 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = min(16, cpus))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=("each", "rlc"), default="each",
+                    help="each: per-proof verification (configs[1], the headline); rlc: random-linear-"
+                         "combination batch check via Pippenger MSM (configs[2]/[3]: per-rank partials, "
+                         "all-gather of 32-B partials, combine)")
+    ap.add_argument("--rlc-extra", type=int, default=1,
+                    help="at N=1 in 'each' mode also time the RLC batch path on the same proofs (reported "
+                         "under 'rlc', not in value)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -85,8 +92,24 @@ def main():
                                first_index=rank * n, stream=stream)
     torch.cuda.synchronize(dev)
 
-    def step():
+    weight_seed = hashlib.sha256(b"cpz-weights-v1").digest()
+    from chaum_pedersen.shard import all_gather_partials
+
+    def step_each():
         gpu.verify_each_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status, stream=stream)
+
+    rlc_state = {"ok": True}
+
+    def step_rlc():
+        partial, ok = gpu.verify_batch_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status, weight_seed,
+                                              first_index=rank * n, stream=stream)
+        if world > 1:
+            parts = all_gather_partials(partial)
+            total, ident = gpu.combine_partials(parts)
+            ok = ok and ident and total == bytes(32)
+        rlc_state["ok"] = rlc_state["ok"] and ok
+
+    step = step_each if args.mode == "each" else step_rlc
 
     for _ in range(args.warmup):
         step()
@@ -115,8 +138,28 @@ def main():
         elapsed = float(tt.item())
     # the timed steps must also have verified everything
     n_bad = int((status != 0).sum().item())
-    if n_bad:
+    if n_bad or not rlc_state["ok"]:
         raise SystemExit("bench: %d proofs rejected in the timed region" % n_bad)
+
+    rlc_extra = None
+    if args.mode == "each" and world == 1 and args.rlc_extra:
+        for _ in range(2):
+            step_rlc()
+        gpu.set_timing(True)
+        gpu.stage_times()
+        torch.cuda.synchronize(dev)
+        r0 = time.perf_counter()
+        for _ in range(args.steps):
+            step_rlc()
+        torch.cuda.synchronize(dev)
+        r_el = time.perf_counter() - r0
+        r_st = gpu.stage_times()
+        gpu.set_timing(False)
+        if not rlc_state["ok"]:
+            raise SystemExit("bench: RLC batch check rejected a valid batch")
+        rlc_extra = {"workload": "configs[2]: RLC batch check of the same 2^20 proofs (Pippenger, 16-bit windows)",
+                     "proofs_per_s": n * args.steps / r_el, "ms_per_step": r_el * 1e3 / args.steps,
+                     "kernel_ms_per_step": {k: v[0] / args.steps for k, v in r_st.items()}}
 
     total = world * n * args.steps
     value = total / elapsed
@@ -171,6 +214,12 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if args.mode == "rlc":
+            line["config"]["workload"] = ("configs[2]/[3]: RLC batch check via Pippenger MSM, 2^20 proofs per GPU, "
+                                          "per-rank 32-B partial + all-gather + combine")
+            line["roofline"] = None
+        if rlc_extra:
+            line["rlc"] = rlc_extra
         print(json.dumps(line), flush=True)
     gpu.close()
     if world > 1:
