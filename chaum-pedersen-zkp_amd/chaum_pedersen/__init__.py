@@ -321,6 +321,14 @@ class Gpu:
             status_out.data_ptr(), 1 if fallback else 0, stream))
         return partial.raw, bool(ok.value)
 
+    def msm(self, points: Sequence[bytes], scalars: Sequence[int]) -> bytes:
+        """enc(sum [k_j] P_j) through the Pippenger kernels (cpz_msm)."""
+        pb = b"".join(bytes(p) for p in points)
+        sb = b"".join(int(k).to_bytes(32, "little") for k in scalars)
+        out = ctypes.create_string_buffer(32)
+        _native.check(self._lib.cpz_msm(self._h, len(points), pb, sb, out))
+        return out.raw
+
     def combine_partials(self, partials: Sequence[bytes]):
         """(sum encoding, is_identity) of per-shard partials (cpz_combine_partials)."""
         blob = b"".join(bytes(p) for p in partials)

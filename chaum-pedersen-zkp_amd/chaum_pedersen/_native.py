@@ -29,7 +29,7 @@ EXPORTED = (
     "cpz_device_count", "cpz_ctx_create", "cpz_ctx_destroy", "cpz_last_error",
     "cpz_default_generators", "cpz_verify_each", "cpz_verify_each_device", "cpz_challenges",
     "cpz_prove_synthetic", "cpz_prove_synthetic_device", "cpz_ctx_set_timing", "cpz_ctx_stage_times",
-    "cpz_verify_batch", "cpz_verify_batch_device", "cpz_combine_partials",
+    "cpz_verify_batch", "cpz_verify_batch_device", "cpz_combine_partials", "cpz_msm",
 )
 NUM_STAGES = 8
 
@@ -77,6 +77,8 @@ def _declare(lib):
     lib.cpz_verify_batch_device.restype = ctypes.c_int
     lib.cpz_verify_batch_device.argtypes = ([_p, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p, _p, _p,
                                             ctypes.c_uint64, _p, ctypes.POINTER(ctypes.c_int), _p, ctypes.c_int, _p])
+    lib.cpz_msm.restype = ctypes.c_int
+    lib.cpz_msm.argtypes = [_p, ctypes.c_size_t, _p, _p, _p]
     lib.cpz_combine_partials.restype = ctypes.c_int
     lib.cpz_combine_partials.argtypes = [_p, ctypes.c_size_t, _p, _p, ctypes.POINTER(ctypes.c_int)]
     lib.cpz_prove_synthetic_device.restype = ctypes.c_int

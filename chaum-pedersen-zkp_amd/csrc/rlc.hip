@@ -407,6 +407,25 @@ __global__ void __launch_bounds__(64) k_rlc_final(RlcMsmArgs a) {
   }
 }
 
+// Generic MSM input: decode point j, store its Niels form and the digits of scalar j.
+__global__ void __launch_bounds__(256) k_msm_load(int64_t n, const uint32_t* __restrict__ pts_enc,
+                                                  const uint32_t* __restrict__ scalars, ge_niels* __restrict__ pts,
+                                                  int16_t* __restrict__ digits, int64_t dstride, int* __restrict__ bad) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  uint32_t w[8];
+  rlc_load8(w, pts_enc, j);
+  ge_p3 P;
+  const bool ok = ristretto_decode(P, w);
+  if (!ok) atomicOr(bad, 1);
+  store_niels(pts + j, niels_from_p3_affine(P, false));
+  rlc_load8(w, scalars, j);
+  int16_t d[kRlcWindows];
+  recode16(d, w);
+#pragma unroll
+  for (int wv = 0; wv < kRlcWindows; wv++) digits[(int64_t)wv * dstride + j] = d[wv];
+}
+
 // Sum of k encoded partials (multi-GPU / fallback combine).
 __global__ void k_rlc_combine(const uint32_t* __restrict__ parts, int k, uint32_t* __restrict__ out,
                               int* __restrict__ flags) {
@@ -463,6 +482,13 @@ hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0,
   hipLaunchKernelGGL(k_rlc_window, dim3(kRlcWindows), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_rlc_final, dim3(1), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_msm_load(int64_t n, const uint32_t* pts_enc, const uint32_t* scalars, ge_niels* pts,
+                           int16_t* digits, int64_t dstride, int* bad, hipStream_t st) {
+  hipLaunchKernelGGL(k_msm_load, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, pts_enc, scalars, pts, digits,
+                     dstride, bad);
   return hipGetLastError();
 }
 

@@ -539,6 +539,43 @@ int cpz_verify_batch_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[3
                            nullptr, st);
 }
 
+int cpz_msm(cpz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalars, uint8_t out[32]) {
+  if (!ctx || !points || !scalars || !out || n == 0) return fail(CPZ_EINVAL, "bad arguments");
+  for (size_t j = 0; j < n; j++)
+    if (scalars[32 * j + 31] & 0xe0) return fail(CPZ_EINVAL, "scalars must be below 2^253");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  static const uint8_t zero[32] = {0};
+  uint8_t g[32], h[32];
+  cpz_default_generators(g, h);
+  int rc = ctx->have_gh ? CPZ_OK : ensure_generators(ctx, g, h);
+  if (rc) return rc;
+  const int64_t nproofs = (int64_t)(n + 3) / 4;
+  rc = rlc_reserve(ctx, nproofs);
+  if (rc) return rc;
+  CPZ_HIP(ctx->in[0].ensure(n * 32));
+  CPZ_HIP(ctx->in[1].ensure(n * 32));
+  CPZ_HIP(hipMemcpyAsync(ctx->in[0].p, points, n * 32, hipMemcpyHostToDevice, ctx->stream));
+  CPZ_HIP(hipMemcpyAsync(ctx->in[1].p, scalars, n * 32, hipMemcpyHostToDevice, ctx->stream));
+  CPZ_HIP(hipMemsetAsync(ctx->rl_flags.p, 0, 4 * sizeof(int), ctx->stream));
+  cpz::RlcMsmArgs m = rlc_msm_args(ctx, 0, 0);
+  m.p0 = 0;
+  m.p1 = (int64_t)n;
+  CPZ_HIP(cpz::launch_msm_load((int64_t)n, static_cast<const uint32_t*>(ctx->in[0].p),
+                               static_cast<const uint32_t*>(ctx->in[1].p), m.pts, m.digits, m.dstride,
+                               static_cast<int*>(ctx->rl_flags.p) + 2, ctx->stream));
+  (void)zero;
+  // extra points get zero scalars (empty block range)
+  CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_bsum.p), 0, 0,
+                              static_cast<const cpz::ge_niels*>(ctx->tab.p), 1, ctx->stream));
+  int flags[3];
+  CPZ_HIP(hipMemcpyAsync(out, ctx->rl_partial.p, 32, hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipMemcpyAsync(flags, ctx->rl_flags.p, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipStreamSynchronize(ctx->stream));
+  if (flags[2]) return fail(CPZ_EINVAL, "a point does not decode");
+  return CPZ_OK;
+}
+
 int cpz_combine_partials(cpz_ctx* ctx, size_t k, const uint8_t* partials, uint8_t out[32], int* is_identity) {
   if (!ctx || !partials || !out || k == 0 || k > 4096) return fail(CPZ_EINVAL, "bad arguments");
   std::lock_guard<std::mutex> lock(ctx->mu);

@@ -127,6 +127,11 @@ int cpz_verify_batch_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[3
                             uint8_t partial_out[32], int *batch_ok, void *d_status_out, int fallback,
                             void *stream);
 
+/* Multi-scalar multiplication through the same Pippenger kernels: out = enc(sum_j [k_j] P_j)
+ * for n encoded points and n scalars (little-endian, < 2^253).  Exposed for testing the MSM
+ * against the oracle with adversarial digit patterns. */
+int cpz_msm(cpz_ctx *ctx, size_t n, const uint8_t *points, const uint8_t *scalars, uint8_t out[32]);
+
 /* Sum k 32-byte partials (per-GPU shards) on the device: out = encoding of the sum,
  * *is_identity = 1 iff the combined batch equation holds. */
 int cpz_combine_partials(cpz_ctx *ctx, size_t k, const uint8_t *partials, uint8_t out[32], int *is_identity);
