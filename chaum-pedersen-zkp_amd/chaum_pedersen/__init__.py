@@ -223,6 +223,15 @@ def _ptr(a) -> Optional[int]:
     return None if a is None else a.ctypes.data
 
 
+def _torch_stream(stream):
+    """Device entry points default to torch's current stream, so kernels are ordered with
+    the torch ops that produce / consume the tensors."""
+    if stream is not None:
+        return stream
+    import torch
+    return torch.cuda.current_stream().cuda_stream
+
+
 class Gpu:
     """A verifier context on one GPU (cpz_ctx).  Bulk entry points, no batch cap."""
 
@@ -318,7 +327,7 @@ class Gpu:
         _native.check(self._lib.cpz_verify_batch_device(
             self._h, params.g, params.h, int(y1.shape[0]), y1.data_ptr(), y2.data_ptr(), r1.data_ptr(),
             r2.data_ptr(), s.data_ptr(), None, None, None, bytes(seed), first_index, partial, ctypes.byref(ok),
-            status_out.data_ptr(), 1 if fallback else 0, stream))
+            status_out.data_ptr(), 1 if fallback else 0, _torch_stream(stream)))
         return partial.raw, bool(ok.value)
 
     def msm(self, points: Sequence[bytes], scalars: Sequence[int]) -> bytes:
@@ -357,14 +366,14 @@ class Gpu:
         dp = lambda t: None if t is None else t.data_ptr()
         _native.check(self._lib.cpz_verify_each_device(
             self._h, params.g, params.h, n, dp(y1), dp(y2), dp(r1), dp(r2), dp(s), dp(ctx_bytes), dp(ctx_off),
-            dp(ctx_present), dp(status_out), stream))
+            dp(ctx_present), dp(status_out), _torch_stream(stream)))
 
     def prove_synthetic_device(self, n: int, seed_x: bytes, seed_k: bytes, y1, y2, r1, r2, s, first_index: int = 0,
                                params: Optional[Parameters] = None, stream: Optional[int] = None) -> None:
         params = params or Parameters()
         _native.check(self._lib.cpz_prove_synthetic_device(
             self._h, params.g, params.h, n, first_index, bytes(seed_x), bytes(seed_k), None, None, None,
-            y1.data_ptr(), y2.data_ptr(), r1.data_ptr(), r2.data_ptr(), s.data_ptr(), stream))
+            y1.data_ptr(), y2.data_ptr(), r1.data_ptr(), r2.data_ptr(), s.data_ptr(), _torch_stream(stream)))
 
 
 _default_gpu: Optional[Gpu] = None

@@ -25,7 +25,12 @@ struct ge_p2 { fe X, Y, Z; };
 struct ge_p3 { fe X, Y, Z, T; };
 struct ge_p1p1 { fe X, Y, Z, T; };
 struct ge_cached { fe YpX, YmX, Z, T2d; };
-struct ge_niels { fe ypx, ymx, xy2d; };
+struct ge_niels {
+  fe ypx, ymx, xy2d;
+  int32_t pad[2];  // 128 B: whole 16-byte vectors for loads/stores
+};
+static_assert(sizeof(ge_niels) % 16 == 0, "ge_niels must be a whole number of 16-byte vectors");
+static_assert(sizeof(ge_p3) % 16 == 0 && sizeof(ge_cached) % 16 == 0, "16-byte vector copies");
 
 CPZ_HD ge_p3 ge_identity() {
   ge_p3 r;

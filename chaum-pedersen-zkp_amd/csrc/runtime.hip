@@ -447,6 +447,7 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
   if (!ident && fallback) {
     rc = rlc_fallback(ctx, 0, (int64_t)n, y1, y2, r1, r2, s, d_status, st, 0);
     if (rc) return rc;
+    CPZ_HIP(hipStreamSynchronize(st));  // statuses complete on return (documented)
   }
   if (host_status) {
     CPZ_HIP(hipMemcpyAsync(host_status, d_status, n, hipMemcpyDeviceToHost, st));
@@ -484,7 +485,10 @@ int cpz_ctx_create(int device_ordinal, cpz_ctx** out) {
   ctx->device = device_ordinal;
   hipDeviceProp_t prop;
   hipError_t e = hipGetDeviceProperties(&prop, device_ordinal);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  // A blocking stream: it orders with the legacy default stream, so work queued by other
+  // libraries (e.g. torch's default stream, handle 0, which the C ABI reads as "use the
+  // context stream") is ordered with the verifier's kernels in both directions.
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault);
   if (e != hipSuccess) {
     delete ctx;
     return fail(CPZ_EHIP, std::string("context setup: ") + hipGetErrorString(e));

@@ -75,7 +75,8 @@ int cpz_verify_each(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size
                     const uint8_t *ctx_present, uint8_t *status_out);
 
 /* Same with device-resident, 16-byte aligned inputs/outputs, enqueued on `stream`
- * (a hipStream_t, or NULL for the context's own stream).  Does not synchronise. */
+ * (a hipStream_t, or NULL for the context's own stream, which is a blocking stream and so
+ * is ordered with the legacy default stream).  Does not synchronise. */
 int cpz_verify_each_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
                            const void *d_y1, const void *d_y2, const void *d_r1, const void *d_r2,
                            const void *d_s, const void *d_ctx_bytes, const uint64_t *d_ctx_off,
