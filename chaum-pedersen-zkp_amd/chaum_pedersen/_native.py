@@ -10,7 +10,7 @@ import os
 import threading
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libcpz.so")
+LIB_PATH = os.environ.get("CPZ_LIB") or os.path.join(_PKG_ROOT, "lib", "libcpz.so")
 
 CPZ_OK = 0
 CPZ_EINVAL = -1

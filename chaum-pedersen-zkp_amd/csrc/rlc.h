@@ -13,6 +13,8 @@ constexpr int kRlcBuckets = 1 << 15;     // |digit| in [1, 2^15]
 constexpr int kRlcSegLen = 32;           // buckets per reduction segment
 constexpr int kRlcPrepBlock = 256;       // proofs per prepare block (= block_sums granule)
 constexpr int kRlcSortBlock = 1024;
+constexpr int kRlcSortGroups = 64;      // max blocks per window in the counting sort
+constexpr int64_t kRlcSortChunk = 1 << 16;  // target points per sort block
 constexpr int kNielsEntriesRlc = kTableB;
 
 struct RlcPrepArgs {
@@ -30,6 +32,7 @@ struct RlcPrepArgs {
   int16_t* digits;               // [16][dstride] signed radix-2^16 digits
   int64_t dstride;
   sc* block_sums;                // [ceil(n/256)][2]
+  int* any_bad;                  // set to 1 if some proof has a non-zero decode-level status
 };
 
 struct RlcMsmArgs {
@@ -40,7 +43,9 @@ struct RlcMsmArgs {
   int64_t dstride;
   uint32_t* counts;              // [16][2^15]
   uint32_t* offsets;             // [16][2^15 + 1]
-  uint32_t* cursor;              // [16][2^15]
+  uint32_t* bhist;               // [16][groups][2^15] per-sort-block histograms -> block bases
+  int groups;                    // sort blocks per window
+  int64_t chunk;                 // points per sort block
   uint32_t* idx;                 // [16][istride]
   int64_t istride;
   ge_p3* buckets;                // [16][2^15]
@@ -52,8 +57,10 @@ struct RlcMsmArgs {
 };
 
 hipError_t launch_rlc_prepare(const RlcPrepArgs& a, hipStream_t st);
+// Sort geometry for `npts` MSM points: sets a.groups / a.chunk.
+void rlc_sort_geometry(RlcMsmArgs& a, int64_t npts);
 hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0, int64_t b1, const ge_niels* tab,
-                          int sort_blocks, hipStream_t st);
+                          hipStream_t st);
 hipError_t launch_msm_load(int64_t n, const uint32_t* pts_enc, const uint32_t* scalars, ge_niels* pts,
                            int16_t* digits, int64_t dstride, int* bad, hipStream_t st);
 hipError_t launch_rlc_combine(const uint32_t* parts, int k, uint32_t* out, int* flags, hipStream_t st);

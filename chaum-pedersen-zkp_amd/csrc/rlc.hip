@@ -15,9 +15,10 @@
 //                   affine-Niels points, signed radix-2^16 digits (16 windows), per-block
 //                   sums of a_i s_i and b_i s_i.
 //   k_rlc_extra     g and h as two more MSM points with the summed scalars.
-//   k_rlc_hist      per-window bucket histogram (LDS-privatised, 32768 buckets).
+//   k_rlc_hist      per-(chunk, window) bucket histograms (LDS, 32768 buckets).
+//   k_rlc_bscan     per-bucket prefix over chunks; bucket totals.
 //   k_rlc_scan      exclusive scan -> bucket offsets.
-//   k_rlc_scatter   point ids sorted by bucket (counting sort).
+//   k_rlc_scatter   point ids sorted by bucket (counting sort, LDS cursors).
 //   k_rlc_bucket    1 thread / (window, bucket): mixed additions over its list.
 //   k_rlc_segment   1 thread / (window, 32-bucket segment): running sums.
 //   k_rlc_window    1 block / window: sum_b b * B_b from the segments (LDS tree).
@@ -91,7 +92,10 @@ __device__ __forceinline__ ge_p3 load_p3(const ge_p3* src) {
 // ---------------------------------------------------------------------------------------
 // k_rlc_prepare
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(kRlcPrepBlock) k_rlc_prepare(RlcPrepArgs a) {
+// Points are decoded one at a time and written out immediately (register pressure: one
+// decoded point live, not four).  A proof that turns out not to be live afterwards gets
+// all its digits zeroed, so its (possibly garbage) Niels entries never enter a bucket.
+__global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_prepare(RlcPrepArgs a) {
   __shared__ sc red_a[kRlcPrepBlock];
   __shared__ sc red_b[kRlcPrepBlock];
   const int64_t i = (int64_t)blockIdx.x * kRlcPrepBlock + threadIdx.x;
@@ -99,18 +103,33 @@ __global__ void __launch_bounds__(kRlcPrepBlock) k_rlc_prepare(RlcPrepArgs a) {
 #pragma unroll
   for (int k = 0; k < 8; k++) { as.w[k] = 0; bs.w[k] = 0; }
   if (i < a.n) {
-    uint32_t w[8];
-    ge_p3 Y1, Y2, R1, R2;
-    rlc_load8(w, a.y1, i);
-    bool ok = ristretto_decode(Y1, w);
-    rlc_load8(w, a.y2, i);
-    ok = ristretto_decode(Y2, w) && ok;
-    rlc_load8(w, a.r1, i);
-    bool ident = words8_zero(w);
-    ok = ristretto_decode(R1, w) && ok;
-    rlc_load8(w, a.r2, i);
-    ident = words8_zero(w) || ident;
-    ok = ristretto_decode(R2, w) && ok;
+    // weights (batch.rs:240 random_scalar, here ChaCha20Rng-keyed by the seed)
+    uint32_t blk[16];
+    chacha20_block(blk, a.seed, a.first_index + (uint64_t)i, 0);
+    const sc wa = sc_reduce_wide(blk);
+    chacha20_block(blk, a.seed, a.first_index + (uint64_t)i, 1);
+    const sc wb = sc_reduce_wide(blk);
+    sc c;
+    rlc_load8(c.w, a.c, i);
+    bool ok = true, ident = false;
+    // q = 0: -r1 (a), 1: -y1 (a c), 2: -r2 (b), 3: -y2 (b c)
+#pragma unroll 1
+    for (int q = 0; q < 4; q++) {
+      const uint32_t* src = q == 0 ? a.r1 : (q == 1 ? a.y1 : (q == 2 ? a.r2 : a.y2));
+      uint32_t w[8];
+      rlc_load8(w, src, i);
+      if (!(q & 1)) ident = words8_zero(w) || ident;
+      ge_p3 P;
+      ok = ristretto_decode(P, w) && ok;
+      const int64_t j = 4 * i + q;
+      store_niels(a.pts + j, niels_from_p3_affine(P, true));
+      sc k = q < 2 ? wa : wb;
+      if (q & 1) k = sc_mul(k, c);
+      int16_t d[kRlcWindows];
+      recode16(d, k.w);
+#pragma unroll
+      for (int wv = 0; wv < kRlcWindows; wv++) a.digits[(int64_t)wv * a.dstride + j] = d[wv];
+    }
     const uint8_t st_s = a.status[i];
     uint8_t st;
     if (!ok) st = kStBadPoint;
@@ -118,35 +137,16 @@ __global__ void __launch_bounds__(kRlcPrepBlock) k_rlc_prepare(RlcPrepArgs a) {
     else if (ident || st_s == kStIdentityOrZero) st = kStIdentityOrZero;
     else st = kStOk;
     a.status[i] = st;
-    const bool live = (st == kStOk);
-
-    // weights (batch.rs:240 random_scalar, here ChaCha20Rng-keyed by the seed)
-    uint32_t blk[16];
-    chacha20_block(blk, a.seed, a.first_index + (uint64_t)i, 0);
-    const sc wa = sc_reduce_wide(blk);
-    chacha20_block(blk, a.seed, a.first_index + (uint64_t)i, 1);
-    const sc wb = sc_reduce_wide(blk);
-    sc c, s;
-    rlc_load8(c.w, a.c, i);
-    rlc_load8(s.w, a.s, i);
-    sc k[4];
-    k[0] = wa;              // -r1
-    k[1] = sc_mul(wa, c);   // -y1
-    k[2] = wb;              // -r2
-    k[3] = sc_mul(wb, c);   // -y2
-    if (live) {
+    if (st == kStOk) {
+      sc s;
+      rlc_load8(s.w, a.s, i);
       as = sc_mul(wa, s);
       bs = sc_mul(wb, s);
-    }
-    const ge_p3* P[4] = {&R1, &Y1, &R2, &Y2};
+    } else {
+      atomicOr(a.any_bad, 1);
+      for (int q = 0; q < 4; q++)
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int64_t j = 4 * i + q;
-      store_niels(a.pts + j, live ? niels_from_p3_affine(*P[q], true) : ge_niels_identity());
-      int16_t d[kRlcWindows];
-      recode16(d, k[q].w);
-#pragma unroll
-      for (int wv = 0; wv < kRlcWindows; wv++) a.digits[(int64_t)wv * a.dstride + j] = live ? d[wv] : (int16_t)0;
+        for (int wv = 0; wv < kRlcWindows; wv++) a.digits[(int64_t)wv * a.dstride + 4 * i + q] = 0;
     }
   }
   // block sums of a_i s_i, b_i s_i (mod l)
@@ -208,26 +208,49 @@ __device__ __forceinline__ int64_t msm_point(const RlcMsmArgs& a, int64_t t) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Counting sort by bucket, per window.
+// Counting sort by bucket, per window, without global atomics.  Window w's points are cut
+// into `groups` chunks; sort block (g, w) owns chunk g:
+//   k_rlc_hist     LDS histogram of its chunk -> bhist[w][g][*]
+//   k_rlc_bscan    per (w, b): exclusive prefix of bhist[w][*][b] over g, total -> counts
+//   k_rlc_scan     per w: exclusive scan of counts over b -> offsets
+//   k_rlc_scatter  LDS cursors = offsets + block prefix; ranks from LDS atomics
+// The order of points inside a bucket is not fixed, which does not matter: the bucket
+// sum is the same group element whatever the order.
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_hist(RlcMsmArgs a) {
-  extern __shared__ uint32_t hist[];  // kRlcBuckets counters
-  const int w = blockIdx.y;
+  extern __shared__ uint32_t hist[];  // kRlcBuckets counters (128 KB)
+  const int g = blockIdx.x, w = blockIdx.y;
   for (int b = threadIdx.x; b < kRlcBuckets; b += kRlcSortBlock) hist[b] = 0;
   __syncthreads();
   const int64_t total = (a.p1 - a.p0) + 2;
+  const int64_t t0 = (int64_t)g * a.chunk;
+  const int64_t t1 = t0 + a.chunk < total ? t0 + a.chunk : total;
   const int16_t* dig = a.digits + (int64_t)w * a.dstride;
-  for (int64_t t = (int64_t)blockIdx.x * kRlcSortBlock + threadIdx.x; t < total; t += (int64_t)gridDim.x * kRlcSortBlock) {
+  for (int64_t t = t0 + threadIdx.x; t < t1; t += kRlcSortBlock) {
     const int d = dig[msm_point(a, t)];
     if (d != 0) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
   }
   __syncthreads();
-  uint32_t* g = a.counts + (int64_t)w * kRlcBuckets;
-  for (int b = threadIdx.x; b < kRlcBuckets; b += kRlcSortBlock)
-    if (hist[b]) atomicAdd(&g[b], hist[b]);
+  uint32_t* out = a.bhist + ((int64_t)w * a.groups + g) * kRlcBuckets;
+  for (int b = threadIdx.x; b < kRlcBuckets; b += kRlcSortBlock) out[b] = hist[b];
 }
 
-// One block per window: exclusive scan of kRlcBuckets counts -> offsets (and cursors).
+__global__ void __launch_bounds__(256) k_rlc_bscan(RlcMsmArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)kRlcWindows * kRlcBuckets) return;
+  const int w = (int)(t / kRlcBuckets);
+  const int b = (int)(t % kRlcBuckets);
+  uint32_t* h = a.bhist + (int64_t)w * a.groups * kRlcBuckets + b;
+  uint32_t run = 0;
+  for (int g = 0; g < a.groups; g++) {
+    const uint32_t v = h[(int64_t)g * kRlcBuckets];
+    h[(int64_t)g * kRlcBuckets] = run;
+    run += v;
+  }
+  a.counts[t] = run;
+}
+
+// One block per window: exclusive scan of kRlcBuckets counts -> offsets.
 __global__ void __launch_bounds__(1024) k_rlc_scan(RlcMsmArgs a) {
   __shared__ uint32_t part[1024];
   const int w = blockIdx.x;
@@ -251,23 +274,27 @@ __global__ void __launch_bounds__(1024) k_rlc_scan(RlcMsmArgs a) {
   }
   uint32_t run = part[threadIdx.x] - sum;  // exclusive
   uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
-  uint32_t* cur = a.cursor + (int64_t)w * kRlcBuckets;
 #pragma unroll
   for (int k = 0; k < per; k++) {
     off[threadIdx.x * per + k] = run;
-    cur[threadIdx.x * per + k] = run;
     run += local[k];
   }
   if (threadIdx.x == 1023) off[kRlcBuckets] = run;
 }
 
 __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_scatter(RlcMsmArgs a) {
-  const int w = blockIdx.y;
+  extern __shared__ uint32_t cur[];  // kRlcBuckets cursors (128 KB)
+  const int g = blockIdx.x, w = blockIdx.y;
+  const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
+  const uint32_t* base = a.bhist + ((int64_t)w * a.groups + g) * kRlcBuckets;
+  for (int b = threadIdx.x; b < kRlcBuckets; b += kRlcSortBlock) cur[b] = off[b] + base[b];
+  __syncthreads();
   const int64_t total = (a.p1 - a.p0) + 2;
+  const int64_t t0 = (int64_t)g * a.chunk;
+  const int64_t t1 = t0 + a.chunk < total ? t0 + a.chunk : total;
   const int16_t* dig = a.digits + (int64_t)w * a.dstride;
-  uint32_t* cur = a.cursor + (int64_t)w * kRlcBuckets;
   uint32_t* idx = a.idx + (int64_t)w * a.istride;
-  for (int64_t t = (int64_t)blockIdx.x * kRlcSortBlock + threadIdx.x; t < total; t += (int64_t)gridDim.x * kRlcSortBlock) {
+  for (int64_t t = t0 + threadIdx.x; t < t1; t += kRlcSortBlock) {
     const int64_t j = msm_point(a, t);
     const int d = dig[j];
     if (d != 0) {
@@ -279,6 +306,8 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_scatter(RlcMsmArgs a) {
 
 // ---------------------------------------------------------------------------------------
 // Bucket accumulation: B[w][b] = sum of (+/-) points in bucket b of window w.
+// The running sum is kept as p1p1; its conversion to p3 (4 muls) is issued after the next
+// point's gather, so the gather latency overlaps that work.
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -288,13 +317,20 @@ __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
   const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
   const uint32_t* idx = a.idx + (int64_t)w * a.istride;
   const uint32_t e0 = off[b], e1 = off[b + 1];
-  ge_p3 acc = ge_identity();
+  ge_p1p1 r;  // identity as p1p1: (0 : 1 : 1 : 1)
+  r.X = fe_zero();
+  r.Y = fe_one();
+  r.Z = fe_one();
+  r.T = fe_one();
+  uint32_t id = e0 < e1 ? idx[e0] : 0u;
   for (uint32_t e = e0; e < e1; e++) {
-    const uint32_t id = idx[e];
-    const ge_niels p = ge_niels_cneg(load_niels(a.pts + (id & 0x7fffffffu)), (id >> 31) != 0);
-    acc = p1p1_to_p3(ge_add_niels(acc, p));
+    const ge_niels p = load_niels(a.pts + (id & 0x7fffffffu));
+    const bool neg = (id >> 31) != 0;
+    id = e + 1 < e1 ? idx[e + 1] : 0u;
+    const ge_p3 acc = p1p1_to_p3(r);
+    r = ge_add_niels(acc, ge_niels_cneg(p, neg));
   }
-  store_p3(a.buckets + t, acc);
+  store_p3(a.buckets + t, p1p1_to_p3(r));
 }
 
 // One thread per (window, segment of kRlcSegLen buckets):
@@ -453,27 +489,39 @@ hipError_t launch_rlc_prepare(const RlcPrepArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+void rlc_sort_geometry(RlcMsmArgs& a, int64_t npts) {
+  int64_t g = (npts + kRlcSortChunk - 1) / kRlcSortChunk;
+  if (g > kRlcSortGroups) g = kRlcSortGroups;
+  if (g < 1) g = 1;
+  a.groups = (int)g;
+  a.chunk = (npts + g - 1) / g;
+}
+
 hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0, int64_t b1, const ge_niels* tab,
-                          int sort_blocks, hipStream_t st) {
+                          hipStream_t st) {
   hipError_t e;
   hipLaunchKernelGGL(k_rlc_extra, dim3(1), dim3(256), 0, st, a, block_sums, b0, b1, tab);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(a.counts, 0, sizeof(uint32_t) * kRlcWindows * kRlcBuckets, st)) != hipSuccess) return e;
   const size_t lds = sizeof(uint32_t) * kRlcBuckets;  // 128 KB of the 160 KB LDS
   static bool attr_set = false;
   if (!attr_set) {
     if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rlc_hist),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
       return e;
+    if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rlc_scatter),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
+      return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(k_rlc_hist, dim3(sort_blocks, kRlcWindows), dim3(kRlcSortBlock), lds, st, a);
+  const int64_t nb = (int64_t)kRlcWindows * kRlcBuckets;
+  hipLaunchKernelGGL(k_rlc_hist, dim3(a.groups, kRlcWindows), dim3(kRlcSortBlock), lds, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rlc_bscan, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_rlc_scan, dim3(kRlcWindows), dim3(1024), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rlc_scatter, dim3(sort_blocks, kRlcWindows), dim3(kRlcSortBlock), 0, st, a);
+  hipLaunchKernelGGL(k_rlc_scatter, dim3(a.groups, kRlcWindows), dim3(kRlcSortBlock), lds, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  const int64_t nb = (int64_t)kRlcWindows * kRlcBuckets;
   hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const int64_t ns = (int64_t)kRlcWindows * (kRlcBuckets / kRlcSegLen);

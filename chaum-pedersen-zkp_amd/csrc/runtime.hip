@@ -88,10 +88,9 @@ struct cpz_ctx {
   DevBuf in[5];
   DevBuf ctxb, ctxo, ctxp;
   // RLC / Pippenger buffers (sized for the largest batch seen)
-  DevBuf rl_pts, rl_dig, rl_bsum, rl_counts, rl_offsets, rl_cursor, rl_idx, rl_buckets, rl_segs, rl_segw, rl_win,
+  DevBuf rl_pts, rl_dig, rl_bsum, rl_counts, rl_offsets, rl_bhist, rl_idx, rl_buckets, rl_segs, rl_segw, rl_win,
       rl_partial, rl_flags, rl_parts;
   int64_t rl_cap = 0;  // proofs
-  int sort_blocks = 0;
   // optional per-kernel timing
   bool timing = false;
   struct Mark { int stage; hipEvent_t a, b; };
@@ -265,7 +264,7 @@ int rlc_reserve(cpz_ctx* ctx, int64_t n) {
   CPZ_HIP(ctx->rl_bsum.ensure((size_t)nblk * 2 * sizeof(cpz::sc)));
   CPZ_HIP(ctx->rl_counts.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcBuckets));
   CPZ_HIP(ctx->rl_offsets.ensure(sizeof(uint32_t) * cpz::kRlcWindows * (cpz::kRlcBuckets + 1)));
-  CPZ_HIP(ctx->rl_cursor.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcBuckets));
+  CPZ_HIP(ctx->rl_bhist.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcSortGroups * cpz::kRlcBuckets));
   CPZ_HIP(ctx->rl_idx.ensure((size_t)npts * cpz::kRlcWindows * sizeof(uint32_t)));
   CPZ_HIP(ctx->rl_buckets.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * cpz::kRlcBuckets));
   const size_t nseg = (size_t)cpz::kRlcWindows * (cpz::kRlcBuckets / cpz::kRlcSegLen);
@@ -288,7 +287,8 @@ cpz::RlcMsmArgs rlc_msm_args(cpz_ctx* ctx, int64_t lo, int64_t hi) {
   m.dstride = 4 * ctx->rl_cap + 2;
   m.counts = static_cast<uint32_t*>(ctx->rl_counts.p);
   m.offsets = static_cast<uint32_t*>(ctx->rl_offsets.p);
-  m.cursor = static_cast<uint32_t*>(ctx->rl_cursor.p);
+  m.bhist = static_cast<uint32_t*>(ctx->rl_bhist.p);
+  cpz::rlc_sort_geometry(m, (m.p1 - m.p0) + 2);
   m.idx = static_cast<uint32_t*>(ctx->rl_idx.p);
   m.istride = 4 * ctx->rl_cap + 2;
   m.buckets = static_cast<cpz::ge_p3*>(ctx->rl_buckets.p);
@@ -306,14 +306,10 @@ int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t part
   cpz::RlcMsmArgs m = rlc_msm_args(ctx, lo, hi);
   const int64_t b0 = lo / cpz::kRlcPrepBlock;
   const int64_t b1 = (hi + cpz::kRlcPrepBlock - 1) / cpz::kRlcPrepBlock;
-  const int64_t npts = 4 * (hi - lo) + 2;
-  int sort_blocks = (int)((npts + cpz::kRlcSortBlock * 64 - 1) / (cpz::kRlcSortBlock * 64));
-  if (sort_blocks > ctx->cus / 8) sort_blocks = ctx->cus / 8 > 0 ? ctx->cus / 8 : 1;
-  if (sort_blocks < 1) sort_blocks = 1;
   {
     StageTimer t(ctx, 3, st);
     CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_bsum.p), b0, b1,
-                                static_cast<const cpz::ge_niels*>(ctx->tab.p), sort_blocks, st));
+                                static_cast<const cpz::ge_niels*>(ctx->tab.p), st));
   }
   int flags[1];
   CPZ_HIP(hipMemcpyAsync(partial, ctx->rl_partial.p, 32, hipMemcpyDeviceToHost, st));
@@ -363,6 +359,8 @@ int rlc_prepare(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const vo
   pa.digits = static_cast<int16_t*>(ctx->rl_dig.p);
   pa.dstride = 4 * ctx->rl_cap + 2;
   pa.block_sums = static_cast<cpz::sc*>(ctx->rl_bsum.p);
+  pa.any_bad = static_cast<int*>(ctx->rl_flags.p) + 3;
+  CPZ_HIP(hipMemsetAsync(pa.any_bad, 0, sizeof(int), st));
   {
     StageTimer t(ctx, 2, st);
     CPZ_HIP(cpz::launch_rlc_prepare(pa, st));
@@ -438,11 +436,10 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
   if (rc) return rc;
   if (partial_out) std::memcpy(partial_out, part, 32);
   // every entry must also have decoded (zero-weight entries are not "verified")
-  std::vector<uint8_t> hs(n);
-  CPZ_HIP(hipMemcpyAsync(hs.data(), d_status, n, hipMemcpyDeviceToHost, st));
+  int any_bad = 0;
+  CPZ_HIP(hipMemcpyAsync(&any_bad, static_cast<int*>(ctx->rl_flags.p) + 3, sizeof(int), hipMemcpyDeviceToHost, st));
   CPZ_HIP(hipStreamSynchronize(st));
-  bool all_live = true;
-  for (size_t i = 0; i < n; i++) all_live = all_live && hs[i] == 0;
+  const bool all_live = any_bad == 0;
   if (batch_ok) *batch_ok = (ident && all_live) ? 1 : 0;
   if (!ident && fallback) {
     rc = rlc_fallback(ctx, 0, (int64_t)n, y1, y2, r1, r2, s, d_status, st, 0);
@@ -565,13 +562,14 @@ int cpz_msm(cpz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalar
   cpz::RlcMsmArgs m = rlc_msm_args(ctx, 0, 0);
   m.p0 = 0;
   m.p1 = (int64_t)n;
+  cpz::rlc_sort_geometry(m, (int64_t)n + 2);
   CPZ_HIP(cpz::launch_msm_load((int64_t)n, static_cast<const uint32_t*>(ctx->in[0].p),
                                static_cast<const uint32_t*>(ctx->in[1].p), m.pts, m.digits, m.dstride,
                                static_cast<int*>(ctx->rl_flags.p) + 2, ctx->stream));
   (void)zero;
   // extra points get zero scalars (empty block range)
   CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_bsum.p), 0, 0,
-                              static_cast<const cpz::ge_niels*>(ctx->tab.p), 1, ctx->stream));
+                              static_cast<const cpz::ge_niels*>(ctx->tab.p), ctx->stream));
   int flags[3];
   CPZ_HIP(hipMemcpyAsync(out, ctx->rl_partial.p, 32, hipMemcpyDeviceToHost, ctx->stream));
   CPZ_HIP(hipMemcpyAsync(flags, ctx->rl_flags.p, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
@@ -649,7 +647,7 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->ctxb.release();
   ctx->ctxo.release();
   ctx->ctxp.release();
-  for (DevBuf* b : {&ctx->rl_pts, &ctx->rl_dig, &ctx->rl_bsum, &ctx->rl_counts, &ctx->rl_offsets, &ctx->rl_cursor,
+  for (DevBuf* b : {&ctx->rl_pts, &ctx->rl_dig, &ctx->rl_bsum, &ctx->rl_counts, &ctx->rl_offsets, &ctx->rl_bhist,
                     &ctx->rl_idx, &ctx->rl_buckets, &ctx->rl_segs, &ctx->rl_segw, &ctx->rl_win, &ctx->rl_partial,
                     &ctx->rl_flags, &ctx->rl_parts})
     b->release();
