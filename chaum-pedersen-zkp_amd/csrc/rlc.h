@@ -48,7 +48,7 @@ struct RlcMsmArgs {
   int64_t chunk;                 // points per sort block
   uint32_t* idx;                 // [16][istride]
   int64_t istride;
-  ge_p3* buckets;                // [16][2^15]
+  ge_p3* buckets;                // [16 + 1][2^15] (slot 16: top-window partials)
   ge_p3* seg_s;                  // [16][1024]
   ge_p3* seg_w;                  // [16][1024]
   ge_p3* win;                    // [16]

@@ -19,7 +19,8 @@
 //   k_rlc_bscan     per-bucket prefix over chunks; bucket totals.
 //   k_rlc_scan      exclusive scan -> bucket offsets.
 //   k_rlc_scatter   point ids sorted by bucket (counting sort, LDS cursors).
-//   k_rlc_bucket    1 thread / (window, bucket): mixed additions over its list.
+//   k_rlc_bucket    1 thread / (window, bucket): mixed additions over its list (the
+//                   top window's fuller buckets split 7 ways, k_rlc_topfold).
 //   k_rlc_segment   1 thread / (window, 32-bucket segment): running sums.
 //   k_rlc_window    1 block / window: sum_b b * B_b from the segments (LDS tree).
 //   k_rlc_final     2^(16w) combine, encode -> 32-byte partial + identity flag.
@@ -309,6 +310,15 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_scatter(RlcMsmArgs a) {
 // The running sum is kept as p1p1; its conversion to p3 (4 muls) is issued after the next
 // point's gather, so the gather latency overlaps that work.
 // ---------------------------------------------------------------------------------------
+// Scalars are < 2^253 and, reduced mod l, almost always < 2^252: the top window's digit is
+// at most 2^13 and in practice at most 2^12 + 1, so its ~4097 live buckets hold ~8x the
+// points of a full window's bucket.  Its 32768 thread slots are therefore re-assigned:
+// slot q * 4096 + k (q < 7) takes part q of 7 of bucket k < 4096, and slot 28672 + k
+// takes all of bucket 4096 + k.  The partials land in the spare window slot
+// (buckets[kRlcWindows]) and k_rlc_topfold folds them into window 15's buckets.
+constexpr int kTopBase = 4096;
+constexpr int kTopParts = 7;
+
 __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= (int64_t)kRlcWindows * kRlcBuckets) return;
@@ -316,7 +326,23 @@ __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
   const int b = (int)(t % kRlcBuckets);
   const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
   const uint32_t* idx = a.idx + (int64_t)w * a.istride;
-  const uint32_t e0 = off[b], e1 = off[b + 1];
+  uint32_t e0, e1;
+  ge_p3* dst = a.buckets + t;
+  if (w == kRlcWindows - 1) {
+    const int q = b / kTopBase, k = b % kTopBase;
+    if (q < kTopParts) {
+      const uint32_t f0 = off[k], cnt = off[k + 1] - f0;
+      e0 = f0 + (uint32_t)(((uint64_t)cnt * q) / kTopParts);
+      e1 = f0 + (uint32_t)(((uint64_t)cnt * (q + 1)) / kTopParts);
+    } else {
+      e0 = off[kTopBase + k];
+      e1 = off[kTopBase + k + 1];
+    }
+    dst = a.buckets + (int64_t)kRlcWindows * kRlcBuckets + b;
+  } else {
+    e0 = off[b];
+    e1 = off[b + 1];
+  }
   ge_p1p1 r;  // identity as p1p1: (0 : 1 : 1 : 1)
   r.X = fe_zero();
   r.Y = fe_one();
@@ -330,7 +356,24 @@ __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
     const ge_p3 acc = p1p1_to_p3(r);
     r = ge_add_niels(acc, ge_niels_cneg(p, neg));
   }
-  store_p3(a.buckets + t, p1p1_to_p3(r));
+  store_p3(dst, p1p1_to_p3(r));
+}
+
+// Window 15's buckets from the split partials (see k_rlc_bucket).
+__global__ void __launch_bounds__(256) k_rlc_topfold(RlcMsmArgs a) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= kRlcBuckets) return;
+  const ge_p3* part = a.buckets + (int64_t)kRlcWindows * kRlcBuckets;
+  ge_p3 v;
+  if (k < kTopBase) {
+    v = load_p3(part + k);
+    for (int q = 1; q < kTopParts; q++) v = ge_add(v, load_p3(part + q * kTopBase + k));
+  } else if (k < 2 * kTopBase) {
+    v = load_p3(part + kTopParts * kTopBase + (k - kTopBase));
+  } else {
+    v = ge_identity();
+  }
+  store_p3(a.buckets + (int64_t)(kRlcWindows - 1) * kRlcBuckets + k, v);
 }
 
 // One thread per (window, segment of kRlcSegLen buckets):
@@ -523,6 +566,8 @@ hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0,
   hipLaunchKernelGGL(k_rlc_scatter, dim3(a.groups, kRlcWindows), dim3(kRlcSortBlock), lds, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rlc_topfold, dim3(kRlcBuckets / 256), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const int64_t ns = (int64_t)kRlcWindows * (kRlcBuckets / kRlcSegLen);
   hipLaunchKernelGGL(k_rlc_segment, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, st, a);

@@ -266,7 +266,7 @@ int rlc_reserve(cpz_ctx* ctx, int64_t n) {
   CPZ_HIP(ctx->rl_offsets.ensure(sizeof(uint32_t) * cpz::kRlcWindows * (cpz::kRlcBuckets + 1)));
   CPZ_HIP(ctx->rl_bhist.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcSortGroups * cpz::kRlcBuckets));
   CPZ_HIP(ctx->rl_idx.ensure((size_t)npts * cpz::kRlcWindows * sizeof(uint32_t)));
-  CPZ_HIP(ctx->rl_buckets.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * cpz::kRlcBuckets));
+  CPZ_HIP(ctx->rl_buckets.ensure(sizeof(cpz::ge_p3) * (cpz::kRlcWindows + 1) * cpz::kRlcBuckets));  // + top-window parts
   const size_t nseg = (size_t)cpz::kRlcWindows * (cpz::kRlcBuckets / cpz::kRlcSegLen);
   CPZ_HIP(ctx->rl_segs.ensure(sizeof(cpz::ge_p3) * nseg));
   CPZ_HIP(ctx->rl_segw.ensure(sizeof(cpz::ge_p3) * nseg));
