@@ -14,7 +14,7 @@ constexpr uint8_t kStatusBadScalar = 3;
 constexpr uint8_t kStatusIdentityOrZero = 4;
 
 constexpr int kNielsEntries = kTableB;   // radix-256 signed digits: |d| <= 128
-constexpr int kCachedEntries = kTableV;   // radix-16 signed digits: |d| <= 8
+constexpr int kCachedEntries = 2 * kTableV;   // y and r tables, radix-16 signed digits: |d| <= 8
 constexpr int kVerifyBlock = 256;
 
 // Merlin/STROBE sponge snapshot.
@@ -51,7 +51,7 @@ struct VerifyArgs {
   const uint32_t* s;
   const uint32_t* c;
   uint8_t* status;               // in: response-scalar status; out: final status
-  const ge_niels* tab;           // [0, 128): g, [128, 256): h
+  const ge_niels* tab;           // 128 entries each: g, h, 2^128 g, 2^128 h
   ge_cached* scratch;            // grid * kVerifyBlock * kCachedEntries entries
 };
 

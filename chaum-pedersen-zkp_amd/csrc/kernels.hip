@@ -5,12 +5,15 @@
 //   k_challenge          1 thread / proof: Fiat-Shamir challenge c (bit-exact merlin),
 //                        response-scalar checks (from_canonical_bytes, zero)
 //                        batch.rs:188-206, gadgets.rs:466-482
-//   k_build_niels        (k * B) for k = 1..128, B in {g, h}: affine Niels tables
-//   k_verify_each        1 thread / proof: 4 ristretto decodes, then
-//                        [s]g - [c]y1 == r1 and [s]h - [c]y2 == r2 (ristretto equality)
-//                        by a Straus loop: radix-16 signed digits of c against a per-proof
-//                        table of 8 multiples of -y (HBM-backed scratch), radix-256 signed
-//                        digits of s against the shared 128-entry LDS table of g (h).
+//   k_build_niels        (k * B) for k = 1..128, B in {g, h, 2^128 g, 2^128 h}: affine
+//                        Niels tables
+//   k_verify_each        1 thread / proof: challenge split v c = u (mod l) with
+//                        u, |v| < 2^127 (verify.h), 4 ristretto decodes, then per equation
+//                        [v s] B - [u] y - [v] r in E[4]  <=>  [s] B - [c] y == r
+//                        by a half-length Straus loop: radix-16 signed digits of u and |v|
+//                        against per-proof tables of 8 multiples of -y and -+r (HBM-backed
+//                        scratch), radix-256 digits of v s against the shared LDS tables
+//                        of B and 2^128 B.
 //                        batch.rs:185-231, verifier/mod.rs:144-171
 //   k_prove_points /     synthetic-input generator: Prover::prove_with_transcript
 //   k_prove_response     (prover/mod.rs:86-131) with ChaCha20-derived witnesses/nonces
@@ -127,15 +130,21 @@ __global__ void __launch_bounds__(kChallengeBlock) k_challenge(ChallengeArgs a) 
 // ---------------------------------------------------------------------------------------
 // Fixed-base tables: tab[b * 128 + (k - 1)] = k * base_b in affine Niels form.
 // ---------------------------------------------------------------------------------------
+// Tables for 2 * nbases bases: [b0 .. b_{n-1}, 2^128 b0 .. 2^128 b_{n-1}], 128 entries each.
 __global__ void __launch_bounds__(64) k_build_niels(const uint32_t* __restrict__ base_words, int nbases, ge_niels* __restrict__ tab,
                               int* __restrict__ ok) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nbases * kNielsEntries) return;
+  if (t >= 2 * nbases * kNielsEntries) return;
   const int b = t / kNielsEntries;
   const int k = t % kNielsEntries + 1;
+  const int src = b % nbases;
   ge_p3 B;
-  const bool dec = ristretto_decode(B, base_words + 8 * b);
-  if (k == 1) ok[b] = dec ? 1 : 0;
+  const bool dec = ristretto_decode(B, base_words + 8 * src);
+  if (k == 1 && b < nbases) ok[b] = dec ? 1 : 0;
+  if (b >= nbases) {
+#pragma unroll 1
+    for (int d = 0; d < 128; d++) B = p1p1_to_p3(p3_dbl(B));
+  }
   tab[t] = p3_to_niels(small_mul(B, k));
 }
 
@@ -150,11 +159,14 @@ __device__ __forceinline__ void copy_niels_to_lds(ge_niels* dst, const ge_niels*
 }
 
 __global__ void __launch_bounds__(kVerifyBlock, 2) k_verify_each(VerifyArgs a) {
-  __shared__ ge_niels tab_g[kNielsEntries];
-  __shared__ ge_niels tab_h[kNielsEntries];
-  copy_niels_to_lds(tab_g, a.tab, kNielsEntries);
-  copy_niels_to_lds(tab_h, a.tab + kNielsEntries, kNielsEntries);
+  // g, h, 2^128 g, 2^128 h: 4 x 128 Niels entries = 64 KB of LDS
+  __shared__ ge_niels tabs[4 * kNielsEntries];
+  copy_niels_to_lds(tabs, a.tab, 4 * kNielsEntries);
   __syncthreads();
+  const ge_niels* tab_g = tabs;
+  const ge_niels* tab_h = tabs + kNielsEntries;
+  const ge_niels* tab_g2 = tabs + 2 * kNielsEntries;
+  const ge_niels* tab_h2 = tabs + 3 * kNielsEntries;
   const int64_t gtid = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * kVerifyBlock;
   ge_cached* tab_v = a.scratch + gtid * kCachedEntries;
@@ -165,7 +177,7 @@ __global__ void __launch_bounds__(kVerifyBlock, 2) k_verify_each(VerifyArgs a) {
     load_words8(sw, a.s, i);
     load_words8(cw, a.c, i);
     a.status[i] = verify_proof(a.y1 + 8 * i, a.y2 + 8 * i, a.r1 + 8 * i, a.r2 + 8 * i, sw, cw, a.status[i],
-                               tab_g, tab_h, tab_v);
+                               tab_g, tab_h, tab_g2, tab_h2, tab_v);
   }
 }
 
@@ -234,7 +246,7 @@ hipError_t launch_challenge(const ChallengeArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, hipStream_t st) {
-  const int total = nbases * kNielsEntries;
+  const int total = 2 * nbases * kNielsEntries;
   hipLaunchKernelGGL(k_build_niels, dim3((total + 63) / 64), dim3(64), 0, st, base_words, nbases, tab, ok);
   return hipGetLastError();
 }

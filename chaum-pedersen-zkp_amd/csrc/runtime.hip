@@ -140,7 +140,7 @@ int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32]) {
   if (std::memcmp(g, zero, 32) == 0 || std::memcmp(h, zero, 32) == 0)
     return fail(CPZ_EGENERATOR, "generator cannot be identity");
   if (std::memcmp(g, h, 32) == 0) return fail(CPZ_EGENERATOR, "generators g and h must be different");
-  CPZ_HIP(ctx->tab.ensure(2 * cpz::kNielsEntries * sizeof(cpz::ge_niels)));
+  CPZ_HIP(ctx->tab.ensure(4 * cpz::kNielsEntries * sizeof(cpz::ge_niels)));  // g, h, 2^128 g, 2^128 h
   CPZ_HIP(ctx->prefix.ensure(2 * sizeof(cpz::StrobeSnap)));
   CPZ_HIP(ctx->gh_words.ensure(64));
   CPZ_HIP(ctx->ok_flags.ensure(2 * sizeof(int)));

@@ -9,6 +9,8 @@
 // Reduction is Barrett (HAC 14.42, b = 2^32, k = 8, mu = floor(2^512 / l)); every
 // 32x32 partial product is one v_mad_u64_u32.
 #pragma once
+#include <math.h>
+
 #include "fe25519.h"
 
 namespace cpz {
@@ -200,6 +202,156 @@ CPZ_HD void sc_recode_radix256(uint32_t out[8], const uint32_t s[8]) {
       carry = (n + 128) >> 8;
       const int32_t d = n - (carry << 8);
       packed |= ((uint32_t)d & 255u) << (8 * m);
+    }
+    out[j] = packed;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Half-size decomposition of a challenge (2-dimensional lattice reduction by the partial
+// extended Euclidean algorithm, cf. T. Pornin, "Optimized Lattice Basis Reduction In
+// Dimension 2, and Fast Schnorr and EdDSA Signature Verification", 2020).
+//
+// Finds u >= 0 and v != 0 with  v c == u (mod l)  and  u, |v| < 3 * 2^125.  The Euclid
+// remainders r_k = s_k l + t_k c decrease; the first r_k below T = 3 * 2^125 gives
+// u = r_k, v = t_k, and |t_k| <= l / r_{k-1} <= l / T < 2^127 / 1.5 (from the identity
+// r_{k-1} |t_k| + r_k |t_{k-1}| = l).  Both fit 32 signed radix-16 digits with no carry
+// out (top nibble <= 5, + carry <= 6).
+//
+// Quotients come from f64 estimates of r0 / r1 shrunk by a 2^-46 relative margin, so a
+// step never subtracts more than the true quotient: one Euclid step may take several
+// partial steps, but the (r, t) sequence at each swap is the exact Euclid sequence and
+// (u, v) is unique.  Estimates >= 2^62 are applied as q * 2^k with a shifted divisor.
+// ---------------------------------------------------------------------------------------
+CPZ_HD double words8_to_f64(const uint32_t a[8]) {
+  double d = (double)a[7];
+#pragma unroll
+  for (int j = 6; j >= 0; j--) d = d * 4294967296.0 + (double)a[j];
+  return d;
+}
+
+// a < b (unsigned 256-bit)
+CPZ_HD bool words8_lt(const uint32_t a[8], const uint32_t b[8]) {
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const uint64_t d = (uint64_t)a[j] - b[j] - borrow;
+    borrow = (uint32_t)(d >> 63);
+  }
+  return borrow != 0;
+}
+
+// out = a << k (mod 2^256), 0 <= k < 256; selects instead of a dynamically indexed array.
+CPZ_HD void words8_shl(uint32_t out[8], const uint32_t a[8], int k) {
+  const int kl = k >> 5, kb = k & 31;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    uint32_t hi = 0, lo = 0;
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+      if (m == kl) {
+        hi = j - m >= 0 ? a[j - m >= 0 ? j - m : 0] : 0u;
+        lo = j - m - 1 >= 0 ? a[j - m - 1 >= 0 ? j - m - 1 : 0] : 0u;
+      }
+    }
+    out[j] = kb ? ((hi << kb) | (lo >> (32 - kb))) : hi;
+  }
+}
+
+// r -= q x (mod 2^256), q < 2^64.
+CPZ_HD void words8_submul(uint32_t r[8], const uint32_t x[8], uint64_t q) {
+  const uint32_t q0 = (uint32_t)q, q1 = (uint32_t)(q >> 32);
+  uint32_t p[8];
+  uint64_t carry = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const uint64_t t = (uint64_t)x[j] * q0 + carry;
+    p[j] = (uint32_t)t;
+    carry = t >> 32;
+  }
+  carry = 0;
+#pragma unroll
+  for (int j = 1; j < 8; j++) {
+    const uint64_t t = (uint64_t)x[j - 1] * q1 + p[j] + carry;
+    p[j] = (uint32_t)t;
+    carry = t >> 32;
+  }
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const uint64_t d = (uint64_t)r[j] - p[j] - borrow;
+    r[j] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+}
+
+CPZ_HD bool half_below(const uint32_t r[8]) {
+  return (r[4] | r[5] | r[6] | r[7]) == 0 && r[3] < 0x60000000u;  // r < 3 * 2^125
+}
+
+// c < l canonical.  u, vabs: 4 words each (128-bit); vneg: sign of v.
+CPZ_HD void sc_half_split(const uint32_t c[8], uint32_t u[4], uint32_t vabs[4], bool& vneg) {
+  uint32_t r0[8], r1[8], t0[8], t1[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    r0[j] = SC_L(j);
+    r1[j] = c[j];
+    t0[j] = 0;
+    t1[j] = j == 0 ? 1u : 0u;
+  }
+#pragma unroll 1
+  while (!half_below(r1)) {
+    double qf = words8_to_f64(r0) / words8_to_f64(r1);
+    int k = 0;
+    if (qf >= 0x1p62) {
+      k = ilogb(qf) - 61;
+      qf = ldexp(qf, -k);
+    }
+    uint64_t q = (uint64_t)(qf * (1.0 - 0x1p-46));
+    if (q == 0) q = 1;
+    if (k) {
+      uint32_t xs[8], ts[8];
+      words8_shl(xs, r1, k);
+      words8_shl(ts, t1, k);
+      words8_submul(r0, xs, q);
+      words8_submul(t0, ts, q);
+    } else {
+      words8_submul(r0, r1, q);
+      words8_submul(t0, t1, q);
+    }
+    if (words8_lt(r0, r1)) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        uint32_t x = r0[j]; r0[j] = r1[j]; r1[j] = x;
+        x = t0[j]; t0[j] = t1[j]; t1[j] = x;
+      }
+    }
+  }
+  vneg = (t1[7] >> 31) != 0;
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    u[j] = r1[j];
+    // |t1| = vneg ? 0 - t1 : t1
+    const uint64_t d = (uint64_t)0 - t1[j] - borrow;
+    borrow = (uint32_t)(d >> 63);
+    vabs[j] = vneg ? (uint32_t)d : t1[j];
+  }
+}
+
+// Signed radix-16 recoding of a value < 6 * 2^124 held in 4 words: 32 digits in [-8, 7],
+// packed as in sc_recode_radix16 (no carry out of the top digit for such values).
+CPZ_HD void sc_recode_radix16_half(uint32_t out[4], const uint32_t s[4]) {
+  int32_t carry = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+      const int32_t n = (int32_t)((s[j] >> (4 * m)) & 15u) + carry;
+      carry = (n + 8) >> 4;
+      const int32_t d = n - (carry << 4);
+      packed |= ((uint32_t)d & 15u) << (4 * m);
     }
     out[j] = packed;
   }

@@ -25,16 +25,24 @@ fe fe_from(const uint8_t* b) {
 
 void fe_out(uint8_t* b, const fe& f) { fe_tobytes(b, f); }
 
-// Fixed-base tables (k * base, k = 1..128) for one base encoding.
-bool build_table(std::vector<ge_niels>& tab, const uint8_t* enc) {
+// Fixed-base tables (k * base, k = 1..128) for one base encoding, times 2^shift.
+bool build_table(std::vector<ge_niels>& tab, const uint8_t* enc, int shift = 0) {
   uint32_t w[8];
   words_from(w, enc);
   ge_p3 B;
   if (!ristretto_decode(B, w)) return false;
+  for (int d = 0; d < shift; d++) B = p1p1_to_p3(p3_dbl(B));
   tab.resize(kTableB);
   for (int k = 1; k <= kTableB; k++) tab[k - 1] = p3_to_niels(small_mul(B, k));
   return true;
 }
+
+struct GenTables {
+  std::vector<ge_niels> g, h, g2, h2;
+  bool build(const uint8_t* genc, const uint8_t* henc) {
+    return build_table(g, genc) && build_table(h, henc) && build_table(g2, genc, 128) && build_table(h2, henc, 128);
+  }
+};
 
 }  // namespace
 
@@ -197,8 +205,8 @@ void cpzt_challenge(uint8_t* out, const uint8_t* g, const uint8_t* h, const uint
 int cpzt_verify_opcount(unsigned long long* mul, unsigned long long* sq, const uint8_t* g, const uint8_t* h,
                         const uint8_t* y1, const uint8_t* y2, const uint8_t* r1, const uint8_t* r2, const uint8_t* s,
                         const uint8_t* c) {
-  std::vector<ge_niels> tg, th;
-  if (!build_table(tg, g) || !build_table(th, h)) return -1;
+  GenTables gt;
+  if (!gt.build(g, h)) return -1;
   uint32_t a[8], b[8], cc[8], d[8], sw[8], cw[8];
   words_from(a, y1);
   words_from(b, y2);
@@ -206,10 +214,11 @@ int cpzt_verify_opcount(unsigned long long* mul, unsigned long long* sq, const u
   words_from(d, r2);
   words_from(sw, s);
   words_from(cw, c);
-  ge_cached tv[kTableV];
+  ge_cached tv[2 * kTableV];
   unsigned long long m0, s0;
   cpzt_opcount(&m0, &s0);
-  const int st = verify_proof(a, b, cc, d, sw, cw, response_status(sw), tg.data(), th.data(), tv);
+  const int st = verify_proof(a, b, cc, d, sw, cw, response_status(sw), gt.g.data(), gt.h.data(), gt.g2.data(),
+                              gt.h2.data(), tv);
   cpzt_opcount(mul, sq);
   return st;
 }
@@ -217,8 +226,8 @@ int cpzt_verify_opcount(unsigned long long* mul, unsigned long long* sq, const u
 // Full per-proof verification exactly as k_challenge + k_verify_each compute it.
 int cpzt_verify(const uint8_t* g, const uint8_t* h, const uint8_t* y1, const uint8_t* y2, const uint8_t* r1,
                 const uint8_t* r2, const uint8_t* s, const uint8_t* ctx, uint32_t ctx_len, int has_ctx) {
-  std::vector<ge_niels> tg, th;
-  if (!build_table(tg, g) || !build_table(th, h)) return -1;
+  GenTables gt;
+  if (!gt.build(g, h)) return -1;
   uint8_t cb[32];
   cpzt_challenge(cb, g, h, y1, y2, r1, r2, ctx, ctx_len, has_ctx);
   uint32_t a[8], b[8], c[8], d[8], sw[8], cw[8];
@@ -228,8 +237,20 @@ int cpzt_verify(const uint8_t* g, const uint8_t* h, const uint8_t* y1, const uin
   words_from(d, r2);
   words_from(sw, s);
   words_from(cw, cb);
-  ge_cached tv[kTableV];
-  return verify_proof(a, b, c, d, sw, cw, response_status(sw), tg.data(), th.data(), tv);
+  ge_cached tv[2 * kTableV];
+  return verify_proof(a, b, c, d, sw, cw, response_status(sw), gt.g.data(), gt.h.data(), gt.g2.data(), gt.h2.data(),
+                      tv);
+}
+
+// Half-size challenge split: u, |v| (16 bytes each, little-endian), sign of v.
+void cpzt_half_split(uint8_t* u_out, uint8_t* v_out, int* vneg, const uint8_t* c) {
+  uint32_t cw[8], u[4], v[4];
+  words_from(cw, c);
+  bool neg;
+  sc_half_split(cw, u, v, neg);
+  std::memcpy(u_out, u, 16);
+  std::memcpy(v_out, v, 16);
+  *vneg = neg ? 1 : 0;
 }
 
 }  // extern "C"

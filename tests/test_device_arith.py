@@ -176,3 +176,31 @@ def test_golden_proofs_host_build(lib, golden):
         cb = _ctx(p) or b""
         assert lib.cpzt_verify(g2, h2, f["y1"], f["y2"], f["r1"], f["r2"], f["s"], cb, len(cb), 1) == 0
         assert lib.cpzt_verify(g, h, f["y1"], f["y2"], f["r1"], f["r2"], f["s"], cb, len(cb), 1) == 1
+
+
+def _euclid_half(c):
+    """Exact partial extended Euclid on (l, c): first remainder below 3 * 2^125."""
+    T = 3 << 125
+    r0, r1, t0, t1 = L, c, 0, 1
+    while r1 >= T:
+        q = r0 // r1
+        r0, r1 = r1, r0 - q * r1
+        t0, t1 = t1, t0 - q * t1
+    return r1, t1
+
+
+def test_half_split(lib):
+    """sc_half_split (csrc/scalar25519.h): v c = u (mod l), u, |v| < 3 * 2^125, and equal
+    to the exact Euclid values -- incl. huge partial quotients (the shifted-divisor path)."""
+    rng = random.Random(7)
+    cases = [0, 1, 2, (3 << 125) - 1, 3 << 125, L - 1, L - 2, L // 2, L // 3, (L >> 70), (L >> 140) + 5,
+             (L >> 126), (L >> 127) + 1, 2**252, (2**128 + 1) % L]
+    cases += [rng.randrange(L) for _ in range(300)]
+    u, v, neg = buf(16), buf(16), ctypes.c_int()
+    for c in cases:
+        lib.cpzt_half_split(u, v, ctypes.byref(neg), c.to_bytes(32, "little"))
+        uu = fi(u.raw)
+        vv = -fi(v.raw) if neg.value else fi(v.raw)
+        assert (uu, vv) == _euclid_half(c), c
+        assert vv != 0 and (vv * c - uu) % L == 0
+        assert uu < 3 << 125 and abs(vv) < 3 << 125
