@@ -125,3 +125,36 @@ def test_rlc_decode_failures_zero_weight(gpu, golden):
     assert partial == bytes(32)          # the undecodable entry carries zero weight
     assert not ok                         # ... but the batch is not "all verified"
     assert list(st) == [p["status"] for p in ps]
+
+
+def test_c5_16m_batch_with_0p1pct_forged(gpu):
+    """Config C5: a 2^24-proof batch with 16,777 forged entries (0.1 %, seeded indices; half
+    s := s + 1, half y1 replaced by another proof's y1).  The RLC check must fail and the
+    fallback must return exactly the forged index set, every one with status 1."""
+    torch = pytest.importorskip("torch")
+    n = 1 << 24
+    nf = 16_777
+    seed = hashlib.sha256(b"cpz-weights-v1").digest()
+    t = _synthetic(gpu, torch, n)
+    rng = np.random.default_rng(2024)
+    idx = np.sort(rng.choice(n, size=nf, replace=False))
+    bump, swap = idx[0::2], idx[1::2]
+    # s + 1 mod l on the device-side rows (in place, via host round trip of only those rows)
+    sel = torch.from_numpy(bump).to("cuda:0")
+    rows = t["s"].index_select(0, sel).cpu().numpy()
+    for r in range(rows.shape[0]):
+        v = (int.from_bytes(rows[r].tobytes(), "little") + 1) % O.L
+        rows[r] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)
+    t["s"].index_copy_(0, sel, torch.from_numpy(rows).to("cuda:0"))
+    # y1 of another (valid) proof
+    dst = torch.from_numpy(swap).to("cuda:0")
+    src = torch.from_numpy((swap + 7) % n).to("cuda:0")
+    t["y1"].index_copy_(0, dst, t["y1"].index_select(0, src).clone())
+    st = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    partial, ok = gpu.verify_batch_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], st, seed, fallback=True)
+    torch.cuda.synchronize()
+    assert not ok and partial != bytes(32)
+    host = st.cpu().numpy()
+    got = np.nonzero(host)[0]
+    assert np.array_equal(got, idx)
+    assert set(host[idx].tolist()) == {1}
