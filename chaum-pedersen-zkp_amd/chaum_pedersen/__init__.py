@@ -196,6 +196,40 @@ class Proof:
         return self.s
 
 
+# Proof::from_bytes outcome codes of the bulk parser (cpz.h CPZ_PARSE_*), with the
+# reference's error type and message (gadgets.rs:364-489, ristretto.rs:94-138).
+PARSE_ERRORS = {
+    1: (InvalidParams, "Proof too small: {} bytes"),
+    2: (InvalidParams, "Unsupported proof version: {}"),
+    3: (InvalidParams, "Truncated proof: missing r1 length"),
+    4: (InvalidParams, "Invalid r1 length: {}"),
+    5: (InvalidParams, "Truncated proof: incomplete r1 data"),
+    6: (InvalidGroupElement, "Expected 32 bytes, got {}"),
+    7: (InvalidGroupElement, "Bytes do not represent a valid Ristretto point"),
+    8: (InvalidParams, "Truncated proof: missing r2 length"),
+    9: (InvalidParams, "Invalid r2 length: {}"),
+    10: (InvalidParams, "Truncated proof: incomplete r2 data"),
+    11: (InvalidGroupElement, "Expected 32 bytes, got {}"),
+    12: (InvalidGroupElement, "Bytes do not represent a valid Ristretto point"),
+    13: (InvalidParams, "Truncated proof: missing s length"),
+    14: (InvalidParams, "Invalid s length: {}"),
+    15: (InvalidParams, "Truncated proof: incomplete s data"),
+    16: (InvalidScalar, "Expected 32 bytes, got {}"),
+    17: (InvalidScalar, "Bytes do not represent a valid scalar"),
+    18: (InvalidParams, "Proof has {} trailing bytes"),
+    19: (InvalidParams, "Commitment contains identity element"),
+    20: (InvalidParams, "Response scalar is zero"),
+}
+
+
+def parse_error(code: int, aux: int = 0) -> Optional[Error]:
+    """The exception Proof::from_bytes raises for a bulk-parser code (None for 0)."""
+    if code == 0:
+        return None
+    cls, msg = PARSE_ERRORS[int(code)]
+    return cls(msg.format(int(aux)))
+
+
 def _rows(data, n: int, name: str) -> np.ndarray:
     a = np.ascontiguousarray(np.asarray(data, dtype=np.uint8))
     if a.shape != (n, 32):
@@ -329,6 +363,31 @@ class Gpu:
             r2.data_ptr(), s.data_ptr(), None, None, None, bytes(seed), first_index, partial, ctypes.byref(ok),
             status_out.data_ptr(), 1 if fallback else 0, _torch_stream(stream)))
         return partial.raw, bool(ok.value)
+
+    def parse_proofs(self, blobs: Sequence[bytes]):
+        """Bulk Proof::from_bytes on the device (cpz_parse_proofs): returns (r1, r2, s) as
+        uint8[n, 32] rows (zero where not parsed), codes uint8[n] (CPZ_PARSE_*, 0 = ok) and
+        aux uint32[n] (the value printed by the reference's message); parse_error(code, aux)
+        gives the exception."""
+        n = len(blobs)
+        lens = np.fromiter((len(b) for b in blobs), dtype=np.uint64, count=n)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(lens, out=off[1:])
+        blob = np.frombuffer(b"".join(bytes(b) for b in blobs) + b"\0", dtype=np.uint8)
+        rows = [np.empty((n, 32), dtype=np.uint8) for _ in range(3)]
+        codes = np.empty(n, dtype=np.uint8)
+        aux = np.empty(n, dtype=np.uint32)
+        _native.check(self._lib.cpz_parse_proofs(self._h, n, _ptr(blob), _ptr(off), *[_ptr(r) for r in rows],
+                                                 _ptr(codes), _ptr(aux)))
+        return rows[0], rows[1], rows[2], codes, aux
+
+    def parse_proofs_device(self, blob, off, r1, r2, s, codes, aux=None, stream: Optional[int] = None) -> None:
+        """Device form: blob (uint8 tensor), off (int64/uint64 tensor of n + 1 offsets), row
+        outputs uint8[n, 32], codes uint8[n], aux int32/uint32[n] or None."""
+        n = int(off.numel()) - 1
+        dp = lambda t: None if t is None else t.data_ptr()
+        _native.check(self._lib.cpz_parse_proofs_device(
+            self._h, n, dp(blob), dp(off), dp(r1), dp(r2), dp(s), dp(codes), dp(aux), _torch_stream(stream)))
 
     def msm(self, points: Sequence[bytes], scalars: Sequence[int]) -> bytes:
         """enc(sum [k_j] P_j) through the Pippenger kernels (cpz_msm)."""

@@ -30,6 +30,7 @@ EXPORTED = (
     "cpz_default_generators", "cpz_verify_each", "cpz_verify_each_device", "cpz_challenges",
     "cpz_prove_synthetic", "cpz_prove_synthetic_device", "cpz_ctx_set_timing", "cpz_ctx_stage_times",
     "cpz_verify_batch", "cpz_verify_batch_device", "cpz_combine_partials", "cpz_msm",
+    "cpz_parse_proofs", "cpz_parse_proofs_device",
 )
 NUM_STAGES = 8
 
@@ -79,6 +80,10 @@ def _declare(lib):
                                             ctypes.c_uint64, _p, ctypes.POINTER(ctypes.c_int), _p, ctypes.c_int, _p])
     lib.cpz_msm.restype = ctypes.c_int
     lib.cpz_msm.argtypes = [_p, ctypes.c_size_t, _p, _p, _p]
+    lib.cpz_parse_proofs.restype = ctypes.c_int
+    lib.cpz_parse_proofs.argtypes = [_p, ctypes.c_size_t, _p, _p, _p, _p, _p, _p, _p]
+    lib.cpz_parse_proofs_device.restype = ctypes.c_int
+    lib.cpz_parse_proofs_device.argtypes = [_p, ctypes.c_size_t, _p, _p, _p, _p, _p, _p, _p, _p]
     lib.cpz_combine_partials.restype = ctypes.c_int
     lib.cpz_combine_partials.argtypes = [_p, ctypes.c_size_t, _p, _p, ctypes.POINTER(ctypes.c_int)]
     lib.cpz_prove_synthetic_device.restype = ctypes.c_int

@@ -42,6 +42,26 @@ struct ChallengeArgs {
   uint8_t* status_out;           // n (written when s != null)
 };
 
+// Proof::from_bytes outcome codes (gadgets.rs:364-489); kept equal to CPZ_PARSE_* in cpz.h.
+enum ParseCode : uint8_t {
+  kParseOk = 0, kParseTooSmall, kParseBadVersion,
+  kParseR1LenMissing, kParseR1LenInvalid, kParseR1Truncated, kParseR1Size, kParseR1Point,
+  kParseR2LenMissing, kParseR2LenInvalid, kParseR2Truncated, kParseR2Size, kParseR2Point,
+  kParseSLenMissing, kParseSLenInvalid, kParseSTruncated, kParseSSize, kParseSScalar,
+  kParseTrailing, kParseIdentity, kParseZeroS
+};
+
+struct ParseArgs {
+  int64_t n;
+  const uint8_t* blob;           // concatenated Proof::to_bytes blobs
+  const uint64_t* off;           // n + 1 offsets into blob
+  uint32_t* r1;                  // n x 8 words out (zero where not parsed)
+  uint32_t* r2;
+  uint32_t* s;
+  uint8_t* code;                 // n ParseCode
+  uint32_t* aux;                 // n message values (length / version / trailing count), or null
+};
+
 struct VerifyArgs {
   int64_t n;
   const uint32_t* y1;
@@ -72,6 +92,7 @@ struct ProveArgs {
 hipError_t launch_transcript_prefix(const uint32_t* gh_words, StrobeSnap* out, hipStream_t st);
 hipError_t launch_challenge(const ChallengeArgs& a, hipStream_t st);
 hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, hipStream_t st);
+hipError_t launch_parse_proofs(const ParseArgs& a, hipStream_t st);
 hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st);
 hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st);
 hipError_t launch_prove_response(const ProveArgs& a, hipStream_t st);

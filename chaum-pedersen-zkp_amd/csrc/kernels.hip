@@ -15,6 +15,7 @@
 //                        scratch), radix-256 digits of v s against the shared LDS tables
 //                        of B and 2^128 B.
 //                        batch.rs:185-231, verifier/mod.rs:144-171
+//   k_parse_proofs       bulk Proof::from_bytes (gadgets.rs:364-489) into SoA rows + codes
 //   k_prove_points /     synthetic-input generator: Prover::prove_with_transcript
 //   k_prove_response     (prover/mod.rs:86-131) with ChaCha20-derived witnesses/nonces
 //
@@ -149,6 +150,88 @@ __global__ void __launch_bounds__(64) k_build_niels(const uint32_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------
+// Bulk wire-format ingestion: Proof::from_bytes (gadgets.rs:364-489) for n blobs, one
+// thread per blob, checks in the reference's order -- structural checks of each field,
+// each field decoded (element_from_bytes / scalar_from_bytes) before the next field's
+// structure is looked at, trailing bytes, then identity commitments and zero s -- so
+// the first failing check, and hence the error, is the reference's.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t be32_at(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+
+__device__ __forceinline__ void words_at(uint32_t w[8], const uint8_t* p) {
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    w[k] = (uint32_t)p[4 * k] | ((uint32_t)p[4 * k + 1] << 8) | ((uint32_t)p[4 * k + 2] << 16) |
+           ((uint32_t)p[4 * k + 3] << 24);
+}
+
+__global__ void __launch_bounds__(256) k_parse_proofs(ParseArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint64_t o0 = a.off[i];
+  const uint64_t len = a.off[i + 1] - o0;
+  const uint8_t* b = a.blob + o0;
+  uint32_t f0[8], f1[8], f2[8];  // r1, r2, s (separate arrays: q is a runtime index)
+#pragma unroll
+  for (int k = 0; k < 8; k++) f0[k] = f1[k] = f2[k] = 0;
+  uint8_t code = kParseOk;
+  uint32_t aux = 0;
+  if (len < 1 + 4 + 1 + 4 + 1 + 4 + 1) {
+    code = kParseTooSmall;
+    aux = (uint32_t)len;
+  } else if (b[0] != 1) {  // PROTOCOL_VERSION
+    code = kParseBadVersion;
+    aux = b[0];
+  } else {
+    uint64_t pos = 1;
+#pragma unroll 1
+    for (int q = 0; q < 3 && code == kParseOk; q++) {
+      const uint8_t base = (uint8_t)(kParseR1LenMissing + 5 * q);
+      const uint32_t maxlen = q < 2 ? 4096u : 512u;
+      if (pos + 4 > len) { code = base; break; }
+      const uint32_t fl = be32_at(b + pos);
+      pos += 4;
+      if (fl == 0 || fl > maxlen) { code = base + 1; aux = fl; break; }
+      if (pos + fl > len) { code = base + 2; break; }
+      if (fl != 32) { code = base + 3; aux = fl; break; }
+      uint32_t w[8];
+      words_at(w, b + pos);
+      pos += 32;
+      bool ok;
+      if (q < 2) {
+        ge_p3 P;
+        ok = ristretto_decode(P, w);
+      } else {
+        ok = sc_is_canonical(w);
+      }
+      if (!ok) { code = base + 4; break; }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        f0[k] = q == 0 ? w[k] : f0[k];
+        f1[k] = q == 1 ? w[k] : f1[k];
+        f2[k] = q == 2 ? w[k] : f2[k];
+      }
+    }
+    if (code == kParseOk && pos != len) {
+      code = kParseTrailing;
+      aux = (uint32_t)(len - pos);
+    }
+    if (code == kParseOk) {
+      // validate_element (ristretto.rs:173-185) holds for every decoded point.
+      if (words_zero(f0) || words_zero(f1)) code = kParseIdentity;
+      else if (words_zero(f2)) code = kParseZeroS;
+    }
+  }
+  store_words8(a.r1, i, f0);
+  store_words8(a.r2, i, f1);
+  store_words8(a.s, i, f2);
+  a.code[i] = code;
+  if (a.aux) a.aux[i] = aux;
+}
+
+// ---------------------------------------------------------------------------------------
 // Per-proof verification
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ void copy_niels_to_lds(ge_niels* dst, const ge_niels* src, int count) {
@@ -261,6 +344,12 @@ hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
   const int64_t blocks = (a.n + kVerifyBlock - 1) / kVerifyBlock;
   hipLaunchKernelGGL(k_prove_points, dim3((unsigned)blocks), dim3(kVerifyBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_parse_proofs(const ParseArgs& a, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_parse_proofs, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

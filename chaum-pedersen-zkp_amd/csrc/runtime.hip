@@ -76,7 +76,7 @@ struct cpz_ctx {
   // (g, h) cache
   bool have_gh = false;
   uint8_t gh[64];
-  DevBuf tab;       // 256 ge_niels
+  DevBuf tab;       // 4 x 128 ge_niels (g, h, 2^128 g, 2^128 h)
   DevBuf prefix;    // 2 StrobeSnap
   DevBuf gh_words;  // 16 words
   DevBuf ok_flags;  // 2 ints
@@ -87,6 +87,8 @@ struct cpz_ctx {
   // host-API staging
   DevBuf in[5];
   DevBuf ctxb, ctxo, ctxp;
+  // wire-format ingestion
+  DevBuf pz_blob, pz_off, pz_rows, pz_code, pz_aux;
   // RLC / Pippenger buffers (sized for the largest batch seen)
   DevBuf rl_pts, rl_dig, rl_bsum, rl_counts, rl_offsets, rl_bhist, rl_idx, rl_buckets, rl_segs, rl_segw, rl_win,
       rl_partial, rl_flags, rl_parts;
@@ -647,6 +649,7 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->ctxb.release();
   ctx->ctxo.release();
   ctx->ctxp.release();
+  for (DevBuf* b : {&ctx->pz_blob, &ctx->pz_off, &ctx->pz_rows, &ctx->pz_code, &ctx->pz_aux}) b->release();
   for (DevBuf* b : {&ctx->rl_pts, &ctx->rl_dig, &ctx->rl_bsum, &ctx->rl_counts, &ctx->rl_offsets, &ctx->rl_bhist,
                     &ctx->rl_idx, &ctx->rl_buckets, &ctx->rl_segs, &ctx->rl_segw, &ctx->rl_win, &ctx->rl_partial,
                     &ctx->rl_flags, &ctx->rl_parts})
@@ -737,6 +740,70 @@ int cpz_challenges(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_
   CPZ_HIP(cpz::launch_challenge(ca, ctx->stream));
   CPZ_HIP(hipMemcpyAsync(c_out, ctx->c.p, n * 32, hipMemcpyDeviceToHost, ctx->stream));
   CPZ_HIP(hipStreamSynchronize(ctx->stream));
+  return CPZ_OK;
+}
+
+int cpz_parse_proofs_device(cpz_ctx* ctx, size_t n, const void* d_blob, const uint64_t* d_off, void* d_r1,
+                            void* d_r2, void* d_s, void* d_code, void* d_aux, void* stream) {
+  if (!ctx) return fail(CPZ_EINVAL, "null context");
+  if (n == 0) return fail(CPZ_EEMPTY, "empty input");
+  if (!d_blob || !d_off || !d_r1 || !d_r2 || !d_s || !d_code) return fail(CPZ_EINVAL, "null input pointer");
+  if (!aligned16(d_r1) || !aligned16(d_r2) || !aligned16(d_s))
+    return fail(CPZ_EINVAL, "device row outputs must be 16-byte aligned");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  cpz::ParseArgs pa;
+  pa.n = (int64_t)n;
+  pa.blob = static_cast<const uint8_t*>(d_blob);
+  pa.off = d_off;
+  pa.r1 = static_cast<uint32_t*>(d_r1);
+  pa.r2 = static_cast<uint32_t*>(d_r2);
+  pa.s = static_cast<uint32_t*>(d_s);
+  pa.code = static_cast<uint8_t*>(d_code);
+  pa.aux = static_cast<uint32_t*>(d_aux);
+  CPZ_HIP(cpz::launch_parse_proofs(pa, st));
+  CPZ_HIP(hipStreamSynchronize(st));
+  return CPZ_OK;
+}
+
+int cpz_parse_proofs(cpz_ctx* ctx, size_t n, const uint8_t* blob, const uint64_t* off, uint8_t* r1_out,
+                     uint8_t* r2_out, uint8_t* s_out, uint8_t* code_out, uint32_t* aux_out) {
+  if (!ctx) return fail(CPZ_EINVAL, "null context");
+  if (n == 0) return fail(CPZ_EEMPTY, "empty input");
+  if (!blob || !off || !r1_out || !r2_out || !s_out || !code_out) return fail(CPZ_EINVAL, "null input pointer");
+  for (size_t i = 0; i < n; i++)
+    if (off[i + 1] < off[i]) return fail(CPZ_EINVAL, "offsets must be non-decreasing");
+  const size_t bytes = (size_t)(off[n] - off[0]);
+  std::vector<uint64_t> rel(n + 1);
+  for (size_t i = 0; i <= n; i++) rel[i] = off[i] - off[0];
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  CPZ_HIP(ctx->pz_blob.ensure(bytes + 16));
+  CPZ_HIP(ctx->pz_off.ensure((n + 1) * sizeof(uint64_t)));
+  CPZ_HIP(ctx->pz_rows.ensure(3 * n * 32));
+  CPZ_HIP(ctx->pz_code.ensure(n));
+  CPZ_HIP(ctx->pz_aux.ensure(n * sizeof(uint32_t)));
+  if (bytes) CPZ_HIP(hipMemcpyAsync(ctx->pz_blob.p, blob + off[0], bytes, hipMemcpyHostToDevice, st));
+  CPZ_HIP(hipMemcpyAsync(ctx->pz_off.p, rel.data(), (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  uint8_t* rows = static_cast<uint8_t*>(ctx->pz_rows.p);
+  cpz::ParseArgs pa;
+  pa.n = (int64_t)n;
+  pa.blob = static_cast<const uint8_t*>(ctx->pz_blob.p);
+  pa.off = static_cast<const uint64_t*>(ctx->pz_off.p);
+  pa.r1 = reinterpret_cast<uint32_t*>(rows);
+  pa.r2 = reinterpret_cast<uint32_t*>(rows + n * 32);
+  pa.s = reinterpret_cast<uint32_t*>(rows + 2 * n * 32);
+  pa.code = static_cast<uint8_t*>(ctx->pz_code.p);
+  pa.aux = static_cast<uint32_t*>(ctx->pz_aux.p);
+  CPZ_HIP(cpz::launch_parse_proofs(pa, st));
+  CPZ_HIP(hipMemcpyAsync(r1_out, rows, n * 32, hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipMemcpyAsync(r2_out, rows + n * 32, n * 32, hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipMemcpyAsync(s_out, rows + 2 * n * 32, n * 32, hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipMemcpyAsync(code_out, ctx->pz_code.p, n, hipMemcpyDeviceToHost, st));
+  if (aux_out) CPZ_HIP(hipMemcpyAsync(aux_out, ctx->pz_aux.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipStreamSynchronize(st));
   return CPZ_OK;
 }
 

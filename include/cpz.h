@@ -137,6 +137,40 @@ int cpz_msm(cpz_ctx *ctx, size_t n, const uint8_t *points, const uint8_t *scalar
  * *is_identity = 1 iff the combined batch equation holds. */
 int cpz_combine_partials(cpz_ctx *ctx, size_t k, const uint8_t *partials, uint8_t out[32], int *is_identity);
 
+/* Bulk wire-format ingestion: Proof::from_bytes (gadgets.rs:364-489) for n
+ * 109-byte-format blobs at blob[off[i] .. off[i+1]), on the device.  Writes the r1, r2, s rows
+ * (n x 32 B SoA, zero where not parsed) and one CPZ_PARSE_* code per blob -- the first check
+ * the reference would fail, in its order (each field's structure, then its decode
+ * element_from_bytes / scalar_from_bytes, before the next field; trailing bytes; identity
+ * commitment; zero s).  aux_out (optional) holds the value the reference's message prints
+ * (length, version or trailing-byte count).  Entries with a non-zero code are rejected before
+ * batching, as the service does (service.rs:501-507). */
+#define CPZ_PARSE_OK 0
+#define CPZ_PARSE_TOO_SMALL 1        /* InvalidParams "Proof too small: {aux} bytes" */
+#define CPZ_PARSE_BAD_VERSION 2      /* InvalidParams "Unsupported proof version: {aux}" */
+#define CPZ_PARSE_R1_LEN_MISSING 3   /* InvalidParams "Truncated proof: missing r1 length" */
+#define CPZ_PARSE_R1_LEN_INVALID 4   /* InvalidParams "Invalid r1 length: {aux}" */
+#define CPZ_PARSE_R1_TRUNCATED 5     /* InvalidParams "Truncated proof: incomplete r1 data" */
+#define CPZ_PARSE_R1_SIZE 6          /* InvalidGroupElement "Expected 32 bytes, got {aux}" */
+#define CPZ_PARSE_R1_POINT 7         /* InvalidGroupElement "Bytes do not represent a valid Ristretto point" */
+#define CPZ_PARSE_R2_LEN_MISSING 8   /* as 3..7 for r2 */
+#define CPZ_PARSE_R2_LEN_INVALID 9
+#define CPZ_PARSE_R2_TRUNCATED 10
+#define CPZ_PARSE_R2_SIZE 11
+#define CPZ_PARSE_R2_POINT 12
+#define CPZ_PARSE_S_LEN_MISSING 13   /* InvalidParams "Truncated proof: missing s length" */
+#define CPZ_PARSE_S_LEN_INVALID 14   /* InvalidParams "Invalid s length: {aux}" */
+#define CPZ_PARSE_S_TRUNCATED 15     /* InvalidParams "Truncated proof: incomplete s data" */
+#define CPZ_PARSE_S_SIZE 16          /* InvalidScalar "Expected 32 bytes, got {aux}" */
+#define CPZ_PARSE_S_SCALAR 17        /* InvalidScalar "Bytes do not represent a valid scalar" */
+#define CPZ_PARSE_TRAILING 18        /* InvalidParams "Proof has {aux} trailing bytes" */
+#define CPZ_PARSE_IDENTITY 19        /* InvalidParams "Commitment contains identity element" */
+#define CPZ_PARSE_ZERO_S 20          /* InvalidParams "Response scalar is zero" */
+int cpz_parse_proofs(cpz_ctx *ctx, size_t n, const uint8_t *blob, const uint64_t *off, uint8_t *r1_out,
+                     uint8_t *r2_out, uint8_t *s_out, uint8_t *code_out, uint32_t *aux_out);
+int cpz_parse_proofs_device(cpz_ctx *ctx, size_t n, const void *d_blob, const uint64_t *d_off, void *d_r1,
+                            void *d_r2, void *d_s, void *d_code, void *d_aux, void *stream);
+
 /* Per-kernel timing (HIP events recorded on the launch stream around every kernel).
  * Stages: 0 = k_challenge, 1 = k_verify_each, 2 = RLC decode/weights, 3 = RLC MSM,
  * 4 = fallback.  cpz_ctx_stage_times synchronises, writes the summed milliseconds and

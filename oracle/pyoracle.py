@@ -680,3 +680,41 @@ def proof_from_bytes(b: bytes):
     if int.from_bytes(s, "little") == 0:
         return "err", "InvalidParams"
     return "ok", (r1, r2, s)
+
+
+def proof_from_bytes_code(b: bytes):
+    """(code, aux) of Proof::from_bytes (gadgets.rs:364-489) with the bulk parser's numbering
+    (include/cpz.h CPZ_PARSE_*): the first check the reference fails, in its order; aux is
+    the value its message prints (length, version, trailing count) or 0."""
+    if len(b) < 1 + 4 + 1 + 4 + 1 + 4 + 1:
+        return 1, len(b)
+    if b[0] != PROTOCOL_VERSION:
+        return 2, b[0]
+    pos = 1
+    parts = []
+    for q, maxlen in enumerate((4096, 4096, 512)):
+        base = 3 + 5 * q
+        if pos + 4 > len(b):
+            return base, 0
+        ln = struct.unpack(">I", b[pos:pos + 4])[0]
+        pos += 4
+        if ln == 0 or ln > maxlen:
+            return base + 1, ln
+        if pos + ln > len(b):
+            return base + 2, 0
+        if ln != 32:                       # element_from_bytes / scalar_from_bytes size check
+            return base + 3, ln
+        field = b[pos:pos + 32]
+        pos += 32
+        ok = (ristretto_decode(field) is not None) if q < 2 else (scalar_from_canonical(field) is not None)
+        if not ok:
+            return base + 4, 0
+        parts.append(field)
+    if pos != len(b):
+        return 18, len(b) - pos
+    r1, r2, s = parts
+    if pt_is_identity(ristretto_decode(r1)) or pt_is_identity(ristretto_decode(r2)):
+        return 19, 0
+    if int.from_bytes(s, "little") == 0:
+        return 20, 0
+    return 0, 0

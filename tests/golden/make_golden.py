@@ -238,6 +238,46 @@ def main():
                 "statuses": [O.verify_one(r) for r in forged_set]})
     out["rlc"] = rlc
 
+    # 7. Wire format (Proof::from_bytes, gadgets.rs:364-489): valid blobs, every truncation,
+    #    bad versions / lengths / points / scalars, trailing bytes, identity / zero, and
+    #    doubly-malformed blobs where the reference's order of checks decides the error.
+    import struct
+    def blob(r1, r2, s, ver=1, l1=None, l2=None, l3=None, tail=b""):
+        return (bytes([ver]) + struct.pack(">I", len(r1) if l1 is None else l1) + r1 +
+                struct.pack(">I", len(r2) if l2 is None else l2) + r2 +
+                struct.pack(">I", len(s) if l3 is None else l3) + s + tail)
+    good = recs[0]
+    gb = blob(good.r1, good.r2, good.s)
+    assert len(gb) == 109 and gb == O.proof_to_bytes(good.r1, good.r2, good.s)
+    bad_pt = bytes.fromhex(RFC_BAD[3])
+    big_s = L.to_bytes(32, "little")
+    wire = [gb, blob(recs[1].r1, recs[1].r2, recs[1].s)]
+    wire += [gb[:k] for k in range(0, 109)]                      # every truncation
+    wire += [bytes([v]) + gb[1:] for v in (0, 2, 255)]           # versions
+    wire += [gb + b"\x00", gb + b"\x01\x02\x03\x04\x05"]       # trailing
+    wire += [blob(good.r1, good.r2, good.s, l1=0), blob(good.r1, good.r2, good.s, l1=4097),
+             blob(good.r1, good.r2, good.s, l2=0), blob(good.r1, good.r2, good.s, l2=5000),
+             blob(good.r1, good.r2, good.s, l3=0), blob(good.r1, good.r2, good.s, l3=513),
+             blob(good.r1 + b"\x00", good.r2, good.s), blob(good.r1[:31], good.r2, good.s),
+             blob(good.r1, good.r2 + b"\x07", good.s), blob(good.r1, good.r2[:30], good.s),
+             blob(good.r1, good.r2, good.s + b"\x00"), blob(good.r1, good.r2, good.s[:31]),
+             blob(good.r1, good.r2, good.s, l1=4096)]
+    wire += [blob(bad_pt, good.r2, good.s), blob(good.r1, bad_pt, good.s), blob(good.r1, good.r2, big_s),
+             blob(bytes(32), good.r2, good.s), blob(good.r1, bytes(32), good.s), blob(good.r1, good.r2, bytes(32))]
+    # precedence: r1 decode before r2 structure; r2 decode before s; s before trailing;
+    # trailing before identity; identity before zero s
+    wire += [blob(bad_pt, good.r2, good.s)[:50], blob(bad_pt, good.r2, good.s, l2=0),
+             blob(good.r1, bad_pt, good.s)[:90], blob(good.r1, bad_pt, good.s, l3=600),
+             blob(good.r1, good.r2, big_s, tail=b"\x00"), blob(bytes(32), good.r2, good.s, tail=b"\x00"),
+             blob(bytes(32), good.r2, bytes(32)), blob(bad_pt, bad_pt, big_s, tail=b"zz")]
+    for rb in RFC_BAD[:12]:
+        wire.append(blob(good.r1, bytes.fromhex(rb), good.s))
+    out["wire"] = [{"blob": w.hex(), "code": O.proof_from_bytes_code(w)[0], "aux": O.proof_from_bytes_code(w)[1]}
+                   for w in wire]
+    for w, e in zip(wire, out["wire"]):  # the coarse oracle (error kind) agrees
+        kind = O.proof_from_bytes(w)
+        assert (kind[0] == "ok") == (e["code"] == 0)
+
     path = os.path.join(HERE, "golden.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)

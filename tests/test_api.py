@@ -74,3 +74,28 @@ def test_verify_result_mapping():
     assert isinstance(cp.VerifyResult(2).error(), cp.InvalidGroupElement)
     assert isinstance(cp.VerifyResult(3).error(), cp.InvalidScalar)
     assert isinstance(cp.VerifyResult(4).error(), cp.InvalidParams)
+
+
+def test_parse_error_messages():
+    """Bulk-parser codes map to the reference's error types and messages (gadgets.rs:364-489)."""
+    assert cp.parse_error(0) is None
+    assert set(cp.PARSE_ERRORS) == set(range(1, 21))
+    e = cp.parse_error(1, 17)
+    assert isinstance(e, cp.InvalidParams) and str(e).endswith("Proof too small: 17 bytes")
+    assert isinstance(cp.parse_error(7), cp.InvalidGroupElement)
+    assert isinstance(cp.parse_error(16, 31), cp.InvalidScalar) and "got 31" in str(cp.parse_error(16, 31))
+    assert "Proof has 5 trailing bytes" in str(cp.parse_error(18, 5))
+
+
+def test_wire_golden_oracle_codes(golden):
+    """The committed wire fixtures agree with the oracle's from_bytes (structural Python mirror too)."""
+    import pyoracle as O
+    for w in golden["wire"]:
+        b = bytes.fromhex(w["blob"])
+        assert O.proof_from_bytes_code(b) == (w["code"], w["aux"])
+        struct_codes = {1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 13, 14, 15, 16, 18}
+        if w["code"] in struct_codes:
+            with pytest.raises(cp.Error) as exc:
+                cp.Proof.from_bytes(b)
+            ref = cp.parse_error(w["code"], w["aux"])
+            assert type(exc.value) is type(ref) and str(exc.value) == str(ref)
