@@ -135,25 +135,54 @@ CPZ_HD void fe_check_operand(const fe& a) {
 CPZ_HD void fe_check_operand(const fe&) {}
 #endif
 
-// Signed carry chain on 64-bit column sums -> tight limbs.
-CPZ_HD fe fe_carry_wide(int64_t h[10]) {
-  int64_t c;
-  c = (h[0] + (1 << 25)) >> 26; h[1] += c; h[0] -= c * (1LL << 26);
-  c = (h[4] + (1 << 25)) >> 26; h[5] += c; h[4] -= c * (1LL << 26);
-  c = (h[1] + (1 << 24)) >> 25; h[2] += c; h[1] -= c * (1LL << 25);
-  c = (h[5] + (1 << 24)) >> 25; h[6] += c; h[5] -= c * (1LL << 25);
-  c = (h[2] + (1 << 25)) >> 26; h[3] += c; h[2] -= c * (1LL << 26);
-  c = (h[6] + (1 << 25)) >> 26; h[7] += c; h[6] -= c * (1LL << 26);
-  c = (h[3] + (1 << 24)) >> 25; h[4] += c; h[3] -= c * (1LL << 25);
-  c = (h[7] + (1 << 24)) >> 25; h[8] += c; h[7] -= c * (1LL << 25);
-  c = (h[4] + (1 << 25)) >> 26; h[5] += c; h[4] -= c * (1LL << 26);
-  c = (h[8] + (1 << 25)) >> 26; h[9] += c; h[8] -= c * (1LL << 26);
-  c = (h[9] + (1 << 24)) >> 25; h[0] += c * 19; h[9] -= c * (1LL << 25);
-  c = (h[0] + (1 << 25)) >> 26; h[1] += c; h[0] -= c * (1LL << 26);
+// Carry bias of column k: 2^(w_k - 1), w = 26, 25, 26, ...  Column accumulators start
+// at this value (the first v_mad_i64_i32 adds it for free), so each carry step is just
+//   c = H_k >> w_k,  H_(k+1) += c,  limb_k = (lo(H_k) & (2^w_k - 1)) - 2^(w_k - 1)
+// (a 64-bit shift, a 64-bit add and two cheap 32-bit ops), which is the centred residue
+// h_k - 2^w_k * round(h_k / 2^w_k) of the unbiased column h_k = H_k - bias_k.
+CPZ_HD constexpr int64_t carry_bias(int k) { return (k & 1) ? (1LL << 24) : (1LL << 25); }
+
+// Opaque copy of a column accumulator.  Every partial column sum goes through it, so
+// LLVM cannot reassociate the sum (it would move the constant carry bias to the end, or
+// split the chain into two halves, each costing an extra 64-bit add): column k is then
+// exactly one v_mad_i64_i32 per product, the first one adding the bias from an SGPR pair.
+// Non-volatile, so the scheduler still interleaves the ten columns freely.
+CPZ_HD int64_t acc_pin(int64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(x));
+#endif
+  return x;
+}
+
+CPZ_HD int32_t unbias_limb(int64_t H, int k) {
+  const uint32_t mask = (k & 1) ? 0x1ffffffu : 0x3ffffffu;
+  return (int32_t)(((uint32_t)H & mask) - (uint32_t)carry_bias(k));
+}
+
+// Biased column sums -> tight limbs.  One chain 0 -> 1 -> ... -> 9 -> 0 (x19) -> 1: every
+// column is carried once and the small wrap-around carry into limb 0 once more, so no
+// reduced limb has to be widened back to 64 bits (the two-chain ref10 order needs that
+// twice and is ~15 % more VALU work here).
+CPZ_HD fe fe_carry_biased(int64_t H[10]) {
   fe r;
 #pragma unroll
-  for (int i = 0; i < 10; i++) r.v[i] = (int32_t)h[i];
+  for (int k = 0; k < 9; k++) {
+    H[k + 1] += H[k] >> ((k & 1) ? 25 : 26);
+    r.v[k] = unbias_limb(H[k], k);
+  }
+  const int64_t c9 = H[9] >> 25;
+  r.v[9] = unbias_limb(H[9], 9);
+  const int64_t h0 = (int64_t)r.v[0] + 19 * c9 + carry_bias(0);
+  r.v[1] += (int32_t)(h0 >> 26);
+  r.v[0] = unbias_limb(h0, 0);
   return r;
+}
+
+// Unbiased 64-bit columns -> tight limbs.
+CPZ_HD fe fe_carry_wide(int64_t h[10]) {
+#pragma unroll
+  for (int k = 0; k < 10; k++) h[k] += carry_bias(k);
+  return fe_carry_biased(h);
 }
 
 // h = f * g.  Column k collects f_i g_j with (i + j) % 10 == k, times 19 when i + j >= 10
@@ -165,39 +194,36 @@ CPZ_HD fe fe_mul(const fe& f, const fe& g) {
   int32_t g19[10], f2[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    g19[i] = 19 * g.v[i];
-    f2[i] = 2 * f.v[i];
+    g19[i] = (int32_t)(19u * (uint32_t)g.v[i]);
+    f2[i] = (int32_t)(2u * (uint32_t)f.v[i]);
   }
   int64_t h[10];
 #pragma unroll
-  for (int k = 0; k < 10; k++) {
-    int64_t acc = 0;
+  for (int i = 0; i < 10; i++) {
 #pragma unroll
-    for (int i = 0; i < 10; i++) {
+    for (int k = 0; k < 10; k++) {
       const int j = (k - i + 10) % 10;
       const int32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
       const int32_t b = (i + j >= 10) ? g19[j] : g.v[j];
-      acc += (int64_t)a * (int64_t)b;
+      h[k] = acc_pin((int64_t)a * (int64_t)b + (i == 0 ? carry_bias(k) : h[k]));
     }
-    h[k] = acc;
   }
-  fe r = fe_carry_wide(h);
+  fe r = fe_carry_biased(h);
   CPZ_SEQ();
   return r;
 }
 
-// Column sums of f^2, using f_i f_j = f_j f_i: 55 products.
-CPZ_HD void fe_sq_wide(int64_t h[10], const fe& f) {
+// Column sums of f^2 (using f_i f_j = f_j f_i: 55 products), each started at bias_k / div.
+CPZ_HD void fe_sq_wide(int64_t h[10], const fe& f, int div) {
   CPZ_COUNT(sq);
   fe_check_operand(f);
   int32_t f2[10], f19[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) {
-    f2[i] = 2 * f.v[i];
-    f19[i] = 19 * f.v[i];
+    f2[i] = (int32_t)(2u * (uint32_t)f.v[i]);
+    f19[i] = (int32_t)(19u * (uint32_t)f.v[i]);
   }
-#pragma unroll
-  for (int k = 0; k < 10; k++) h[k] = 0;
+  bool first[10] = {true, true, true, true, true, true, true, true, true, true};
 #pragma unroll
   for (int i = 0; i < 10; i++) {
 #pragma unroll
@@ -205,9 +231,10 @@ CPZ_HD void fe_sq_wide(int64_t h[10], const fe& f) {
       const int k = (i + j) % 10;
       // coefficient = (i != j ? 2 : 1) * (both odd ? 2 : 1) * (i + j >= 10 ? 19 : 1)
       const int m2 = (i != j ? 2 : 1) * (((i & 1) && (j & 1)) ? 2 : 1);
-      const int32_t a = (m2 == 1) ? f.v[i] : (m2 == 2 ? f2[i] : 2 * f2[i]);
+      const int32_t a = (m2 == 1) ? f.v[i] : (m2 == 2 ? f2[i] : (int32_t)(2u * (uint32_t)f2[i]));
       const int32_t b = (i + j >= 10) ? f19[j] : f.v[j];
-      h[k] += (int64_t)a * (int64_t)b;
+      h[k] = acc_pin((int64_t)a * (int64_t)b + (first[k] ? carry_bias(k) / div : h[k]));
+      first[k] = false;
     }
   }
 }
@@ -215,19 +242,20 @@ CPZ_HD void fe_sq_wide(int64_t h[10], const fe& f) {
 // h = f^2.
 CPZ_HD fe fe_sq(const fe& f) {
   int64_t h[10];
-  fe_sq_wide(h, f);
-  fe r = fe_carry_wide(h);
+  fe_sq_wide(h, f, 1);
+  fe r = fe_carry_biased(h);
   CPZ_SEQ();
   return r;
 }
 
-// h = 2 f^2 (tight), as dalek's square2: the doubling is folded into the column sums.
+// h = 2 f^2 (tight), as dalek's square2: the doubling is folded into the column sums
+// (which start at half the bias, so the doubled sums carry the full bias).
 CPZ_HD fe fe_sq2(const fe& f) {
   int64_t h[10];
-  fe_sq_wide(h, f);
+  fe_sq_wide(h, f, 2);
 #pragma unroll
   for (int i = 0; i < 10; i++) h[i] += h[i];
-  fe r = fe_carry_wide(h);
+  fe r = fe_carry_biased(h);
   CPZ_SEQ();
   return r;
 }
