@@ -71,7 +71,7 @@ struct VerifyArgs {
   const uint32_t* s;
   const uint32_t* c;
   uint8_t* status;               // in: response-scalar status; out: final status
-  const ge_niels* tab;           // 128 entries each: g, h, 2^128 g, 2^128 h
+  const ge_niels* comb;          // fixed-base combs of g then h, kCombPerBase entries each
   ge_cached* scratch;            // grid * kVerifyBlock * kCachedEntries entries
 };
 
@@ -80,7 +80,7 @@ struct ProveArgs {
   uint64_t first_index;
   uint32_t seed_x[8];
   uint32_t seed_k[8];
-  const ge_niels* tab;
+  const ge_niels* comb;          // fixed-base combs of g then h
   uint32_t* y1;
   uint32_t* y2;
   uint32_t* r1;
@@ -93,6 +93,8 @@ hipError_t launch_transcript_prefix(const uint32_t* gh_words, StrobeSnap* out, h
 hipError_t launch_challenge(const ChallengeArgs& a, hipStream_t st);
 hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, hipStream_t st);
 hipError_t launch_parse_proofs(const ParseArgs& a, hipStream_t st);
+// Fixed-base combs of 2 bases (g, h): bases_scratch holds 2 * kCombWindows ge_p3.
+hipError_t launch_build_comb(const uint32_t* gh_words, ge_p3* bases_scratch, ge_niels* comb, hipStream_t st);
 hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st);
 hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st);
 hipError_t launch_prove_response(const ProveArgs& a, hipStream_t st);

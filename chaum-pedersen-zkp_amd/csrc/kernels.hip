@@ -150,6 +150,39 @@ __global__ void __launch_bounds__(64) k_build_niels(const uint32_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------
+// Fixed-base combs (scalarmul.h): comb[b][k][j - 1] = j * 2^(16 k) * base_b, affine Niels.
+// k_comb_bases: thread (b, k) doubles base_b 16 k times.  k_comb_fill: one thread per
+// entry, [j] Q_(b,k) by double-and-add over the 15-bit j, then one inversion to affine.
+// 2^20 entries, a few milliseconds, once per (g, h) pair.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_comb_bases(const uint32_t* __restrict__ gh_words, ge_p3* __restrict__ q) {
+  const int t = threadIdx.x;
+  if (t >= 2 * kCombWindows) return;
+  const int b = t / kCombWindows, k = t % kCombWindows;
+  ge_p3 B;
+  (void)ristretto_decode(B, gh_words + 8 * b);  // validity is checked by k_build_niels
+#pragma unroll 1
+  for (int d = 0; d < 16 * k; d++) B = p1p1_to_p3(p3_dbl(B));
+  q[t] = B;
+}
+
+__global__ void __launch_bounds__(256) k_comb_fill(const ge_p3* __restrict__ q, ge_niels* __restrict__ comb) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= 2 * kCombPerBase) return;
+  const int bk = (int)(t / kCombEntries);  // b * kCombWindows + k
+  const int j = (int)(t % kCombEntries) + 1;
+  const ge_p3 Q = q[bk];
+  ge_p3 acc = Q;  // bit 15 of j set only for j = 2^15
+  const int top = 31 - __builtin_clz((unsigned)j);
+#pragma unroll 1
+  for (int bit = top - 1; bit >= 0; bit--) {
+    acc = p1p1_to_p3(p3_dbl(acc));
+    if ((j >> bit) & 1) acc = ge_add(acc, Q);
+  }
+  comb[t] = p3_to_niels(acc);
+}
+
+// ---------------------------------------------------------------------------------------
 // Bulk wire-format ingestion: Proof::from_bytes (gadgets.rs:364-489) for n blobs, one
 // thread per blob, checks in the reference's order -- structural checks of each field,
 // each field decoded (element_from_bytes / scalar_from_bytes) before the next field's
@@ -234,22 +267,9 @@ __global__ void __launch_bounds__(256) k_parse_proofs(ParseArgs a) {
 // ---------------------------------------------------------------------------------------
 // Per-proof verification
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ void copy_niels_to_lds(ge_niels* dst, const ge_niels* src, int count) {
-  const uint4* s = reinterpret_cast<const uint4*>(src);
-  uint4* d = reinterpret_cast<uint4*>(dst);
-  const int nvec = count * (int)sizeof(ge_niels) / 16;
-  for (int v = threadIdx.x; v < nvec; v += blockDim.x) d[v] = s[v];
-}
 
 __global__ void __launch_bounds__(kVerifyBlock, 2) k_verify_each(VerifyArgs a) {
-  // g, h, 2^128 g, 2^128 h: 4 x 128 Niels entries = 64 KB of LDS
-  __shared__ ge_niels tabs[4 * kNielsEntries];
-  copy_niels_to_lds(tabs, a.tab, 4 * kNielsEntries);
-  __syncthreads();
-  const ge_niels* tab_g = tabs;
-  const ge_niels* tab_h = tabs + kNielsEntries;
-  const ge_niels* tab_g2 = tabs + 2 * kNielsEntries;
-  const ge_niels* tab_h2 = tabs + 3 * kNielsEntries;
+  const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
   const int64_t gtid = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * kVerifyBlock;
   ge_cached* tab_v = a.scratch + gtid * kCachedEntries;
@@ -259,8 +279,8 @@ __global__ void __launch_bounds__(kVerifyBlock, 2) k_verify_each(VerifyArgs a) {
     uint32_t sw[8], cw[8];
     load_words8(sw, a.s, i);
     load_words8(cw, a.c, i);
-    a.status[i] = verify_proof(a.y1 + 8 * i, a.y2 + 8 * i, a.r1 + 8 * i, a.r2 + 8 * i, sw, cw, a.status[i],
-                               tab_g, tab_h, tab_g2, tab_h2, tab_v);
+    a.status[i] = verify_proof(a.y1 + 8 * i, a.y2 + 8 * i, a.r1 + 8 * i, a.r2 + 8 * i, sw, cw, a.status[i], comb_g,
+                               comb_h, tab_v);
   }
 }
 
@@ -274,30 +294,26 @@ __device__ __forceinline__ sc chacha_scalar(const uint32_t key[8], uint64_t coun
 }
 
 __global__ void __launch_bounds__(kVerifyBlock, 2) k_prove_points(ProveArgs a) {
-  __shared__ ge_niels tab_g[kNielsEntries];
-  __shared__ ge_niels tab_h[kNielsEntries];
-  copy_niels_to_lds(tab_g, a.tab, kNielsEntries);
-  copy_niels_to_lds(tab_h, a.tab + kNielsEntries, kNielsEntries);
-  __syncthreads();
+  const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
   const int64_t i = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
   if (i >= a.n) return;
   const uint64_t idx = a.first_index + (uint64_t)i;
   uint32_t d[8], w[8];
   {
     const sc x = chacha_scalar(a.seed_x, idx);
-    sc_recode_radix256(d, x.w);
+    sc_recode_radix65536(d, x.w);
   }
-  ristretto_encode(w, fixed_base_mul(tab_g, d));
+  ristretto_encode(w, comb_mul(comb_g, d));
   store_words8(a.y1, i, w);
-  ristretto_encode(w, fixed_base_mul(tab_h, d));
+  ristretto_encode(w, comb_mul(comb_h, d));
   store_words8(a.y2, i, w);
   {
     const sc k = chacha_scalar(a.seed_k, idx);
-    sc_recode_radix256(d, k.w);
+    sc_recode_radix65536(d, k.w);
   }
-  ristretto_encode(w, fixed_base_mul(tab_g, d));
+  ristretto_encode(w, comb_mul(comb_g, d));
   store_words8(a.r1, i, w);
-  ristretto_encode(w, fixed_base_mul(tab_h, d));
+  ristretto_encode(w, comb_mul(comb_h, d));
   store_words8(a.r2, i, w);
 }
 
@@ -331,6 +347,13 @@ hipError_t launch_challenge(const ChallengeArgs& a, hipStream_t st) {
 hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, hipStream_t st) {
   const int total = 2 * nbases * kNielsEntries;
   hipLaunchKernelGGL(k_build_niels, dim3((total + 63) / 64), dim3(64), 0, st, base_words, nbases, tab, ok);
+  return hipGetLastError();
+}
+
+hipError_t launch_build_comb(const uint32_t* gh_words, ge_p3* bases_scratch, ge_niels* comb, hipStream_t st) {
+  hipLaunchKernelGGL(k_comb_bases, dim3(1), dim3(64), 0, st, gh_words, bases_scratch);
+  hipLaunchKernelGGL(k_comb_fill, dim3((unsigned)(2 * kCombPerBase / 256)), dim3(256), 0, st,
+                     (const ge_p3*)bases_scratch, comb);
   return hipGetLastError();
 }
 

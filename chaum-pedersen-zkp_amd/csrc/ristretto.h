@@ -165,6 +165,9 @@ CPZ_HD bool ristretto_equal(const ge_p3& a, const ge_p3& b) {
 // Equal to the identity (0 : 1 : 1 : 0) in the ristretto sense: X == 0 or Y == 0.
 CPZ_HD bool ristretto_is_identity(const ge_p3& a) { return fe_iszero(a.X) || fe_iszero(a.Y); }
 
+// The same test on a completed point ((X:Z), (Y:T)), Z, T != 0: x == 0 or y == 0.
+CPZ_HD bool ristretto_is_identity(const ge_p1p1& a) { return fe_iszero(a.X) || fe_iszero(a.Y); }
+
 // 8 little-endian words of an encoding.
 CPZ_HD bool words_lt_p(const uint32_t w[8]) {
   // p = 2^255 - 19 : words ffffffed ffffffff x6 7fffffff.  s < p iff s - p borrows.

@@ -3,6 +3,7 @@
 //
 // Call sequence for cpz_verify_each (replaces BatchVerifier::verify, batch.rs:171-231):
 //   [cache miss on (g, h)]  k_build_niels(g, h) + k_transcript_prefix(g, h)
+//                           + k_comb_bases / k_comb_fill (128 MiB fixed-base combs)
 //   k_challenge   -> c_i, response-scalar status          (transcript + gadgets checks)
 //   k_verify_each -> final status                         (decode + two equations)
 #include <hip/hip_runtime.h>
@@ -77,6 +78,8 @@ struct cpz_ctx {
   bool have_gh = false;
   uint8_t gh[64];
   DevBuf tab;       // 4 x 128 ge_niels (g, h, 2^128 g, 2^128 h)
+  DevBuf comb;      // fixed-base combs of g and h: 2 x 16 x 2^15 ge_niels (128 MiB)
+  DevBuf comb_q;    // 32 ge_p3: 2^(16 k) g, 2^(16 k) h
   DevBuf prefix;    // 2 StrobeSnap
   DevBuf gh_words;  // 16 words
   DevBuf ok_flags;  // 2 ints
@@ -162,6 +165,11 @@ int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32]) {
     ctx->have_gh = false;
     return fail(CPZ_EGENERATOR, "generator encoding does not decode to a ristretto255 point");
   }
+  CPZ_HIP(ctx->comb.ensure((size_t)2 * cpz::kCombPerBase * sizeof(cpz::ge_niels)));
+  CPZ_HIP(ctx->comb_q.ensure((size_t)2 * cpz::kCombWindows * sizeof(cpz::ge_p3)));
+  CPZ_HIP(cpz::launch_build_comb(static_cast<const uint32_t*>(ctx->gh_words.p), static_cast<cpz::ge_p3*>(ctx->comb_q.p),
+                                 static_cast<cpz::ge_niels*>(ctx->comb.p), ctx->stream));
+  CPZ_HIP(hipStreamSynchronize(ctx->stream));  // callers may launch on another stream
   std::memcpy(ctx->gh, both, 64);
   ctx->have_gh = true;
   return CPZ_OK;
@@ -211,7 +219,7 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   va.s = ca.s;
   va.c = ca.c_out;
   va.status = status;
-  va.tab = static_cast<const cpz::ge_niels*>(ctx->tab.p);
+  va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
   va.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p);
   {
     StageTimer t(ctx, 1, st);
@@ -389,8 +397,7 @@ int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const voi
     va.s = static_cast<const uint32_t*>(s) + 8 * a;
     va.c = static_cast<const uint32_t*>(ctx->c.p) + 8 * a;
     va.status = status + a;  // decode-level status in, final status out
-    va.tab = static_cast<const cpz::ge_niels*>(ctx->tab.p);
-    va.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p);
+    va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
     const int grid = verify_grid(ctx, (size_t)(b - a));
     CPZ_HIP(ctx->scratch.ensure((size_t)grid * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached)));
     va.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p);
@@ -639,6 +646,8 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   }
   for (auto e : ctx->free_events) (void)hipEventDestroy(e);
   ctx->tab.release();
+  ctx->comb.release();
+  ctx->comb_q.release();
   ctx->prefix.release();
   ctx->gh_words.release();
   ctx->ok_flags.release();
@@ -827,7 +836,7 @@ int cpz_prove_synthetic_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t 
   pa.first_index = first_index;
   std::memcpy(pa.seed_x, seed_x, 32);
   std::memcpy(pa.seed_k, seed_k, 32);
-  pa.tab = static_cast<const cpz::ge_niels*>(ctx->tab.p);
+  pa.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
   pa.y1 = static_cast<uint32_t*>(d_y1);
   pa.y2 = static_cast<uint32_t*>(d_y2);
   pa.r1 = static_cast<uint32_t*>(d_r1);

@@ -207,6 +207,24 @@ CPZ_HD void sc_recode_radix256(uint32_t out[8], const uint32_t s[8]) {
   }
 }
 
+// Signed radix-2^16 recoding of a scalar < 2^253: 16 digits in [-2^15, 2^15 - 1] packed
+// as int16 halves, digit i in half i%2 of word i/2 (the fixed-base comb of scalarmul.h).
+CPZ_HD void sc_recode_radix65536(uint32_t out[8], const uint32_t s[8]) {
+  int32_t carry = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+      const int32_t n = (int32_t)((s[j] >> (16 * m)) & 0xffffu) + carry;
+      carry = (n + 32768) >> 16;
+      const int32_t d = n - (carry << 16);
+      packed |= ((uint32_t)d & 0xffffu) << (16 * m);
+    }
+    out[j] = packed;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Half-size decomposition of a challenge (2-dimensional lattice reduction by the partial
 // extended Euclidean algorithm, cf. T. Pornin, "Optimized Lattice Basis Reduction In

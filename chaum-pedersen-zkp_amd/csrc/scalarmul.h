@@ -15,6 +15,32 @@ namespace cpz {
 constexpr int kTableV = 8;     // cached multiples 1..8 of a variable base (radix-16 digits)
 constexpr int kTableB = 128;   // Niels multiples 1..128 of a fixed base (radix-256 digits)
 
+// Fixed-base comb: for each of the 16 radix-2^16 windows k, the affine Niels multiples
+// j * 2^(16 k) * B, j = 1..2^15, of one base (64 MiB per base in HBM).  [s] B for any
+// s < 2^253 is then 16 mixed additions and no doubling.
+constexpr int kCombWindows = 16;
+constexpr int kCombEntries = 1 << 15;
+constexpr int64_t kCombPerBase = (int64_t)kCombWindows * kCombEntries;
+
+// Device view of one base's comb (entries in global memory).
+struct CombTable {
+  const ge_niels* p;
+  CPZ_HDM ge_niels lookup(int k, int digit) const {
+    const int mag = digit < 0 ? -digit : digit;
+    const ge_niels* e = p + (int64_t)k * kCombEntries + (mag == 0 ? 0 : mag - 1);
+    ge_niels r;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint4* s = reinterpret_cast<const uint4*>(e);
+    uint4* d = reinterpret_cast<uint4*>(&r);
+#pragma unroll
+    for (int v = 0; v < (int)(sizeof(ge_niels) / 16); v++) d[v] = s[v];
+#else
+    r = *e;
+#endif
+    return ge_niels_cneg(mag == 0 ? ge_niels_identity() : r, digit < 0);
+  }
+};
+
 CPZ_HD ge_cached cached_load(const ge_cached* p) {
   ge_cached r;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -153,6 +179,68 @@ CPZ_HD ge_p3 straus_half(const ge_cached* tab_y, const ge_cached* tab_r, const g
     }
   }
   return p1p1_to_p3(cur);
+}
+
+// Adds [s] B to a pending completed point through the comb (16 mixed additions).
+// sdig: 16 radix-2^16 signed digits (sc_recode_radix65536).
+template <class Comb>
+CPZ_HD ge_p1p1 comb_add(ge_p1p1 cur, const Comb& comb, const uint32_t sdig_in[8]) {
+  uint32_t sd[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) sd[j] = sdig_in[j];
+#pragma unroll 1
+  for (int j = 0; j < 8; j++) {
+    const uint32_t w = sd[0];
+#pragma unroll
+    for (int t = 0; t < 7; t++) sd[t] = sd[t + 1];
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+      const int d = (int32_t)(w << (16 - 16 * m)) >> 16;
+      cur = ge_add_niels(p1p1_to_p3(cur), comb.lookup(2 * j + m, d));
+    }
+  }
+  return cur;
+}
+
+// Half-size per-proof check with the comb (see verify.h):
+//   Q = [u] Y' + [v] R' (Straus, 31 x 4 doublings, 64 cached additions) + [s'] B (comb),
+// returned as a completed point (callers only test it for the identity).
+// tab_y / tab_r: cached multiples 1..8 of Y' / R'; udig, vdig: 32 radix-16 signed digits of
+// u, |v| < 6 * 2^124; sdig: 16 radix-2^16 signed digits of s' < 2^253.
+template <class Comb>
+CPZ_HD ge_p1p1 straus_half_comb(const ge_cached* tab_y, const ge_cached* tab_r, const Comb& comb,
+                              const uint32_t udig_in[4], const uint32_t vdig_in[4], const uint32_t sdig[8]) {
+  uint32_t ud[4], vd[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    ud[j] = udig_in[j];
+    vd[j] = vdig_in[j];
+  }
+  ge_p1p1 cur = p1p1_identity();
+#pragma unroll 1
+  for (int j = 3; j >= 0; j--) {
+    const uint32_t wu = ud[3], wv = vd[3];
+#pragma unroll
+    for (int t = 3; t > 0; t--) {
+      ud[t] = ud[t - 1];
+      vd[t] = vd[t - 1];
+    }
+#pragma unroll 1
+    for (int m = 7; m >= 0; m--) {
+      if (j != 3 || m != 7) cur = dbl4(cur);
+      const int du = ((int32_t)(wu << (28 - 4 * m))) >> 28;
+      cur = ge_add_cached(p1p1_to_p3(cur), cached_lookup(tab_y, du));
+      const int dv = ((int32_t)(wv << (28 - 4 * m))) >> 28;
+      cur = ge_add_cached(p1p1_to_p3(cur), cached_lookup(tab_r, dv));
+    }
+  }
+  return comb_add(cur, comb, sdig);
+}
+
+// [s] B through the comb (prover path): 16 mixed additions.
+template <class Comb>
+CPZ_HD ge_p3 comb_mul(const Comb& comb, const uint32_t sdig[8]) {
+  return p1p1_to_p3(comb_add(p1p1_identity(), comb, sdig));
 }
 
 // [s] B by Horner over radix-256 signed digits (prover path).

@@ -80,12 +80,13 @@ CPZ_HD void transcript_parameters(Strobe<Acc>& s, const uint32_t g[8], const uin
 //   Q = [v s mod l] B + [u] (-Y) + [v] (-R)  lies in E[4]   <=>   [s] B - [c] Y == R.
 // (Decoded points lie in 2E = Z_l x Z_4; ristretto equality is equality modulo E[4].
 // Multiplying by v != 0 (mod l) keeps the Z_l part zero iff it was; [v c] Y and [u] Y,
-// [v s] B and [v s mod l] B differ by elements of E[4].)  B = g or h, B' = 2^128 B;
-// s' = v s mod l (sdig, radix 256) splits as s'_lo + 2^128 s'_hi.  Also reports whether
-// Y and R decode and whether R encodes the identity.
+// [v s] B and [v s mod l] B differ by elements of E[4].)  [v s mod l] B comes from the
+// fixed-base comb of B (sdig: radix-2^16 digits).  Also reports whether Y and R decode
+// and whether R encodes the identity.
+template <class Comb>
 CPZ_HD bool check_equation(const uint32_t y[8], const uint32_t r[8], const uint32_t udig[4], const uint32_t vdig[4],
-                           bool vneg, const uint32_t sdig[8], const ge_niels* tab_b, const ge_niels* tab_b2,
-                           ge_cached* tab_y, ge_cached* tab_r, bool& decoded, bool& r_identity) {
+                           bool vneg, const uint32_t sdig[8], const Comb& comb, ge_cached* tab_y, ge_cached* tab_r,
+                           bool& decoded, bool& r_identity) {
   {
     ge_p3 P;
     decoded = ristretto_decode(P, y);
@@ -97,15 +98,16 @@ CPZ_HD bool check_equation(const uint32_t y[8], const uint32_t r[8], const uint3
     build_cached_table(tab_r, vneg ? R : ge_neg(R));
   }
   r_identity = words8_zero(r);
-  return ristretto_is_identity(straus_half(tab_y, tab_r, tab_b, tab_b2, udig, vdig, sdig));
+  return ristretto_is_identity(straus_half_comb(tab_y, tab_r, comb, udig, vdig, sdig));
 }
 
 // Full per-proof outcome given the challenge c (canonical) and the response status st_s.
-// tab_g2 / tab_h2: Niels multiples of 2^128 g / 2^128 h; tab_v: 2 * kTableV entries of
-// per-proof scratch.
+// comb_g / comb_h: fixed-base combs of g and h; tab_v: 2 * kTableV entries of per-proof
+// scratch.
+template <class Comb>
 CPZ_HD uint8_t verify_proof(const uint32_t y1[8], const uint32_t y2[8], const uint32_t r1[8], const uint32_t r2[8],
-                            const uint32_t s[8], const uint32_t c[8], uint8_t st_s, const ge_niels* tab_g,
-                            const ge_niels* tab_h, const ge_niels* tab_g2, const ge_niels* tab_h2, ge_cached* tab_v) {
+                            const uint32_t s[8], const uint32_t c[8], uint8_t st_s, const Comb& comb_g,
+                            const Comb& comb_h, ge_cached* tab_v) {
   uint32_t udig[4], vdig[4], sdig[8];
   bool vneg;
   {
@@ -121,11 +123,11 @@ CPZ_HD uint8_t verify_proof(const uint32_t y1[8], const uint32_t y2[8], const ui
     }
     sc sp = sc_mul(vs, ss);
     if (vneg) sp = sc_neg(sp);
-    sc_recode_radix256(sdig, sp.w);
+    sc_recode_radix65536(sdig, sp.w);
   }
   bool dec1, dec2, id1, id2;
-  const bool eq1 = check_equation(y1, r1, udig, vdig, vneg, sdig, tab_g, tab_g2, tab_v, tab_v + kTableV, dec1, id1);
-  const bool eq2 = check_equation(y2, r2, udig, vdig, vneg, sdig, tab_h, tab_h2, tab_v, tab_v + kTableV, dec2, id2);
+  const bool eq1 = check_equation(y1, r1, udig, vdig, vneg, sdig, comb_g, tab_v, tab_v + kTableV, dec1, id1);
+  const bool eq2 = check_equation(y2, r2, udig, vdig, vneg, sdig, comb_h, tab_v, tab_v + kTableV, dec2, id2);
   if (!(dec1 && dec2)) return kStBadPoint;
   if (st_s == kStBadScalar) return kStBadScalar;
   if (id1 || id2 || st_s == kStIdentityOrZero) return kStIdentityOrZero;

@@ -37,11 +37,43 @@ bool build_table(std::vector<ge_niels>& tab, const uint8_t* enc, int shift = 0) 
   return true;
 }
 
-struct GenTables {
-  std::vector<ge_niels> g, h, g2, h2;
-  bool build(const uint8_t* genc, const uint8_t* henc) {
-    return build_table(g, genc) && build_table(h, henc) && build_table(g2, genc, 128) && build_table(h2, henc, 128);
+// Host stand-in for the device comb (CombTable): the same entries, j * 2^(16 k) * B in
+// affine Niels form, computed on demand (the 64 MiB table is not worth building on the
+// CPU for a handful of proofs).  Operation counting is suspended inside lookup, which
+// stands for a memory read on the device.
+struct HostComb {
+  ge_p3 q[kCombWindows];
+  bool build(const uint8_t* enc) {
+    uint32_t w[8];
+    words_from(w, enc);
+    ge_p3 B;
+    if (!ristretto_decode(B, w)) return false;
+    for (int k = 0; k < kCombWindows; k++) {
+      q[k] = B;
+      for (int d = 0; d < 16; d++) B = p1p1_to_p3(p3_dbl(B));
+    }
+    return true;
   }
+  ge_niels lookup(int k, int digit) const {
+    const OpCounts saved = op_counts();
+    const int mag = digit < 0 ? -digit : digit;
+    ge_niels r = ge_niels_identity();
+    if (mag != 0) {
+      ge_p3 acc = q[k];
+      for (int bit = 30 - __builtin_clz((unsigned)mag); bit >= 0; bit--) {
+        acc = p1p1_to_p3(p3_dbl(acc));
+        if ((mag >> bit) & 1) acc = ge_add(acc, q[k]);
+      }
+      r = p3_to_niels(acc);
+    }
+    op_counts() = saved;
+    return ge_niels_cneg(r, digit < 0);
+  }
+};
+
+struct GenTables {
+  HostComb g, h;
+  bool build(const uint8_t* genc, const uint8_t* henc) { return g.build(genc) && h.build(henc); }
 };
 
 }  // namespace
@@ -217,8 +249,7 @@ int cpzt_verify_opcount(unsigned long long* mul, unsigned long long* sq, const u
   ge_cached tv[2 * kTableV];
   unsigned long long m0, s0;
   cpzt_opcount(&m0, &s0);
-  const int st = verify_proof(a, b, cc, d, sw, cw, response_status(sw), gt.g.data(), gt.h.data(), gt.g2.data(),
-                              gt.h2.data(), tv);
+  const int st = verify_proof(a, b, cc, d, sw, cw, response_status(sw), gt.g, gt.h, tv);
   cpzt_opcount(mul, sq);
   return st;
 }
@@ -238,8 +269,7 @@ int cpzt_verify(const uint8_t* g, const uint8_t* h, const uint8_t* y1, const uin
   words_from(sw, s);
   words_from(cw, cb);
   ge_cached tv[2 * kTableV];
-  return verify_proof(a, b, c, d, sw, cw, response_status(sw), gt.g.data(), gt.h.data(), gt.g2.data(), gt.h2.data(),
-                      tv);
+  return verify_proof(a, b, c, d, sw, cw, response_status(sw), gt.g, gt.h, tv);
 }
 
 // Half-size challenge split: u, |v| (16 bytes each, little-endian), sign of v.
