@@ -52,30 +52,33 @@ def _run(cmd):
     return r.stdout
 
 
-def build_libcpz(force: bool = False, verbose: bool = False) -> str:
+def build_libcpz(force: bool = False, verbose: bool = False, out: str = LIBCPZ, defines=()) -> str:
+    """Build the product library.  `out` / `defines` build a tuning variant (e.g.
+    CPZ_VERIFY_WAVES=3) elsewhere, for side-by-side measurement with CPZ_LIB=<out>."""
     units = ["kernels.hip", "rlc.hip", "runtime.hip"]
     srcs = [os.path.join(CSRC, u) for u in units] + _headers()
-    if not force and not _newer(LIBCPZ, srcs):
-        return LIBCPZ
-    os.makedirs(os.path.join(LIBDIR, "obj"), exist_ok=True)
+    if not force and not defines and not _newer(out, srcs):
+        return out
+    objdir = os.path.join(os.path.dirname(out), "obj" if not defines else "obj_" + "_".join(defines).replace("=", ""))
+    os.makedirs(objdir, exist_ok=True)
     hipcc = _hipcc()
     common = [hipcc, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-I", CSRC,
-              "-I", os.path.join(ROOT, "include")]
+              "-I", os.path.join(ROOT, "include")] + ["-D" + d for d in defines]
 
     def compile_one(u):
-        obj = os.path.join(LIBDIR, "obj", u.replace(".hip", ".o"))
-        if force or _newer(obj, [os.path.join(CSRC, u)] + _headers()):
+        obj = os.path.join(objdir, u.replace(".hip", ".o"))
+        if force or defines or _newer(obj, [os.path.join(CSRC, u)] + _headers()):
             _run(common + ["-c", os.path.join(CSRC, u), "-o", obj])
         return obj
 
     with ThreadPoolExecutor(max_workers=len(units)) as ex:
         objs = list(ex.map(compile_one, units))
-    tmp = LIBCPZ + ".tmp"
+    tmp = out + ".tmp"
     _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs)
-    os.replace(tmp, LIBCPZ)
+    os.replace(tmp, out)
     if verbose:
-        print("built", LIBCPZ)
-    return LIBCPZ
+        print("built", out)
+    return out
 
 
 def build_hosttest(force: bool = False) -> str:

@@ -268,7 +268,10 @@ __global__ void __launch_bounds__(256) k_parse_proofs(ParseArgs a) {
 // Per-proof verification
 // ---------------------------------------------------------------------------------------
 
-__global__ void __launch_bounds__(kVerifyBlock, 2) k_verify_each(VerifyArgs a) {
+#ifndef CPZ_VERIFY_WAVES
+#define CPZ_VERIFY_WAVES 2  // waves per SIMD (256 VGPRs each)
+#endif
+__global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each(VerifyArgs a) {
   const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
   const int64_t gtid = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * kVerifyBlock;
@@ -355,6 +358,12 @@ hipError_t launch_build_comb(const uint32_t* gh_words, ge_p3* bases_scratch, ge_
   hipLaunchKernelGGL(k_comb_fill, dim3((unsigned)(2 * kCombPerBase / 256)), dim3(256), 0, st,
                      (const ge_p3*)bases_scratch, comb);
   return hipGetLastError();
+}
+
+int verify_each_blocks_per_cu() {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_verify_each, kVerifyBlock, 0) != hipSuccess || nb < 1) nb = 2;
+  return nb;
 }
 
 hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st) {

@@ -500,6 +500,7 @@ int cpz_ctx_create(int device_ordinal, cpz_ctx** out) {
     return fail(CPZ_EHIP, std::string("context setup: ") + hipGetErrorString(e));
   }
   ctx->cus = prop.multiProcessorCount;
+  ctx->verify_blocks_per_cu = cpz::verify_each_blocks_per_cu();  // the grid-stride verify grid fills the chip once
   *out = ctx;
   return CPZ_OK;
 }
