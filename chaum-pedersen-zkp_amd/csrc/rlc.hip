@@ -5,9 +5,12 @@
 // batch.rs:233-312) with the CORRECT equation (the reference omits alpha on y*c,
 // batch.rs:297-300):
 //   P = sum_i  [a_i s_i] g - [a_i] r1_i - [a_i c_i] y1_i + [b_i s_i] h - [b_i] r2_i - [b_i c_i] y2_i
-// with a_i = wide(ChaCha20(seed, block first+i, stream 0)), b_i = stream 1 (the i-th
-// `random_scalar` of ChaCha20Rng::from_seed(seed), batch.rs:240).  P is the identity iff
-// every weighted proof satisfies both equations (w.o.p.).  Proofs whose decode-level
+// with 128-bit weights in place of random_scalar (batch.rs:240): ChaCha20 block first+i of
+// the seed read as 32 int16 words w_k, a_i = sum_{k<8} w_k 2^(16k), b_i = the same over
+// w_8..w_15 (pyoracle.rlc_weights).  P is the identity iff every weighted proof satisfies
+// both equations, except with probability <= 2^-128 per forged proof.  The r-points'
+// scalars a_i, b_i ARE signed radix-2^16 digit vectors (8 windows, no recoding, windows
+// 8..15 empty): 48 instead of 64 bucket additions per proof.  Proofs whose decode-level
 // status is non-zero carry zero weight and are reported individually.
 //
 // Pipeline (all on one stream):
@@ -36,6 +39,34 @@ __device__ __forceinline__ void rlc_load8(uint32_t w[8], const uint32_t* base, i
   const uint4 a = p[0], b = p[1];
   w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
   w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+
+// The weight sum_{k<8} w_k 2^(16k) (w_k the int16 halves of u[0..3]) reduced mod l: with
+// U the unsigned 128-bit value of u, the signed value is U - 2 (U & 0x8000...8000).
+__device__ __forceinline__ sc rlc_weight(const uint32_t u[4]) {
+  uint32_t d[8];
+  uint32_t borrow = 0, carry = 0;
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    const uint32_t m = k < 4 ? (u[k] & 0x80008000u) : 0u;
+    const uint32_t twice = (m << 1) | carry;  // bits shifted out of the previous word
+    carry = m >> 31;
+    const uint32_t x = k < 4 ? u[k] : 0u;
+    const uint64_t t = (uint64_t)x - twice - borrow;
+    d[k] = (uint32_t)t;
+    borrow = (uint32_t)(t >> 63);
+  }
+#pragma unroll
+  for (int k = 5; k < 8; k++) d[k] = borrow ? 0xffffffffu : 0u;  // sign extension
+  sc r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {  // negative: add l (wraps mod 2^256 to the value in [0, l))
+    const uint64_t t = (uint64_t)d[k] + (borrow ? SC_L(k) : 0u) + c;
+    r.w[k] = (uint32_t)t;
+    c = (uint32_t)(t >> 32);
+  }
+  return r;
 }
 
 // Signed radix-2^16 digits of a scalar < 2^253 (16 windows, digit in [-2^15, 2^15)).
@@ -104,12 +135,10 @@ __global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_prepare(RlcPrepArgs a)
 #pragma unroll
   for (int k = 0; k < 8; k++) { as.w[k] = 0; bs.w[k] = 0; }
   if (i < a.n) {
-    // weights (batch.rs:240 random_scalar, here ChaCha20Rng-keyed by the seed)
+    // weights (replacing random_scalar, batch.rs:240): one ChaCha20 block per proof
     uint32_t blk[16];
     chacha20_block(blk, a.seed, a.first_index + (uint64_t)i, 0);
-    const sc wa = sc_reduce_wide(blk);
-    chacha20_block(blk, a.seed, a.first_index + (uint64_t)i, 1);
-    const sc wb = sc_reduce_wide(blk);
+    const sc wa = rlc_weight(blk), wb = rlc_weight(blk + 4);
     sc c;
     rlc_load8(c.w, a.c, i);
     bool ok = true, ident = false;
@@ -124,10 +153,15 @@ __global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_prepare(RlcPrepArgs a)
       ok = ristretto_decode(P, w) && ok;
       const int64_t j = 4 * i + q;
       store_niels(a.pts + j, niels_from_p3_affine(P, true));
-      sc k = q < 2 ? wa : wb;
-      if (q & 1) k = sc_mul(k, c);
       int16_t d[kRlcWindows];
-      recode16(d, k.w);
+      if (q & 1) {
+        recode16(d, sc_mul(q == 1 ? wa : wb, c).w);
+      } else {
+        const uint32_t* u = q == 0 ? blk : blk + 4;
+#pragma unroll
+        for (int wv = 0; wv < kRlcWindows; wv++)
+          d[wv] = wv < 8 ? (int16_t)(u[wv >> 1] >> (16 * (wv & 1))) : (int16_t)0;
+      }
 #pragma unroll
       for (int wv = 0; wv < kRlcWindows; wv++) a.digits[(int64_t)wv * a.dstride + j] = d[wv];
     }

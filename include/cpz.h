@@ -105,9 +105,11 @@ int cpz_prove_synthetic_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t 
 /* Random-linear-combination batch verification (configs C3-C5): one Pippenger MSM checks
  *   P = sum_i [a_i s_i] g - [a_i] r1_i - [a_i c_i] y1_i + [b_i s_i] h - [b_i] r2_i - [b_i c_i] y2_i == O
  * -- the reference's verify_batch_equations (batch.rs:271-312) with the equation corrected
- * (the reference omits alpha on y*c, batch.rs:297-300).  Weights a_i / b_i are the
- * (first_index + i)-th ChaCha20 keystream blocks of `seed`, stream 0 / 1, reduced wide mod l
- * (random_scalar, batch.rs:240, ristretto.rs:146-150).
+ * (the reference omits alpha on y*c, batch.rs:297-300).  Weights replace random_scalar
+ * (batch.rs:240): the (first_index + i)-th ChaCha20 keystream block of `seed` read as 32
+ * little-endian int16 words w_k; a_i = sum_{k<8} w_k 2^(16k), b_i = sum_{k<8} w_(8+k) 2^(16k)
+ * (mod l) -- 128-bit weights, uniform over 2^128 values each (error <= 2^-128 per forged
+ * entry), whose MSM digits are the words themselves.
  *   partial_out  32-byte encoding of P for this batch / shard (identity = 32 zero bytes);
  *                shards with global first_index values sum to the single-GPU P.
  *   batch_ok     1 iff every entry decodes and P is the identity.

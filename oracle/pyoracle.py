@@ -485,6 +485,19 @@ def batch_weight2(seed: bytes, index: int) -> int:
     return scalar_wide(chacha20_block(seed, index, 1))
 
 
+def rlc_weights(seed: bytes, index: int):
+    """(a_i, b_i) of the corrected RLC batch check: 128-bit weights drawn as signed
+    radix-2^16 digit vectors.  ChaCha20 block `index` (stream 0) read as 32 little-endian
+    int16 words: a_i = sum_k w_k 2^(16k) over words 0..7, b_i over words 8..15 (mod l).
+    Each weight is uniform over a set of 2^128 values (error 2^-128 per forged entry, the
+    standard batch-verification bound), and its MSM digits are the words themselves: 8
+    radix-2^16 windows, no carry -- half the bucket work of a full 253-bit weight."""
+    w = struct.unpack("<32h", chacha20_block(seed, index))
+    a = sum(w[k] << (16 * k) for k in range(8)) % L
+    b = sum(w[8 + k] << (16 * k) for k in range(8)) % L
+    return a, b
+
+
 # ----------------------------------------------------------------------------
 # Protocol: prover (input generator) and per-proof verification
 # ----------------------------------------------------------------------------
@@ -606,7 +619,7 @@ def rlc_partial(recs: Sequence[ProofRecord], seed: bytes, base_index: int = 0,
 
         [a_i s_i] G - [a_i] R1_i - [a_i c_i] Y1_i  +  [b_i s_i] H - [b_i] R2_i - [b_i c_i] Y2_i
 
-    with a_i = batch_weight(seed, base_index+i), b_i = batch_weight2(seed, base_index+i).
+    with (a_i, b_i) = rlc_weights(seed, base_index+i).
     Entries whose decode status is non-zero carry zero weight.  Identity iff every
     weighted entry satisfies both verification equations (w.o.p.).
     """
@@ -620,8 +633,7 @@ def rlc_partial(recs: Sequence[ProofRecord], seed: bytes, base_index: int = 0,
             continue
         y1, y2, r1, r2 = pts
         c = challenge(g_bytes, h_bytes, rec.y1, rec.y2, rec.r1, rec.r2, rec.ctx)
-        a = batch_weight(seed, base_index + j)
-        b = batch_weight2(seed, base_index + j)
+        a, b = rlc_weights(seed, base_index + j)
         sg = (sg + a * s) % L
         sh = (sh + b * s) % L
         acc = pt_add(acc, pt_mul(r1, (L - a) % L))

@@ -209,6 +209,9 @@ def main():
     out["weight_seed"] = wseed.hex()
     out["weights"] = [{"index": i, "alpha": O.scalar_bytes(O.batch_weight(wseed, i)).hex(),
                        "gamma": O.scalar_bytes(O.batch_weight2(wseed, i)).hex()} for i in (0, 1, 2, 63, 1 << 20)]
+    # RLC weights (a_i, b_i) of the corrected batch check (pyoracle.rlc_weights).
+    out["rlc_weights"] = [{"index": i, "a": O.scalar_bytes(O.rlc_weights(wseed, i)[0]).hex(),
+                           "b": O.scalar_bytes(O.rlc_weights(wseed, i)[1]).hex()} for i in (0, 1, 2, 63, 1 << 20)]
 
     # 7. RLC partials (corrected batch equation, the MSM the GPU runs) for fixed seeds:
     #    all-valid batches are the identity; forged / malformed entries make a specific point;
