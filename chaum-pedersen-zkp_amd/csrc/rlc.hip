@@ -503,9 +503,11 @@ __global__ void __launch_bounds__(64) k_rlc_final(RlcMsmArgs a) {
     if (active) {
       lo = lds[w];
       hi = lds[w + span];
+      // 16 span doublings on the projective chain (3M + 4S each), T only at the end
+      ge_p1p1 t = p3_dbl(hi);
 #pragma unroll 1
-      for (int k = 0; k < 16 * span; k++) hi = p1p1_to_p3(p3_dbl(hi));
-      lo = ge_add(lo, hi);
+      for (int k = 1; k < 16 * span; k++) t = p2_dbl(p1p1_to_p2(t));
+      lo = ge_add(lo, p1p1_to_p3(t));
     }
     __syncthreads();
     if (active) lds[w] = lo;
