@@ -16,6 +16,7 @@ constexpr int kRlcSortBlock = 1024;
 constexpr int kRlcSortGroups = 64;      // max blocks per window in the counting sort
 constexpr int64_t kRlcSortChunk = 1 << 16;  // target points per sort block
 constexpr int kNielsEntriesRlc = kTableB;
+constexpr int kRlcChunk = 64;            // sorted entries per bucket-accumulation thread
 
 struct RlcPrepArgs {
   int64_t n;
@@ -48,7 +49,9 @@ struct RlcMsmArgs {
   int64_t chunk;                 // points per sort block
   uint32_t* idx;                 // [16][istride]
   int64_t istride;
-  ge_p3* buckets;                // [16 + 1][2^15] (slot 16: top-window partials)
+  ge_p3* buckets;                // [16][2^15]
+  ge_p3* heads;                  // [16][hstride] partials of buckets begun in an earlier chunk
+  int64_t hstride;               // >= ceil(istride / kRlcChunk)
   ge_p3* seg_s;                  // [16][1024]
   ge_p3* seg_w;                  // [16][1024]
   ge_p3* win;                    // [16]

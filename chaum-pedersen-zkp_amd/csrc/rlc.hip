@@ -22,8 +22,9 @@
 //   k_rlc_bscan     per-bucket prefix over chunks; bucket totals.
 //   k_rlc_scan      exclusive scan -> bucket offsets.
 //   k_rlc_scatter   point ids sorted by bucket (counting sort, LDS cursors).
-//   k_rlc_bucket    1 thread / (window, bucket): mixed additions over its list (the
-//                   top window's fuller buckets split 7 ways, k_rlc_topfold).
+//   k_rlc_bucket    1 thread / (window, 64-entry chunk of the sorted list): mixed
+//                   additions, partials of buckets spanning chunks fixed up by
+//                   k_rlc_bucket_fix (load-balanced whatever the bucket sizes).
 //   k_rlc_segment   1 thread / (window, 32-bucket segment): running sums.
 //   k_rlc_window    1 block / window: sum_b b * B_b from the segments (LDS tree).
 //   k_rlc_final     2^(16w) combine, encode -> 32-byte partial + identity flag.
@@ -317,6 +318,9 @@ __global__ void __launch_bounds__(1024) k_rlc_scan(RlcMsmArgs a) {
   if (threadIdx.x == 1023) off[kRlcBuckets] = run;
 }
 
+// LDS cursors = bucket offset + this block's base; a rank from an LDS atomic.  (A two-level
+// coarse/fine variant, meant to keep every write stream L2-coalesced, measured no faster:
+// the pass is bound by the LDS atomics, one per entry, not by the scattered writes.)
 __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_scatter(RlcMsmArgs a) {
   extern __shared__ uint32_t cur[];  // kRlcBuckets cursors (128 KB)
   const int g = blockIdx.x, w = blockIdx.y;
@@ -340,74 +344,85 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_scatter(RlcMsmArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Bucket accumulation: B[w][b] = sum of (+/-) points in bucket b of window w.
+// Bucket accumulation: B[w][b] = sum of (+/-) points in bucket b of window w, load-balanced.
+// Window w's sorted entries [0, E_w) are cut into chunks of kRlcChunk; thread (w, t) adds
+// exactly the points of chunk t (every lane of a wave does the same number of additions,
+// whatever the bucket sizes -- the top window's 8x fuller buckets included).  A bucket that
+// starts inside chunk t is owned by t, which writes its partial to B[w][b]; the partial of
+// a bucket that started in an earlier chunk goes to heads[w][t], and k_rlc_bucket_fix adds
+// the heads of the chunks a bucket spans (one or two for an average bucket).
 // The running sum is kept as p1p1; its conversion to p3 (4 muls) is issued after the next
 // point's gather, so the gather latency overlaps that work.
 // ---------------------------------------------------------------------------------------
-// Scalars are < 2^253 and, reduced mod l, almost always < 2^252: the top window's digit is
-// at most 2^13 and in practice at most 2^12 + 1, so its ~4097 live buckets hold ~8x the
-// points of a full window's bucket.  Its 32768 thread slots are therefore re-assigned:
-// slot q * 4096 + k (q < 7) takes part q of 7 of bucket k < 4096, and slot 28672 + k
-// takes all of bucket 4096 + k.  The partials land in the spare window slot
-// (buckets[kRlcWindows]) and k_rlc_topfold folds them into window 15's buckets.
-constexpr int kTopBase = 4096;
-constexpr int kTopParts = 7;
-
-__global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (int64_t)kRlcWindows * kRlcBuckets) return;
-  const int w = (int)(t / kRlcBuckets);
-  const int b = (int)(t % kRlcBuckets);
-  const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
-  const uint32_t* idx = a.idx + (int64_t)w * a.istride;
-  uint32_t e0, e1;
-  ge_p3* dst = a.buckets + t;
-  if (w == kRlcWindows - 1) {
-    const int q = b / kTopBase, k = b % kTopBase;
-    if (q < kTopParts) {
-      const uint32_t f0 = off[k], cnt = off[k + 1] - f0;
-      e0 = f0 + (uint32_t)(((uint64_t)cnt * q) / kTopParts);
-      e1 = f0 + (uint32_t)(((uint64_t)cnt * (q + 1)) / kTopParts);
-    } else {
-      e0 = off[kTopBase + k];
-      e1 = off[kTopBase + k + 1];
-    }
-    dst = a.buckets + (int64_t)kRlcWindows * kRlcBuckets + b;
-  } else {
-    e0 = off[b];
-    e1 = off[b + 1];
-  }
+__device__ __forceinline__ ge_p1p1 p1p1_identity_rlc() {
   ge_p1p1 r;  // identity as p1p1: (0 : 1 : 1 : 1)
   r.X = fe_zero();
   r.Y = fe_one();
   r.Z = fe_one();
   r.T = fe_one();
-  uint32_t id = e0 < e1 ? idx[e0] : 0u;
+  return r;
+}
+
+__global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
+  const int w = blockIdx.y;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
+  const uint32_t total = off[kRlcBuckets];
+  const int64_t e0l = t * kRlcChunk;
+  if (e0l >= (int64_t)total) return;
+  const uint32_t e0 = (uint32_t)e0l;
+  const uint32_t e1 = e0 + kRlcChunk < total ? e0 + kRlcChunk : total;
+  const uint32_t* idx = a.idx + (int64_t)w * a.istride;
+  ge_p3* bw = a.buckets + (int64_t)w * kRlcBuckets;
+  ge_p3* heads = a.heads + (int64_t)w * a.hstride;
+  // bucket of entry e0: the last b with off[b] <= e0
+  int lo = 0, hi = kRlcBuckets - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= e0) lo = mid; else hi = mid - 1;
+  }
+  int b = lo;
+  uint32_t bend = off[b + 1];
+  bool head = off[b] < e0;  // bucket b started in an earlier chunk
+  ge_p1p1 r = p1p1_identity_rlc();
+  uint32_t id = idx[e0];
   for (uint32_t e = e0; e < e1; e++) {
     const ge_niels p = load_niels(a.pts + (id & 0x7fffffffu));
     const bool neg = (id >> 31) != 0;
     id = e + 1 < e1 ? idx[e + 1] : 0u;
-    const ge_p3 acc = p1p1_to_p3(r);
+    ge_p3 acc = p1p1_to_p3(r);
+    if (e == bend) {  // bucket b complete: emit it (a store, no extra field work), restart
+      if (head) store_p3(heads + t, acc); else store_p3(bw + b, acc);
+      head = false;
+      acc = ge_identity();
+      do { b++; bend = off[b + 1]; } while (bend <= e);
+    }
     r = ge_add_niels(acc, ge_niels_cneg(p, neg));
   }
-  store_p3(dst, p1p1_to_p3(r));
+  const ge_p3 v = p1p1_to_p3(r);
+  if (head) store_p3(heads + t, v); else store_p3(bw + b, v);
 }
 
-// Window 15's buckets from the split partials (see k_rlc_bucket).
-__global__ void __launch_bounds__(256) k_rlc_topfold(RlcMsmArgs a) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= kRlcBuckets) return;
-  const ge_p3* part = a.buckets + (int64_t)kRlcWindows * kRlcBuckets;
-  ge_p3 v;
-  if (k < kTopBase) {
-    v = load_p3(part + k);
-    for (int q = 1; q < kTopParts; q++) v = ge_add(v, load_p3(part + q * kTopBase + k));
-  } else if (k < 2 * kTopBase) {
-    v = load_p3(part + kTopParts * kTopBase + (k - kTopBase));
-  } else {
-    v = ge_identity();
+// B[w][b] += heads of the chunks after the owner that bucket b spans; empty buckets
+// become the identity.
+__global__ void __launch_bounds__(256) k_rlc_bucket_fix(RlcMsmArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)kRlcWindows * kRlcBuckets) return;
+  const int w = (int)(t / kRlcBuckets);
+  const int b = (int)(t % kRlcBuckets);
+  const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
+  const uint32_t s = off[b], e = off[b + 1];
+  ge_p3* dst = a.buckets + t;
+  if (s == e) {
+    store_p3(dst, ge_identity());
+    return;
   }
-  store_p3(a.buckets + (int64_t)(kRlcWindows - 1) * kRlcBuckets + k, v);
+  const uint32_t c0 = s / kRlcChunk, c1 = (e - 1) / kRlcChunk;
+  if (c1 == c0) return;  // entirely inside its owner's chunk
+  const ge_p3* heads = a.heads + (int64_t)w * a.hstride;
+  ge_p3 v = load_p3(dst);
+  for (uint32_t c = c0 + 1; c <= c1; c++) v = ge_add(v, load_p3(heads + c));
+  store_p3(dst, v);
 }
 
 // One thread per (window, segment of kRlcSegLen buckets):
@@ -601,9 +616,10 @@ hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0,
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_rlc_scatter, dim3(a.groups, kRlcWindows), dim3(kRlcSortBlock), lds, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, a);
+  const int64_t chunks = (a.istride + kRlcChunk - 1) / kRlcChunk;  // per window, upper bound
+  hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((chunks + 255) / 256), kRlcWindows), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rlc_topfold, dim3(kRlcBuckets / 256), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_rlc_bucket_fix, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const int64_t ns = (int64_t)kRlcWindows * (kRlcBuckets / kRlcSegLen);
   hipLaunchKernelGGL(k_rlc_segment, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, st, a);

@@ -47,6 +47,24 @@ def test_msm_adversarial_digits(gpu):
     _check(gpu, [P, P], [O.L - 3, 3])
 
 
+def test_msm_buckets_spanning_chunks(gpu):
+    """Buckets far larger than one accumulation chunk (64 sorted entries per thread): the
+    owner / head partials of every chunk a bucket spans must all be summed."""
+    B = O.BASEPOINT
+    pts, P = [], B
+    for _ in range(300):
+        pts.append(P)                       # (i + 1) B
+        P = O.pt_add(P, B)
+    rnd = random.Random(5)
+    small = [5, 0x00030001, (7 << 240) | (9 << 16) | 2]                # a few distinct digit patterns
+    scal = [small[rnd.randrange(3)] for _ in range(300)]
+    want = O.pt_mul(B, sum((i + 1) * k for i, k in enumerate(scal)) % O.L)
+    assert gpu.msm([O.ristretto_encode(Q) for Q in pts], scal) == O.ristretto_encode(want)
+    # one bucket per window holding all 300 entries (5 chunks), same point repeated
+    assert gpu.msm([O.ristretto_encode(B)] * 300, [0x8000_0003] * 300) == \
+        O.ristretto_encode(O.pt_mul(B, 300 * 0x8000_0003 % O.L))
+
+
 def test_msm_single_weights_from_failing_case(gpu, golden):
     """The single-proof RLC partial (golden forged proof #3) at several first indices."""
     case = golden["rlc"][1]
