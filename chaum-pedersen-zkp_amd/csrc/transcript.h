@@ -21,7 +21,26 @@ namespace cpz {
 constexpr int kStrobeR = 166;
 constexpr uint8_t kFlagI = 1, kFlagA = 2, kFlagC = 4, kFlagM = 16;
 
-CPZ_HD uint64_t rol64(uint64_t v, int n) { return n ? ((v << n) | (v >> (64 - n))) : v; }
+// 64-bit rotation; n is a compile-time constant at every call site after unrolling.  On the
+// device it is two v_alignbit_b32 (funnel shifts of the 32-bit halves) instead of two
+// 64-bit shifts and an OR.
+CPZ_HD uint64_t rol64(uint64_t v, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  if (n & 32) {
+    const uint32_t t = lo;
+    lo = hi;
+    hi = t;
+  }
+  const int r = n & 31;
+  if (r == 0) return ((uint64_t)hi << 32) | lo;
+  const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - r);
+  const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - r);
+  return ((uint64_t)nhi << 32) | nlo;
+#else
+  return n ? ((v << n) | (v >> (64 - n))) : v;
+#endif
+}
 
 CPZ_HD uint64_t KECCAK_RC(int i) {
   const uint64_t rc[24] = {
