@@ -166,8 +166,10 @@ def test_security_corrupted_bytes(gpu):
 
 # ---- at scale: size-independent properties ----------------------------------------------
 def test_scale_synthetic_all_valid_and_forged_exact(gpu, golden):
+    """Config C2 at full size: 2^20 proofs, all valid -> all 0; 1 % seeded forgeries ->
+    exactly that index set with status 1; a sample cross-checked against the oracle."""
     torch = pytest.importorskip("torch")
-    n = 1 << 17
+    n = 1 << 20
     sx, sk = bytes.fromhex(golden["seed_x"]), bytes.fromhex(golden["seed_k"])
     dev = torch.device("cuda:0")
     t = {k: torch.empty((n, 32), dtype=torch.uint8, device=dev) for k in ("y1", "y2", "r1", "r2", "s")}

@@ -127,6 +127,52 @@ def test_rlc_decode_failures_zero_weight(gpu, golden):
     assert list(st) == [p["status"] for p in ps]
 
 
+def _bump_s_rows(t, torch, idx):
+    """s := s + 1 (mod l) for the given rows only (device index_select / index_copy)."""
+    sel = torch.from_numpy(np.asarray(idx, dtype=np.int64)).to("cuda:0")
+    rows = t["s"].index_select(0, sel).cpu().numpy()
+    for r in range(rows.shape[0]):
+        v = (int.from_bytes(rows[r].tobytes(), "little") + 1) % O.L
+        rows[r] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)
+    t["s"].index_copy_(0, sel, torch.from_numpy(rows).to("cuda:0"))
+
+
+def test_c4_64m_sharded_partials(gpu):
+    """Config C4 at full size on one GPU: 2^26 proofs cut into the 8-GPU split (8 shards of
+    2^23), each reduced to a 32-byte partial with weights keyed by GLOBAL index.  All valid:
+    every shard partial and their combination are the identity.  With forged proofs in two
+    shards: exactly those shards' partials are non-identity and the 8 partials combine to
+    the partial of the whole 2^26-proof batch computed as one MSM."""
+    torch = pytest.importorskip("torch")
+    n, shards = 1 << 26, 8
+    per = n // shards
+    seed = hashlib.sha256(b"cpz-weights-v1").digest()
+    t = _synthetic(gpu, torch, n)
+    st = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    keys = ("y1", "y2", "r1", "r2", "s")
+
+    def shard_partials():
+        out = []
+        for k in range(shards):
+            lo, hi = k * per, (k + 1) * per
+            p, ok = gpu.verify_batch_device(*(t[x][lo:hi] for x in keys), st[lo:hi], seed, first_index=lo)
+            out.append((p, ok))
+        return out
+
+    parts = shard_partials()
+    assert all(ok and p == bytes(32) for p, ok in parts)
+    assert gpu.combine_partials([p for p, _ in parts]) == (bytes(32), True)
+    bad = [2 * per + 17, 2 * per + 123_456, 3 * per - 1, 5 * per + 999]
+    _bump_s_rows(t, torch, bad)
+    whole, ok = gpu.verify_batch_device(*(t[x] for x in keys), st, seed)
+    assert not ok and whole != bytes(32)
+    parts = shard_partials()
+    assert [k for k, (p, ok) in enumerate(parts) if not ok] == [2, 5]
+    assert all(p == bytes(32) for k, (p, _) in enumerate(parts) if k not in (2, 5))
+    total, ident = gpu.combine_partials([p for p, _ in parts])
+    assert total == whole and not ident
+
+
 def test_c5_16m_batch_with_0p1pct_forged(gpu):
     """Config C5: a 2^24-proof batch with 16,777 forged entries (0.1 %, seeded indices; half
     s := s + 1, half y1 replaced by another proof's y1).  The RLC check must fail and the
