@@ -14,7 +14,7 @@ constexpr uint8_t kStatusBadScalar = 3;
 constexpr uint8_t kStatusIdentityOrZero = 4;
 
 constexpr int kNielsEntries = kTableB;   // radix-256 signed digits: |d| <= 128
-constexpr int kCachedEntries = 2 * kTableV;   // y and r tables, radix-16 signed digits: |d| <= 8
+constexpr int kCachedEntries = 2 * kTableSlots;   // y and r tables (identity + 1..8): |d| <= 8
 constexpr int kVerifyBlock = 256;
 
 // Merlin/STROBE sponge snapshot.

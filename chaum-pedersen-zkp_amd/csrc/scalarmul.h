@@ -13,6 +13,7 @@
 namespace cpz {
 
 constexpr int kTableV = 8;     // cached multiples 1..8 of a variable base (radix-16 digits)
+constexpr int kTableSlots = kTableV + 1;  // + the identity at slot 0 (digit 0 needs no select)
 constexpr int kTableB = 128;   // Niels multiples 1..128 of a fixed base (radix-256 digits)
 
 // Fixed-base comb: for each of the 16 radix-2^16 windows k, the affine Niels multiples
@@ -72,13 +73,11 @@ CPZ_HD ge_niels niels_lookup(const ge_niels* tab, int digit) {
   return ge_niels_cneg(r, digit < 0);
 }
 
+// tab[0] is the identity, tab[k] = k P: one load and a conditional negation.
 CPZ_HD ge_cached cached_lookup(const ge_cached* tab, int digit) {
   const int mag = digit < 0 ? -digit : digit;
-  const ge_cached e = cached_load(tab + (mag == 0 ? 1 : mag) - 1);
-  const ge_cached r = mag == 0 ? ge_cached_identity() : e;
-  return ge_cached_cneg(r, digit < 0);
+  return ge_cached_cneg(cached_load(tab + mag), digit < 0);
 }
-
 // Four doublings of a pending completed point.
 CPZ_HD ge_p1p1 dbl4(const ge_p1p1& cur) {
   ge_p1p1 t = cur;
@@ -93,8 +92,9 @@ CPZ_HD ge_p1p1 p1p1_identity() {
   return cur;
 }
 
-// Writes the cached multiples 1..8 of an AFFINE P (Z = 1, as decoded): 1 doubling + 6
-// mixed additions of P in Niels form (3M each instead of 4M for a cached addition).
+// Writes the identity and the cached multiples 1..8 of an AFFINE P (Z = 1, as decoded) to
+// tab[0..8]: 1 doubling + 6 mixed additions of P in Niels form (3M each instead of 4M for a
+// cached addition).
 // (An unrolled 4-doubling / 3-addition schedule saves a few more multiplications but keeps
 // three extended points live and measured slower from the extra spills.)
 CPZ_HD void build_cached_table(ge_cached* tab, const ge_p3& P) {
@@ -102,18 +102,19 @@ CPZ_HD void build_cached_table(ge_cached* tab, const ge_p3& P) {
   n1.ypx = fe_add(P.Y, P.X);
   n1.ymx = fe_sub(P.Y, P.X);
   n1.xy2d = fe_mul(P.T, FE_D2());
+  cached_store(tab, ge_cached_identity());
   {
     ge_cached c1;
     c1.YpX = n1.ypx;
     c1.YmX = n1.ymx;
     c1.Z = P.Z;
     c1.T2d = n1.xy2d;
-    cached_store(tab, c1);
+    cached_store(tab + 1, c1);
   }
   ge_p3 acc = p1p1_to_p3(p3_dbl(P));
-  cached_store(tab + 1, p3_to_cached(acc));
+  cached_store(tab + 2, p3_to_cached(acc));
 #pragma unroll 1
-  for (int k = 2; k < kTableV; k++) {
+  for (int k = 3; k <= kTableV; k++) {
     acc = p1p1_to_p3(ge_add_niels(acc, n1));
     cached_store(tab + k, p3_to_cached(acc));
   }

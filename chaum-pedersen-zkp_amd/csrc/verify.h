@@ -102,7 +102,7 @@ CPZ_HD bool check_equation(const uint32_t y[8], const uint32_t r[8], const uint3
 }
 
 // Full per-proof outcome given the challenge c (canonical) and the response status st_s.
-// comb_g / comb_h: fixed-base combs of g and h; tab_v: 2 * kTableV entries of per-proof
+// comb_g / comb_h: fixed-base combs of g and h; tab_v: 2 * kTableSlots entries of per-proof
 // scratch.
 template <class Comb>
 CPZ_HD uint8_t verify_proof(const uint32_t y1[8], const uint32_t y2[8], const uint32_t r1[8], const uint32_t r2[8],
@@ -126,8 +126,8 @@ CPZ_HD uint8_t verify_proof(const uint32_t y1[8], const uint32_t y2[8], const ui
     sc_recode_radix65536(sdig, sp.w);
   }
   bool dec1, dec2, id1, id2;
-  const bool eq1 = check_equation(y1, r1, udig, vdig, vneg, sdig, comb_g, tab_v, tab_v + kTableV, dec1, id1);
-  const bool eq2 = check_equation(y2, r2, udig, vdig, vneg, sdig, comb_h, tab_v, tab_v + kTableV, dec2, id2);
+  const bool eq1 = check_equation(y1, r1, udig, vdig, vneg, sdig, comb_g, tab_v, tab_v + kTableSlots, dec1, id1);
+  const bool eq2 = check_equation(y2, r2, udig, vdig, vneg, sdig, comb_h, tab_v, tab_v + kTableSlots, dec2, id2);
   if (!(dec1 && dec2)) return kStBadPoint;
   if (st_s == kStBadScalar) return kStBadScalar;
   if (id1 || id2 || st_s == kStIdentityOrZero) return kStIdentityOrZero;

@@ -149,7 +149,7 @@ int cpzt_straus(uint8_t* out, uint8_t* out_fixed, const uint8_t* base, const uin
   words_from(w, v);
   ge_p3 V;
   if (!ristretto_decode(V, w)) return 0;
-  ge_cached tv[kTableV];
+  ge_cached tv[kTableSlots];
   build_cached_table(tv, V);
   words_from(sw, s);
   words_from(cw, c);
@@ -246,7 +246,7 @@ int cpzt_verify_opcount(unsigned long long* mul, unsigned long long* sq, const u
   words_from(d, r2);
   words_from(sw, s);
   words_from(cw, c);
-  ge_cached tv[2 * kTableV];
+  ge_cached tv[2 * kTableSlots];
   unsigned long long m0, s0;
   cpzt_opcount(&m0, &s0);
   const int st = verify_proof(a, b, cc, d, sw, cw, response_status(sw), gt.g, gt.h, tv);
@@ -268,7 +268,7 @@ int cpzt_verify(const uint8_t* g, const uint8_t* h, const uint8_t* y1, const uin
   words_from(d, r2);
   words_from(sw, s);
   words_from(cw, cb);
-  ge_cached tv[2 * kTableV];
+  ge_cached tv[2 * kTableSlots];
   return verify_proof(a, b, c, d, sw, cw, response_status(sw), gt.g, gt.h, tv);
 }
 
