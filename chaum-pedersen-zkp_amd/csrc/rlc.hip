@@ -506,29 +506,77 @@ __global__ void __launch_bounds__(256) k_rlc_window(RlcMsmArgs a) {
 }
 
 // Single block: P = sum_w 2^(16 w) T_w (tree), encode.
+// Quad-cooperative doubling for the latency-bound combine below: the four lanes of a quad
+// hold the same projective point; lane q squares [X, Y, Z, X+Y][q] (lane 2 folds the 2 of
+// 2Z^2 into its column sums), the four squares are broadcast inside the quad with DPP
+// quad_perm moves (full-rate VALU, no LDS), and lanes 0-2 do the three products of the
+// p1p1 -> p2 conversion.  One wave then issues 1 S + 1 M per doubling instead of 4 S + 3 M.
+template <int K>
+__device__ __forceinline__ fe fe_quad_bcast(const fe& a) {
+  fe r;
+#pragma unroll
+  for (int i = 0; i < 10; i++) r.v[i] = __builtin_amdgcn_mov_dpp(a.v[i], K * 0x55, 0xf, 0xf, false);
+  return r;
+}
+
+__device__ __forceinline__ ge_p2 p2_dbl_quad(const ge_p2& p, int q) {
+  const fe xpy = fe_add(p.X, p.Y);
+  fe op = fe_select(p.X, p.Y, q == 1);
+  op = fe_select(op, p.Z, q == 2);
+  op = fe_select(op, xpy, q == 3);
+  int64_t h[10];
+  fe_sq_wide(h, op, 1);
+#pragma unroll
+  for (int i = 0; i < 10; i++) h[i] = q == 2 ? 2 * h[i] - carry_bias(i) : h[i];  // 2 Z^2, bias once
+  const fe sq = fe_carry_biased(h);
+  const fe XX = fe_quad_bcast<0>(sq), YY = fe_quad_bcast<1>(sq), ZZ2 = fe_quad_bcast<2>(sq),
+           XpY2 = fe_quad_bcast<3>(sq);
+  const fe Y1 = fe_add(YY, XX), Z1 = fe_sub(YY, XX);
+  const fe X1 = fe_sub(XpY2, Y1), T1 = fe_sub(ZZ2, Z1);
+  // lane 0: X1 T1, lane 1: Y1 Z1, lane 2: Z1 T1 (lane 3 repeats lane 0)
+  fe ma = fe_select(X1, Y1, q == 1);
+  ma = fe_select(ma, Z1, q == 2);
+  const fe mb = fe_select(T1, Z1, q == 1);
+  const fe m = fe_mul(ma, mb);
+  ge_p2 r;
+  r.X = fe_quad_bcast<0>(m);
+  r.Y = fe_quad_bcast<1>(m);
+  r.Z = fe_quad_bcast<2>(m);
+  return r;
+}
+
+// Single block: P = sum_w 2^(16 w) T_w by a tree, encode.  Quad g (lanes 4g..4g+3) owns
+// window g; at level `span` the active quads double their upper partner 16 span times
+// (240 doublings deep in all) with p2_dbl_quad and add it to their own.
 __global__ void __launch_bounds__(64) k_rlc_final(RlcMsmArgs a) {
   __shared__ ge_p3 lds[kRlcWindows];
-  const int w = threadIdx.x;
-  if (w < kRlcWindows) lds[w] = load_p3(a.win + w);
+  const int w = threadIdx.x >> 2, q = threadIdx.x & 3;
+  if (q == 0) lds[w] = load_p3(a.win + w);
   __syncthreads();
-  // level L: pairs (2k, 2k+1) at stride 2^L windows: T = T_2k + 2^(16 * 2^L) T_2k+1
   for (int span = 1; span < kRlcWindows; span <<= 1) {
-    const bool active = (w < kRlcWindows) && (w % (2 * span) == 0);
-    ge_p3 hi = ge_identity(), lo = ge_identity();
+    const bool active = (w % (2 * span)) == 0;
+    ge_p3 lo = ge_identity();
     if (active) {
       lo = lds[w];
-      hi = lds[w + span];
-      // 16 span doublings on the projective chain (3M + 4S each), T only at the end
-      ge_p1p1 t = p3_dbl(hi);
+      const ge_p3 hi = lds[w + span];
+      ge_p2 t;
+      t.X = hi.X;
+      t.Y = hi.Y;
+      t.Z = hi.Z;
 #pragma unroll 1
-      for (int k = 1; k < 16 * span; k++) t = p2_dbl(p1p1_to_p2(t));
-      lo = ge_add(lo, p1p1_to_p3(t));
+      for (int k = 0; k < 16 * span; k++) t = p2_dbl_quad(t, q);
+      ge_p3 d;  // (X : Y : Z) -> extended (XZ : YZ : Z^2 : XY)
+      d.X = fe_mul(t.X, t.Z);
+      d.Y = fe_mul(t.Y, t.Z);
+      d.Z = fe_sq(t.Z);
+      d.T = fe_mul(t.X, t.Y);
+      lo = ge_add(lo, d);
     }
     __syncthreads();
-    if (active) lds[w] = lo;
+    if (active && q == 0) lds[w] = lo;
     __syncthreads();
   }
-  if (w == 0) {
+  if (threadIdx.x == 0) {
     const ge_p3 P = lds[0];
     uint32_t enc[8];
     ristretto_encode(enc, P);
