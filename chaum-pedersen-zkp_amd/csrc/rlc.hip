@@ -480,20 +480,23 @@ __global__ void __launch_bounds__(256) k_rlc_window(RlcMsmArgs a) {
   }
   // X_u = [u >= 1] suf_u  + 4^-1 ... combine: total = sum W + 32 * (4 * sum_{u>=1} suf_u + sum M)
   ge_p3 x = (u >= 1) ? suf : ge_identity();
-  // tree-sum three quantities: x, M, Wsum
-  ge_p3 vals[3] = {x, M, Wsum};
-  ge_p3 tot[3];
-  for (int q = 0; q < 3; q++) {
-    lds[u] = vals[q];
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-      if (u < off) lds[u] = ge_add(lds[u], lds[u + off]);
-      __syncthreads();
+  // tree-sum the three quantities x, M, Wsum side by side (8 levels, not 3 x 8)
+  __shared__ ge_p3 lds_m[256], lds_w[256];
+  __syncthreads();
+  lds[u] = x;
+  lds_m[u] = M;
+  lds_w[u] = Wsum;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (u < off) {
+      lds[u] = ge_add(lds[u], lds[u + off]);
+      lds_m[u] = ge_add(lds_m[u], lds_m[u + off]);
+      lds_w[u] = ge_add(lds_w[u], lds_w[u + off]);
     }
-    tot[q] = lds[0];
     __syncthreads();
   }
   if (u == 0) {
+    const ge_p3 tot[3] = {lds[0], lds_m[0], lds_w[0]};
     ge_p3 r = tot[0];
     r = p1p1_to_p3(p3_dbl(r));
     r = p1p1_to_p3(p3_dbl(r));  // 4 * sum suf
