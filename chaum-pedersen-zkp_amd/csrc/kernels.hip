@@ -128,6 +128,26 @@ __global__ void __launch_bounds__(kChallengeBlock) k_challenge(ChallengeArgs a) 
   }
 }
 
+// No-context fast path (verify.h, challenge_fixed): the sponge in 50 registers, the
+// framing as two constant masks, two permutations, no LDS.  Chosen by the runtime when the
+// prefix snapshot sits at the fixed position.
+__global__ void __launch_bounds__(256) k_challenge_noctx(ChallengeArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  uint32_t y1[8], y2[8], r1[8], r2[8];
+  load_words8(y1, a.y1, i);
+  load_words8(y2, a.y2, i);
+  load_words8(r1, a.r1, i);
+  load_words8(r2, a.r2, i);
+  const sc c = challenge_fixed(reinterpret_cast<const uint32_t*>(a.prefix[1].state), a.k1, a.k2, y1, y2, r1, r2);
+  store_words8(a.c_out, i, c.w);
+  if (a.s != nullptr) {
+    uint32_t w[8];
+    load_words8(w, a.s, i);
+    a.status_out[i] = response_status(w);
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Fixed-base tables: tab[b * 128 + (k - 1)] = k * base_b in affine Niels form.
 // ---------------------------------------------------------------------------------------
@@ -340,8 +360,16 @@ hipError_t launch_transcript_prefix(const uint32_t* gh_words, StrobeSnap* out, h
   return hipGetLastError();
 }
 
+bool challenge_prefix_is_fixed(const StrobeSnap& snap) {
+  return snap.pos == kTailPrefixPos && snap.pos_begin == kTailPrefixBegin && snap.flags == kTailPrefixFlags;
+}
+
 hipError_t launch_challenge(const ChallengeArgs& a, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
+  if (a.ctx_off == nullptr && a.fast_noctx) {
+    hipLaunchKernelGGL(k_challenge_noctx, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
   const int64_t blocks = (a.n + kChallengeBlock - 1) / kChallengeBlock;
   hipLaunchKernelGGL(k_challenge, dim3((unsigned)blocks), dim3(kChallengeBlock), 0, st, a);
   return hipGetLastError();

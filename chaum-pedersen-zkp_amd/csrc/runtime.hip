@@ -17,6 +17,7 @@
 #include "../../include/cpz.h"
 #include "cpz_kernels.h"
 #include "rlc.h"
+#include "verify.h"
 
 namespace {
 
@@ -81,6 +82,8 @@ struct cpz_ctx {
   DevBuf comb;      // fixed-base combs of g and h: 2 x 16 x 2^15 ge_niels (128 MiB)
   DevBuf comb_q;    // 32 ge_p3: 2^(16 k) g, 2^(16 k) h
   DevBuf prefix;    // 2 StrobeSnap
+  bool prefix_fixed = false;  // prefix[1] at the fixed position: k_challenge_noctx applies
+  uint32_t chal_k1[50], chal_k2[50];  // its framing masks
   DevBuf gh_words;  // 16 words
   DevBuf ok_flags;  // 2 ints
   // work buffers
@@ -160,8 +163,12 @@ int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32]) {
   CPZ_HIP(cpz::launch_transcript_prefix(static_cast<const uint32_t*>(ctx->gh_words.p),
                                         static_cast<cpz::StrobeSnap*>(ctx->prefix.p), ctx->stream));
   int ok[2] = {0, 0};
+  cpz::StrobeSnap snap1;
   CPZ_HIP(hipMemcpyAsync(ok, ctx->ok_flags.p, sizeof(ok), hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipMemcpyAsync(&snap1, static_cast<cpz::StrobeSnap*>(ctx->prefix.p) + 1, sizeof(snap1),
+                         hipMemcpyDeviceToHost, ctx->stream));
   CPZ_HIP(hipStreamSynchronize(ctx->stream));
+  ctx->prefix_fixed = cpz::challenge_prefix_is_fixed(snap1) && cpz::challenge_masks(ctx->chal_k1, ctx->chal_k2);
   if (!ok[0] || !ok[1]) {
     ctx->have_gh = false;
     return fail(CPZ_EGENERATOR, "generator encoding does not decode to a ristretto255 point");
@@ -194,6 +201,9 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   const int grid = verify_grid(ctx, n);
   CPZ_HIP(ctx->scratch.ensure((size_t)grid * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached)));
   cpz::ChallengeArgs ca;
+  ca.fast_noctx = ctx->prefix_fixed ? 1 : 0;
+  std::memcpy(ca.k1, ctx->chal_k1, sizeof(ca.k1));
+  std::memcpy(ca.k2, ctx->chal_k2, sizeof(ca.k2));
   ca.n = (int64_t)n;
   words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
   ca.y1 = static_cast<const uint32_t*>(y1);
@@ -341,6 +351,9 @@ int rlc_prepare(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const vo
   if (rc) return rc;
   CPZ_HIP(ctx->c.ensure(n * 32));
   cpz::ChallengeArgs ca;
+  ca.fast_noctx = ctx->prefix_fixed ? 1 : 0;
+  std::memcpy(ca.k1, ctx->chal_k1, sizeof(ca.k1));
+  std::memcpy(ca.k2, ctx->chal_k2, sizeof(ca.k2));
   ca.n = (int64_t)n;
   words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
   ca.y1 = static_cast<const uint32_t*>(y1);
@@ -738,6 +751,9 @@ int cpz_challenges(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_
   if (rc) return rc;
   CPZ_HIP(ctx->c.ensure(n * 32));
   cpz::ChallengeArgs ca;
+  ca.fast_noctx = ctx->prefix_fixed ? 1 : 0;
+  std::memcpy(ca.k1, ctx->chal_k1, sizeof(ca.k1));
+  std::memcpy(ca.k2, ctx->chal_k2, sizeof(ca.k2));
   ca.n = (int64_t)n;
   words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
   ca.y1 = static_cast<const uint32_t*>(dev[0]);
@@ -850,6 +866,9 @@ int cpz_prove_synthetic_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t 
   pa.s_out = static_cast<uint32_t*>(d_s);
   CPZ_HIP(cpz::launch_prove_points(pa, st));
   cpz::ChallengeArgs ca;
+  ca.fast_noctx = ctx->prefix_fixed ? 1 : 0;
+  std::memcpy(ca.k1, ctx->chal_k1, sizeof(ca.k1));
+  std::memcpy(ca.k2, ctx->chal_k2, sizeof(ca.k2));
   ca.n = (int64_t)n;
   words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
   ca.y1 = pa.y1;

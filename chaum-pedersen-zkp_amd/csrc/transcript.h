@@ -112,6 +112,7 @@ struct Strobe {
     if (pos == kStrobeR) run_f();
   }
   CPZ_HDM void absorb(const uint8_t* data, int n) {
+#pragma unroll
     for (int i = 0; i < n; i++) absorb_byte(data[i]);
   }
   CPZ_HDM void absorb_u32le(uint32_t v) {
@@ -121,6 +122,7 @@ struct Strobe {
     absorb_byte((uint8_t)(v >> 24));
   }
   CPZ_HDM void absorb_words(const uint32_t* w, int nwords) {
+#pragma unroll
     for (int i = 0; i < nwords; i++) absorb_u32le(w[i]);
   }
   CPZ_HDM uint8_t squeeze_byte() {
@@ -155,6 +157,7 @@ struct Strobe {
     absorb((const uint8_t*)label, label_len);
     absorb_u32le((uint32_t)n);
     begin_op(kFlagI | kFlagA | kFlagC);
+#pragma unroll
     for (int i = 0; i < n; i++) out[i] = squeeze_byte();
   }
 };
@@ -176,6 +179,20 @@ struct ArrayState {
     for (int i = 0; i < 25; i++)
       for (int k = 0; k < 8; k++) b[8 * i + k] = (uint8_t)(a[i] >> (8 * k));
   }
+};
+
+// Records, per sponge segment (between permutations), the bytes XORed into the state:
+// run over the transcript tail with all-zero messages it yields the constant framing masks
+// of the fixed-schedule challenge (verify.h, challenge_fixed).
+struct MaskState {
+  uint8_t m[3][200];
+  int seg = 0;
+  CPZ_HDM uint8_t get(int) const { return 0; }
+  CPZ_HDM void put(int, uint8_t) {}
+  CPZ_HDM void xor_(int i, uint8_t v) {
+    if (seg < 3) m[seg][i] ^= v;
+  }
+  CPZ_HDM void permute() { seg++; }
 };
 
 // Fresh STROBE-128 state for protocol label "Merlin v1.0" (state, pos, pos_begin, flags).

@@ -52,6 +52,86 @@ CPZ_HD sc transcript_challenge(Strobe<Acc>& s, const uint32_t y1[8], const uint3
   return sc_reduce_wide(wide);
 }
 
+// Fixed-schedule transcript tail for entries WITHOUT a context.  Transcript::new +
+// append_parameters always leave the sponge at byte 32 (begin 0, flags A): every message
+// length is fixed, so the tail's schedule is fixed too -- y1, y2, r1 land at bytes 42, 84,
+// 126 of the first segment, the r2 header crosses the rate (166) and forces the first
+// permutation, r2 lands at byte 2 of the second segment, the challenge header's C flag
+// forces the second permutation, and the 64 challenge bytes are state bytes 0..63.  All
+// other bytes the framing XORs in are constants: k1 / k2 (50 words each, from
+// challenge_masks).  The state is then 50 registers and no byte is touched individually.
+constexpr int kTailPrefixPos = 32, kTailPrefixBegin = 0, kTailPrefixFlags = kFlagA;
+constexpr int kTailY1 = 42, kTailY2 = 84, kTailR1 = 126, kTailR2 = 2;
+
+template <int OFF>
+CPZ_HD void xor_message(uint32_t st[50], const uint32_t w[8]) {
+  static_assert(OFF % 2 == 0, "messages start on 16-bit boundaries in this schedule");
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (OFF % 4 == 0) {
+      st[OFF / 4 + k] ^= w[k];
+    } else {
+      st[OFF / 4 + k] ^= w[k] << 16;
+      st[OFF / 4 + k + 1] ^= w[k] >> 16;
+    }
+  }
+}
+
+CPZ_HD void keccak_words(uint32_t st[50]) {
+  uint64_t a[25];
+#pragma unroll
+  for (int l = 0; l < 25; l++) a[l] = (uint64_t)st[2 * l] | ((uint64_t)st[2 * l + 1] << 32);
+  keccak_f1600(a);
+#pragma unroll
+  for (int l = 0; l < 25; l++) {
+    st[2 * l] = (uint32_t)a[l];
+    st[2 * l + 1] = (uint32_t)(a[l] >> 32);
+  }
+}
+
+CPZ_HD sc challenge_fixed(const uint32_t prefix[50], const uint32_t k1[50], const uint32_t k2[50],
+                          const uint32_t y1[8], const uint32_t y2[8], const uint32_t r1[8], const uint32_t r2[8]) {
+  uint32_t st[50];
+#pragma unroll
+  for (int w = 0; w < 50; w++) st[w] = prefix[w] ^ k1[w];
+  xor_message<kTailY1>(st, y1);
+  xor_message<kTailY2>(st, y2);
+  xor_message<kTailR1>(st, r1);
+  keccak_words(st);
+#pragma unroll
+  for (int w = 0; w < 50; w++) st[w] ^= k2[w];
+  xor_message<kTailR2>(st, r2);
+  keccak_words(st);
+  return sc_reduce_wide(st);  // challenge bytes 0..63 = state words 0..15
+}
+
+template <class Acc>
+CPZ_HD sc transcript_challenge(Strobe<Acc>& s, const uint32_t y1[8], const uint32_t y2[8], const uint32_t r1[8],
+                               const uint32_t r2[8]);
+
+// The constant masks of challenge_fixed, derived by running the generic tail over zero
+// messages with a recording accessor; false if the schedule is not the expected one (two
+// permutations), in which case callers must use the generic path.
+CPZ_HD bool challenge_masks(uint32_t k1[50], uint32_t k2[50]) {
+  MaskState ms;
+  for (int g = 0; g < 3; g++)
+    for (int i = 0; i < 200; i++) ms.m[g][i] = 0;
+  Strobe<MaskState> s(ms, kTailPrefixPos, kTailPrefixBegin, (uint8_t)kTailPrefixFlags);
+  const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  (void)transcript_challenge(s, z, z, z, z);
+  if (ms.seg != 2) return false;
+  for (int w = 0; w < 50; w++) {
+    uint32_t a = 0, b = 0;
+    for (int k = 3; k >= 0; k--) {
+      a = (a << 8) | ms.m[0][4 * w + k];
+      b = (b << 8) | ms.m[1][4 * w + k];
+    }
+    k1[w] = a;
+    k2[w] = b;
+  }
+  return true;
+}
+
 // Transcript::new() (transcript.rs:29-33) on a fresh sponge.
 template <class Acc>
 CPZ_HD Strobe<Acc> transcript_new(Acc& st) {

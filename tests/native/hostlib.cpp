@@ -272,6 +272,29 @@ int cpzt_verify(const uint8_t* g, const uint8_t* h, const uint8_t* y1, const uin
   return verify_proof(a, b, c, d, sw, cw, response_status(sw), gt.g, gt.h, tv);
 }
 
+// The fixed-schedule no-context challenge (k_challenge_noctx's arithmetic) from the prefix
+// state of (g, h); returns -1 if the prefix is not at the fixed position or the masks fail.
+int cpzt_challenge_fixed(uint8_t* out, const uint8_t* g, const uint8_t* h, const uint8_t* y1, const uint8_t* y2,
+                         const uint8_t* r1, const uint8_t* r2) {
+  ArrayState st;
+  Strobe<ArrayState> s = transcript_new(st);
+  uint32_t gw[8], hw[8];
+  words_from(gw, g);
+  words_from(hw, h);
+  transcript_parameters(s, gw, hw);
+  if (s.pos != kTailPrefixPos || s.pos_begin != kTailPrefixBegin || s.cur_flags != kTailPrefixFlags) return -1;
+  uint32_t k1[50], k2[50], pre[50];
+  if (!challenge_masks(k1, k2)) return -1;
+  std::memcpy(pre, st.b, 200);
+  uint32_t a[8], b[8], c[8], d[8];
+  words_from(a, y1);
+  words_from(b, y2);
+  words_from(c, r1);
+  words_from(d, r2);
+  bytes_from(out, challenge_fixed(pre, k1, k2, a, b, c, d).w);
+  return 0;
+}
+
 // Half-size challenge split: u, |v| (16 bytes each, little-endian), sign of v.
 void cpzt_half_split(uint8_t* u_out, uint8_t* v_out, int* vneg, const uint8_t* c) {
   uint32_t cw[8], u[4], v[4];

@@ -204,3 +204,27 @@ def test_half_split(lib):
         assert (uu, vv) == _euclid_half(c), c
         assert vv != 0 and (vv * c - uu) % L == 0
         assert uu < 3 << 125 and abs(vv) < 3 << 125
+
+
+def test_challenge_fixed_schedule(lib, golden):
+    """The no-context fast path (two permutations over a register sponge with constant
+    framing masks, k_challenge_noctx) equals the generic byte-wise STROBE tail."""
+    import os
+    g, h = bytes.fromhex(golden["g"]), bytes.fromhex(golden["h"])
+    rnd = __import__("random").Random(11)
+    for t in range(40):
+        y1, y2, r1, r2 = (bytes(rnd.randrange(256) for _ in range(32)) for _ in range(4))
+        if t == 0:
+            y1 = y2 = r1 = r2 = bytes(32)
+        want = ctypes.create_string_buffer(32)
+        lib.cpzt_challenge(want, g, h, y1, y2, r1, r2, None, 0, 0)
+        got = ctypes.create_string_buffer(32)
+        assert lib.cpzt_challenge_fixed(got, g, h, y1, y2, r1, r2) == 0
+        assert got.raw == want.raw, t
+    # custom generators reach the same fixed position
+    p = [q for q in golden["proofs"] if q["kind"] == "valid"][0]
+    want = ctypes.create_string_buffer(32)
+    got = ctypes.create_string_buffer(32)
+    lib.cpzt_challenge(want, h, g, *(bytes.fromhex(p[k]) for k in ("y1", "y2", "r1", "r2")), None, 0, 0)
+    assert lib.cpzt_challenge_fixed(got, h, g, *(bytes.fromhex(p[k]) for k in ("y1", "y2", "r1", "r2"))) == 0
+    assert got.raw == want.raw
