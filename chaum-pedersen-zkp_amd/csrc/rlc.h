@@ -48,6 +48,7 @@ struct RlcMsmArgs {
   int groups;                    // sort blocks per window
   int64_t chunk;                 // points per sort block
   uint32_t* idx;                 // [16][istride]
+  uint64_t* inter;               // [16][istride] coarse-sorted (fine bucket << 32 | id) entries
   int64_t istride;
   ge_p3* buckets;                // [16][2^15]
   ge_p3* heads;                  // [16][hstride] partials of buckets begun in an earlier chunk

@@ -21,7 +21,8 @@
 //   k_rlc_hist      per-(chunk, window) bucket histograms (LDS, 32768 buckets).
 //   k_rlc_bscan     per-bucket prefix over chunks; bucket totals.
 //   k_rlc_scan      exclusive scan -> bucket offsets.
-//   k_rlc_scatter   point ids sorted by bucket (counting sort, LDS cursors).
+//   k_rlc_coarse /  point ids sorted by bucket in two LDS-staged passes (256 coarse bins,
+//   k_rlc_fine      then 128 buckets per bin) so that every global write is a contiguous run.
 //   k_rlc_bucket    1 thread / (window, 64-entry chunk of the sorted list): mixed
 //                   additions, partials of buckets spanning chunks fixed up by
 //                   k_rlc_bucket_fix (load-balanced whatever the bucket sizes).
@@ -318,29 +319,123 @@ __global__ void __launch_bounds__(1024) k_rlc_scan(RlcMsmArgs a) {
   if (threadIdx.x == 1023) off[kRlcBuckets] = run;
 }
 
-// LDS cursors = bucket offset + this block's base; a rank from an LDS atomic.  (A two-level
-// coarse/fine variant, meant to keep every write stream L2-coalesced, measured no faster:
-// the pass is bound by the LDS atomics, one per entry, not by the scattered writes.)
-__global__ void __launch_bounds__(kRlcSortBlock) k_rlc_scatter(RlcMsmArgs a) {
-  extern __shared__ uint32_t cur[];  // kRlcBuckets cursors (128 KB)
+// Scatter of the point ids into bucket order, in two LDS-staged passes so that every
+// global write is part of a contiguous run.  (A direct scatter -- one 4-byte write per
+// entry to a random position of a 16 MB window array -- costs a whole HBM burst per entry:
+// measured 0.94 ms per 2^20 proofs, against 0.21 ms for the same kernel writing
+// sequentially.)
+//   k_rlc_coarse  block (chunk g, window w), tiles of 8192 points: an LDS counting sort of
+//                 the tile by coarse bin (256 bins of 128 buckets), then each bin's run is
+//                 appended to the bin's region of `inter` (runs of ~32 entries).
+//   k_rlc_fine    block (coarse bin c, window w): the region's entries (~16 K for a full
+//                 window) are ranked by bucket with LDS cursors into an LDS image of the
+//                 region, which is then copied to idx contiguously.  A region too large for
+//                 LDS (the top window's concentrated bins) is scattered directly instead;
+//                 it spans < 1 MB, so its writes still merge in L2.
+// A coarse bin's region of `inter` is the same range of positions its buckets occupy in
+// idx, so both passes share the offsets from k_rlc_scan.
+constexpr int kRlcCoarse = 256;
+constexpr int kRlcFinePerCoarse = kRlcBuckets / kRlcCoarse;  // 128
+constexpr int kRlcTile = 8192;
+constexpr int kRlcFineCap = 36 * 1024;  // entries staged in LDS by k_rlc_fine (144 KB)
+
+__global__ void __launch_bounds__(kRlcSortBlock) k_rlc_coarse(RlcMsmArgs a) {
+  __shared__ uint64_t buf[kRlcTile];
+  __shared__ uint32_t gbase[kRlcCoarse], cnt[kRlcCoarse], start[kRlcCoarse];
+  __shared__ uint32_t part[kRlcSortBlock];
   const int g = blockIdx.x, w = blockIdx.y;
+  const int tid = threadIdx.x;
   const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
   const uint32_t* base = a.bhist + ((int64_t)w * a.groups + g) * kRlcBuckets;
-  for (int b = threadIdx.x; b < kRlcBuckets; b += kRlcSortBlock) cur[b] = off[b] + base[b];
+  {  // this block's start in each coarse bin: off[first bucket] + its bucket bases
+    constexpr int per = kRlcBuckets / kRlcSortBlock;  // 32 buckets per thread, 4 threads per bin
+    uint32_t sum = 0;
+    for (int k = 0; k < per; k++) sum += base[tid * per + k];
+    part[tid] = sum;
+  }
+  __syncthreads();
+  if (tid < kRlcCoarse) {
+    constexpr int tpb = kRlcSortBlock / kRlcCoarse;
+    uint32_t sum = off[tid * kRlcFinePerCoarse];
+    for (int k = 0; k < tpb; k++) sum += part[tid * tpb + k];
+    gbase[tid] = sum;
+    cnt[tid] = 0;
+  }
   __syncthreads();
   const int64_t total = (a.p1 - a.p0) + 2;
-  const int64_t t0 = (int64_t)g * a.chunk;
-  const int64_t t1 = t0 + a.chunk < total ? t0 + a.chunk : total;
+  const int64_t c0 = (int64_t)g * a.chunk;
+  const int64_t c1 = c0 + a.chunk < total ? c0 + a.chunk : total;
   const int16_t* dig = a.digits + (int64_t)w * a.dstride;
-  uint32_t* idx = a.idx + (int64_t)w * a.istride;
-  for (int64_t t = t0 + threadIdx.x; t < t1; t += kRlcSortBlock) {
-    const int64_t j = msm_point(a, t);
-    const int d = dig[j];
-    if (d != 0) {
-      const uint32_t pos = atomicAdd(&cur[(d < 0 ? -d : d) - 1], 1u);
-      idx[pos] = (uint32_t)j | (d < 0 ? 0x80000000u : 0u);
+  uint64_t* inter = a.inter + (int64_t)w * a.istride;
+  constexpr int per_thread = kRlcTile / kRlcSortBlock;  // 8
+  for (int64_t t0 = c0; t0 < c1; t0 += kRlcTile) {
+    uint64_t ent[per_thread];
+    uint32_t rank[per_thread];
+#pragma unroll
+    for (int k = 0; k < per_thread; k++) {
+      const int64_t t = t0 + tid + (int64_t)k * kRlcSortBlock;
+      ent[k] = ~0ull;
+      if (t < c1) {
+        const int64_t j = msm_point(a, t);
+        const int d = dig[j];
+        if (d != 0) {
+          const uint32_t b = (uint32_t)((d < 0 ? -d : d) - 1);
+          const uint32_t c = b / kRlcFinePerCoarse;
+          ent[k] = ((uint64_t)c << 40) | ((uint64_t)(b % kRlcFinePerCoarse) << 32) | (uint32_t)j |
+                   (d < 0 ? 0x80000000u : 0u);
+          rank[k] = atomicAdd(&cnt[c], 1u);
+        }
+      }
     }
+    __syncthreads();
+    if (tid == 0) {  // exclusive scan of the 256 bin counts (tiny)
+      uint32_t run = 0;
+      for (int c = 0; c < kRlcCoarse; c++) {
+        start[c] = run;
+        run += cnt[c];
+      }
+      part[0] = run;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < per_thread; k++)
+      if (ent[k] != ~0ull) buf[start[ent[k] >> 40] + rank[k]] = ent[k];
+    __syncthreads();
+    const uint32_t nt = part[0];
+    for (uint32_t e = tid; e < nt; e += kRlcSortBlock) {
+      const uint64_t v = buf[e];
+      const uint32_t c = (uint32_t)(v >> 40);
+      inter[gbase[c] + (e - start[c])] = v & 0xffffffffffull;
+    }
+    __syncthreads();
+    if (tid < kRlcCoarse) {
+      gbase[tid] += cnt[tid];
+      cnt[tid] = 0;
+    }
+    __syncthreads();
   }
+}
+
+__global__ void __launch_bounds__(kRlcSortBlock) k_rlc_fine(RlcMsmArgs a) {
+  __shared__ uint32_t img[kRlcFineCap];
+  __shared__ uint32_t cur[kRlcFinePerCoarse];
+  const int c = blockIdx.x, w = blockIdx.y;
+  const int tid = threadIdx.x;
+  const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1) + c * kRlcFinePerCoarse;
+  const uint32_t r0 = off[0], r1 = off[kRlcFinePerCoarse];
+  const bool staged = r1 - r0 <= (uint32_t)kRlcFineCap;
+  if (tid < kRlcFinePerCoarse) cur[tid] = off[tid] - (staged ? r0 : 0u);
+  __syncthreads();
+  const uint64_t* inter = a.inter + (int64_t)w * a.istride;
+  uint32_t* idx = a.idx + (int64_t)w * a.istride;
+  for (uint32_t e = r0 + tid; e < r1; e += kRlcSortBlock) {
+    const uint64_t v = inter[e];
+    const uint32_t pos = atomicAdd(&cur[(uint32_t)(v >> 32)], 1u);
+    if (staged) img[pos] = (uint32_t)v; else idx[pos] = (uint32_t)v;
+  }
+  if (!staged) return;
+  __syncthreads();
+  for (uint32_t e = tid; e < r1 - r0; e += kRlcSortBlock) idx[r0 + e] = img[e];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -653,9 +748,6 @@ hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0,
     if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rlc_hist),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
       return e;
-    if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rlc_scatter),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
-      return e;
     attr_set = true;
   }
   const int64_t nb = (int64_t)kRlcWindows * kRlcBuckets;
@@ -665,7 +757,9 @@ hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0,
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_rlc_scan, dim3(kRlcWindows), dim3(1024), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rlc_scatter, dim3(a.groups, kRlcWindows), dim3(kRlcSortBlock), lds, st, a);
+  hipLaunchKernelGGL(k_rlc_coarse, dim3(a.groups, kRlcWindows), dim3(kRlcSortBlock), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rlc_fine, dim3(kRlcCoarse, kRlcWindows), dim3(kRlcSortBlock), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const int64_t chunks = (a.istride + kRlcChunk - 1) / kRlcChunk;  // per window, upper bound
   hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((chunks + 255) / 256), kRlcWindows), dim3(256), 0, st, a);

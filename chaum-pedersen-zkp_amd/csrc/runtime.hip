@@ -96,7 +96,7 @@ struct cpz_ctx {
   // wire-format ingestion
   DevBuf pz_blob, pz_off, pz_rows, pz_code, pz_aux;
   // RLC / Pippenger buffers (sized for the largest batch seen)
-  DevBuf rl_pts, rl_dig, rl_bsum, rl_counts, rl_offsets, rl_bhist, rl_idx, rl_buckets, rl_heads, rl_segs,
+  DevBuf rl_pts, rl_dig, rl_bsum, rl_counts, rl_offsets, rl_bhist, rl_idx, rl_inter, rl_buckets, rl_heads, rl_segs,
       rl_segw, rl_win,
       rl_partial, rl_flags, rl_parts;
   int64_t rl_cap = 0;  // proofs
@@ -287,6 +287,7 @@ int rlc_reserve(cpz_ctx* ctx, int64_t n) {
   CPZ_HIP(ctx->rl_offsets.ensure(sizeof(uint32_t) * cpz::kRlcWindows * (cpz::kRlcBuckets + 1)));
   CPZ_HIP(ctx->rl_bhist.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcSortGroups * cpz::kRlcBuckets));
   CPZ_HIP(ctx->rl_idx.ensure((size_t)npts * cpz::kRlcWindows * sizeof(uint32_t)));
+  CPZ_HIP(ctx->rl_inter.ensure((size_t)npts * cpz::kRlcWindows * sizeof(uint64_t)));
   CPZ_HIP(ctx->rl_buckets.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * cpz::kRlcBuckets));
   CPZ_HIP(ctx->rl_heads.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * (size_t)((npts + cpz::kRlcChunk - 1) / cpz::kRlcChunk)));
   const size_t nseg = (size_t)cpz::kRlcWindows * (cpz::kRlcBuckets / cpz::kRlcSegLen);
@@ -312,6 +313,7 @@ cpz::RlcMsmArgs rlc_msm_args(cpz_ctx* ctx, int64_t lo, int64_t hi) {
   m.bhist = static_cast<uint32_t*>(ctx->rl_bhist.p);
   cpz::rlc_sort_geometry(m, (m.p1 - m.p0) + 2);
   m.idx = static_cast<uint32_t*>(ctx->rl_idx.p);
+  m.inter = static_cast<uint64_t*>(ctx->rl_inter.p);
   m.istride = 4 * ctx->rl_cap + 2;
   m.buckets = static_cast<cpz::ge_p3*>(ctx->rl_buckets.p);
   m.heads = static_cast<cpz::ge_p3*>(ctx->rl_heads.p);
@@ -678,7 +680,7 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->ctxp.release();
   for (DevBuf* b : {&ctx->pz_blob, &ctx->pz_off, &ctx->pz_rows, &ctx->pz_code, &ctx->pz_aux}) b->release();
   for (DevBuf* b : {&ctx->rl_pts, &ctx->rl_dig, &ctx->rl_bsum, &ctx->rl_counts, &ctx->rl_offsets, &ctx->rl_bhist,
-                    &ctx->rl_idx, &ctx->rl_buckets, &ctx->rl_heads, &ctx->rl_segs, &ctx->rl_segw, &ctx->rl_win, &ctx->rl_partial,
+                    &ctx->rl_idx, &ctx->rl_inter, &ctx->rl_buckets, &ctx->rl_heads, &ctx->rl_segs, &ctx->rl_segw, &ctx->rl_win, &ctx->rl_partial,
                     &ctx->rl_flags, &ctx->rl_parts})
     b->release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
