@@ -10,7 +10,7 @@ namespace cpz {
 
 constexpr int kRlcWindows = 16;          // 16-bit signed windows cover scalars < 2^255
 constexpr int kRlcBuckets = 1 << 15;     // |digit| in [1, 2^15]
-constexpr int kRlcSegLen = 32;           // buckets per reduction segment
+constexpr int kRlcSegLen = 16;           // buckets per reduction segment
 constexpr int kRlcPrepBlock = 256;       // proofs per prepare block (= block_sums granule)
 constexpr int kRlcSortBlock = 1024;
 constexpr int kRlcSortGroups = 64;      // max blocks per window in the counting sort
@@ -53,8 +53,8 @@ struct RlcMsmArgs {
   ge_p3* buckets;                // [16][2^15]
   ge_p3* heads;                  // [16][hstride] partials of buckets begun in an earlier chunk
   int64_t hstride;               // >= ceil(istride / kRlcChunk)
-  ge_p3* seg_s;                  // [16][1024]
-  ge_p3* seg_w;                  // [16][1024]
+  ge_p3* seg_s;                  // [16][2^15 / kRlcSegLen]
+  ge_p3* seg_w;                  // [16][2^15 / kRlcSegLen]
   ge_p3* win;                    // [16]
   uint32_t* partial_out;         // 8 words
   int* identity_out;             // 1

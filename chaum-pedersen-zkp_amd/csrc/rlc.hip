@@ -538,27 +538,29 @@ __global__ void __launch_bounds__(256) k_rlc_segment(RlcMsmArgs a) {
   store_p3(a.seg_w + t, acc);
 }
 
-// One block (256 threads) per window.  Segment t covers bucket values 32t+1..32t+32:
-//   T_w = sum_t W_t + 32 * sum_t t S_t.
-// Thread u owns segments 4u..4u+3: A_u = sum_j S_{4u+j}, M_u = sum_j j S_{4u+j},
-//   sum_t t S_t = 4 sum_u u A_u + sum_u M_u,   sum_u u A_u = sum_{k>=1} suffix_k(A).
+// One block (256 threads) per window.  Segment t covers bucket values L t + 1 .. L t + L
+// (L = kRlcSegLen):  T_w = sum_t W_t + L * sum_t t S_t.  Thread u owns the P = nseg / 256
+// segments P u .. P u + P - 1:  A_u = sum_j S_{Pu+j},  M_u = sum_j j S_{Pu+j},
+//   sum_t t S_t = P sum_u u A_u + sum_u M_u,   sum_u u A_u = sum_{k>=1} suffix_k(A).
 __global__ void __launch_bounds__(256) k_rlc_window(RlcMsmArgs a) {
   __shared__ ge_p3 lds[256];
   const int w = blockIdx.x;
   const int u = threadIdx.x;
   constexpr int nseg = kRlcBuckets / kRlcSegLen;
-  static_assert(nseg == 4 * 256, "window kernel assumes 1024 segments");
+  constexpr int P = nseg / 256;
+  static_assert(P * 256 == nseg && (P & (P - 1)) == 0 && (kRlcSegLen & (kRlcSegLen - 1)) == 0,
+                "window kernel assumes power-of-two segment counts");
   const ge_p3* S = a.seg_s + (int64_t)w * nseg;
   const ge_p3* Wt = a.seg_w + (int64_t)w * nseg;
   ge_p3 A = ge_identity(), M = ge_identity(), Wsum = ge_identity();
   {
     ge_p3 run = ge_identity();
-    for (int j = 3; j >= 1; j--) {   // M = sum_j j S_j = sum_{j>=1} suffix_j
-      run = ge_add(run, load_p3(S + 4 * u + j));
+    for (int j = P - 1; j >= 1; j--) {   // M = sum_j j S_j = sum_{j>=1} suffix_j
+      run = ge_add(run, load_p3(S + P * u + j));
       M = ge_add(M, run);
     }
-    A = ge_add(run, load_p3(S + 4 * u));
-    for (int j = 0; j < 4; j++) Wsum = ge_add(Wsum, load_p3(Wt + 4 * u + j));
+    A = ge_add(run, load_p3(S + P * u));
+    for (int j = 0; j < P; j++) Wsum = ge_add(Wsum, load_p3(Wt + P * u + j));
   }
   // suffix scan of A over u (inclusive): suf_u = sum_{v >= u} A_v
   lds[u] = A;
@@ -573,7 +575,7 @@ __global__ void __launch_bounds__(256) k_rlc_window(RlcMsmArgs a) {
     lds[u] = suf;
     __syncthreads();
   }
-  // X_u = [u >= 1] suf_u  + 4^-1 ... combine: total = sum W + 32 * (4 * sum_{u>=1} suf_u + sum M)
+  // total = sum W + L * (P * sum_{u>=1} suf_u + sum M)
   ge_p3 x = (u >= 1) ? suf : ge_identity();
   // tree-sum the three quantities x, M, Wsum side by side (8 levels, not 3 x 8)
   __shared__ ge_p3 lds_m[256], lds_w[256];
@@ -591,14 +593,13 @@ __global__ void __launch_bounds__(256) k_rlc_window(RlcMsmArgs a) {
     __syncthreads();
   }
   if (u == 0) {
-    const ge_p3 tot[3] = {lds[0], lds_m[0], lds_w[0]};
-    ge_p3 r = tot[0];
-    r = p1p1_to_p3(p3_dbl(r));
-    r = p1p1_to_p3(p3_dbl(r));  // 4 * sum suf
-    r = ge_add(r, tot[1]);
+    ge_p3 r = lds[0];
 #pragma unroll 1
-    for (int k = 0; k < 5; k++) r = p1p1_to_p3(p3_dbl(r));  // * 32
-    r = ge_add(r, tot[2]);
+    for (int k = 1; k < P; k <<= 1) r = p1p1_to_p3(p3_dbl(r));  // * P
+    r = ge_add(r, lds_m[0]);
+#pragma unroll 1
+    for (int k = 1; k < kRlcSegLen; k <<= 1) r = p1p1_to_p3(p3_dbl(r));  // * L
+    r = ge_add(r, lds_w[0]);
     store_p3(a.win + w, r);
   }
 }
