@@ -214,7 +214,8 @@ CPZ_HD fe fe_mul(const fe& f, const fe& g) {
   return r;
 }
 
-// Column sums of f^2 (using f_i f_j = f_j f_i: 55 products), each started at bias_k / div.
+// Column sums of f^2 (using f_i f_j = f_j f_i: 55 products), each started at bias_k / div
+// (div == 0: unbiased, for fe_carry_floor).
 CPZ_HD void fe_sq_wide(int64_t h[10], const fe& f, int div) {
   CPZ_COUNT(sq);
   fe_check_operand(f);
@@ -234,7 +235,7 @@ CPZ_HD void fe_sq_wide(int64_t h[10], const fe& f, int div) {
       const int m2 = (i != j ? 2 : 1) * (((i & 1) && (j & 1)) ? 2 : 1);
       const int32_t a = (m2 == 1) ? f.v[i] : (m2 == 2 ? f2[i] : (int32_t)(2u * (uint32_t)f2[i]));
       const int32_t b = (i + j >= 10) ? f19[j] : f.v[j];
-      h[k] = acc_pin((int64_t)a * (int64_t)b + (first[k] ? carry_bias(k) / div : h[k]));
+      h[k] = acc_pin((int64_t)a * (int64_t)b + (first[k] ? (div ? carry_bias(k) / div : 0) : h[k]));
       first[k] = false;
     }
   }
@@ -261,11 +262,36 @@ CPZ_HD fe fe_sq2(const fe& f) {
   return r;
 }
 
-// Repeated squaring (n >= 1).
+// Unbiased columns -> limbs by floor carries: limb k in [0, 2^w_k) (limb 1 a few units
+// above), one v_and_b32 per limb instead of the centred residue's and + subtract.  The
+// limbs are twice as large as centred ones, which only a chain of squarings tolerates:
+// there every operand is such an output, so 19 * limb < 2^30.3 and 4 * odd limb < 2^27.1
+// fit the signed 32-bit multiplicands, and the worst column stays below 2^61.
+CPZ_HD fe fe_carry_floor(int64_t H[10]) {
+  fe r;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    H[k + 1] += H[k] >> ((k & 1) ? 25 : 26);
+    r.v[k] = (int32_t)((uint32_t)H[k] & ((k & 1) ? 0x1ffffffu : 0x3ffffffu));
+  }
+  const int64_t h0 = (int64_t)r.v[0] + 19 * (H[9] >> 25);
+  r.v[9] = (int32_t)((uint32_t)H[9] & 0x1ffffffu);
+  r.v[1] += (int32_t)(h0 >> 26);
+  r.v[0] = (int32_t)((uint32_t)h0 & 0x3ffffffu);
+  return r;
+}
+
+// Repeated squaring (n >= 1): the intermediate squares use floor carries (above), the
+// last one the centred carry, so the result is an ordinary tight element.
 CPZ_HD fe fe_sqn(fe f, int n) {
 #pragma unroll 1
-  for (int i = 0; i < n; i++) f = fe_sq(f);
-  return f;
+  for (int i = 1; i < n; i++) {
+    int64_t h[10];
+    fe_sq_wide(h, f, 0);
+    f = fe_carry_floor(h);
+    CPZ_SEQ();
+  }
+  return fe_sq(f);
 }
 
 // Reduce to the unique canonical representative and write 32 little-endian bytes.

@@ -207,3 +207,32 @@ def test_cpp_batch_verifier_mirror():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "all passed" in r.stdout
+
+
+def test_long_contexts_and_ragged_batch(gpu):
+    """Transcript contexts of every length class (the Merlin/STROBE sponge rate is 166 bytes,
+    so these cross zero, one and several permutations inside append_context) and a batch
+    size that is not a multiple of any launch width; the challenge is checked byte for byte
+    against the oracle (transcript.rs:29-71) and the verdict against verify_one."""
+    lens = [0, 1, 31, 64, 100, 120, 121, 122, 140, 165, 166, 167, 200, 331, 332, 1000]
+    rng = np.random.default_rng(77)
+    recs = [_prove_oracle(40 + i, rng.integers(0, 256, n, dtype=np.uint8).tobytes()) for i, n in enumerate(lens)]
+    ctxs = [r.ctx for r in recs]
+    args = _rec_args(recs)
+    c = gpu.challenges(*args[:4], contexts=ctxs)
+    for r, row in zip(recs, c):
+        exp = O.challenge(O.G_BYTES, O.H_BYTES, r.y1, r.y2, r.r1, r.r2, r.ctx)
+        assert int.from_bytes(bytes(row), "little") == exp, len(r.ctx)
+    # 300 entries = the 16 above repeated, every third with a context shifted by one byte
+    n = 300
+    idx = [i % len(recs) for i in range(n)]
+    rows = [np.ascontiguousarray(a[idx]) for a in args]
+    ctx_n = [ctxs[j] if i % 3 else ctxs[j][1:] + b"\x00" for i, j in enumerate(idx)]
+    st = gpu.verify_each(*rows, contexts=ctx_n)
+    exp = [0 if i % 3 else 1 for i in range(n)]
+    assert st.tolist() == exp
+    seed = bytes(range(32))
+    _, ok, st_b = gpu.verify_batch(*rows, seed=seed, contexts=ctx_n)
+    assert not ok and list(st_b) == exp
+    _, ok, st_b = gpu.verify_batch(*[r[1::3] for r in rows], seed=seed, contexts=ctx_n[1::3])
+    assert ok and not st_b.any()
