@@ -128,7 +128,7 @@ def time_verify(rows, seconds: float = 12.0, threads: int = 1, batch: int = 1000
     except OSError:
         pass
 
-    def run(mode, budget):
+    def run(mode, budget, threads=threads):
         done = [0] * threads
         stop = time.perf_counter() + budget
 
@@ -160,7 +160,9 @@ def time_verify(rows, seconds: float = 12.0, threads: int = 1, batch: int = 1000
         return sum(done) / el, sum(done), el
 
     b_rate, b_n, b_t = run("batch", seconds * 0.6)
-    o_rate, o_n, o_t = run("one", seconds * 0.4)
+    o_rate, o_n, o_t = run("one", seconds * 0.3)
+    # the reference itself is single-threaded: the same batch loop on one core
+    s_rate, s_n, _ = run("batch", seconds * 0.1, threads=1) if threads > 1 else (b_rate, b_n, b_t)
     return {
         "value": b_rate, "unit": "proofs/s", "cores": threads, "kind": "port",
         "sample": "%d proofs: the first %d of the same synthetic set (verified until the time budget ran out, "
@@ -170,6 +172,8 @@ def time_verify(rows, seconds: float = 12.0, threads: int = 1, batch: int = 1000
         "seconds": b_t,
         "verify_one_value": o_rate,
         "verify_one_sample": "%d proofs, per-proof verify_one loop (batch.rs:185-231) incl. decode" % o_n,
+        "single_thread_value": s_rate,
+        "single_thread_sample": "%d proofs, the BatchVerifier::verify loop above on 1 thread" % s_n,
         "cpu_model": cpu_model,
         "implementation": "oracle/cpz_oracle.c (C restatement of dalek's u64 backend + merlin; gcc -O3)",
     }
