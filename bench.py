@@ -63,6 +63,9 @@ def main():
                     help="each: per-proof verification (configs[1], the headline); rlc: random-linear-"
                          "combination batch check via Pippenger MSM (configs[2]/[3]: per-rank partials, "
                          "all-gather of 32-B partials, combine)")
+    ap.add_argument("--ctx-len", type=int, default=0,
+                    help="per-proof transcript context of this many random bytes (0: none, the configs' default; "
+                         "32: the reference service's challenge ids, service.rs:294-295)")
     ap.add_argument("--rlc-extra", type=int, default=1,
                     help="at N=1 in 'each' mode also time the RLC batch path on the same proofs (reported "
                          "under 'rlc', not in value)")
@@ -88,21 +91,28 @@ def main():
     t = {k: torch.empty((n, 32), dtype=torch.uint8, device=dev) for k in ("y1", "y2", "r1", "r2", "s")}
     status = torch.empty(n, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    cx = {}
+    if args.ctx_len:
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(1000 + rank)
+        cx["ctx_bytes"] = torch.randint(0, 256, (n * args.ctx_len,), dtype=torch.int32, device=dev,
+                                        generator=gen).to(torch.uint8)
+        cx["ctx_off"] = torch.arange(n + 1, dtype=torch.int64, device=dev) * args.ctx_len
     gpu.prove_synthetic_device(n, SEED_X, SEED_K, t["y1"], t["y2"], t["r1"], t["r2"], t["s"],
-                               first_index=rank * n, stream=stream)
+                               first_index=rank * n, stream=stream, **cx)
     torch.cuda.synchronize(dev)
 
     weight_seed = hashlib.sha256(b"cpz-weights-v1").digest()
     from chaum_pedersen.shard import all_gather_partials
 
     def step_each():
-        gpu.verify_each_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status, stream=stream)
+        gpu.verify_each_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status, stream=stream, **cx)
 
     rlc_state = {"ok": True}
 
     def step_rlc():
         partial, ok = gpu.verify_batch_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status, weight_seed,
-                                              first_index=rank * n, stream=stream)
+                                              first_index=rank * n, stream=stream, **cx)
         if world > 1:
             parts = all_gather_partials(partial)
             total, ident = gpu.combine_partials(parts)
@@ -209,7 +219,9 @@ def main():
             "dtype": "int32/int64 limbs (GF(2^255-19), radix 2^25.5)",
             "data": "synthetic (GPU prover, ChaCha20-derived witnesses; all proofs valid, checked)",
             "config": {"workload": "configs[1]: 2^20 proofs per GPU, per-proof verification (challenge + 2 equations)",
-                       "proofs_per_gpu": n, "contexts": "none", "generators": "default (g, h)",
+                       "proofs_per_gpu": n,
+                       "contexts": ("%d random bytes per proof" % args.ctx_len) if args.ctx_len else "none",
+                       "generators": "default (g, h)",
                        "parallelism": "dp%d (independent shards, no collective)" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,

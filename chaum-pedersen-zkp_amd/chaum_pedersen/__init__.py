@@ -353,15 +353,17 @@ class Gpu:
 
     def verify_batch_device(self, y1, y2, r1, r2, s, status_out, seed: bytes, first_index: int = 0,
                             fallback: bool = False, params: Optional[Parameters] = None,
-                            stream: Optional[int] = None):
-        """Device-resident RLC batch check; returns (partial, batch_ok); fills status_out."""
+                            stream: Optional[int] = None, ctx_bytes=None, ctx_off=None, ctx_present=None):
+        """Device-resident RLC batch check; returns (partial, batch_ok); fills status_out.
+        Contexts, if any, are device tensors: bytes (uint8), n + 1 offsets (int64), n flags."""
         params = params or Parameters()
         partial = ctypes.create_string_buffer(32)
         ok = ctypes.c_int(0)
+        dp = lambda t: None if t is None else t.data_ptr()
         _native.check(self._lib.cpz_verify_batch_device(
             self._h, params.g, params.h, int(y1.shape[0]), y1.data_ptr(), y2.data_ptr(), r1.data_ptr(),
-            r2.data_ptr(), s.data_ptr(), None, None, None, bytes(seed), first_index, partial, ctypes.byref(ok),
-            status_out.data_ptr(), 1 if fallback else 0, _torch_stream(stream)))
+            r2.data_ptr(), s.data_ptr(), dp(ctx_bytes), dp(ctx_off), dp(ctx_present), bytes(seed), first_index,
+            partial, ctypes.byref(ok), status_out.data_ptr(), 1 if fallback else 0, _torch_stream(stream)))
         return partial.raw, bool(ok.value)
 
     def parse_proofs(self, blobs: Sequence[bytes]):
@@ -428,11 +430,14 @@ class Gpu:
             dp(ctx_present), dp(status_out), _torch_stream(stream)))
 
     def prove_synthetic_device(self, n: int, seed_x: bytes, seed_k: bytes, y1, y2, r1, r2, s, first_index: int = 0,
-                               params: Optional[Parameters] = None, stream: Optional[int] = None) -> None:
+                               params: Optional[Parameters] = None, stream: Optional[int] = None,
+                               ctx_bytes=None, ctx_off=None, ctx_present=None) -> None:
         params = params or Parameters()
+        dp = lambda t: None if t is None else t.data_ptr()
         _native.check(self._lib.cpz_prove_synthetic_device(
-            self._h, params.g, params.h, n, first_index, bytes(seed_x), bytes(seed_k), None, None, None,
-            y1.data_ptr(), y2.data_ptr(), r1.data_ptr(), r2.data_ptr(), s.data_ptr(), _torch_stream(stream)))
+            self._h, params.g, params.h, n, first_index, bytes(seed_x), bytes(seed_k), dp(ctx_bytes), dp(ctx_off),
+            dp(ctx_present), y1.data_ptr(), y2.data_ptr(), r1.data_ptr(), r2.data_ptr(), s.data_ptr(),
+            _torch_stream(stream)))
 
 
 _default_gpu: Optional[Gpu] = None

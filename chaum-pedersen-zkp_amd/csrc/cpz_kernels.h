@@ -43,6 +43,8 @@ struct ChallengeArgs {
   int fast_noctx = 0;            // prefix[1] at the fixed position: k_challenge_noctx with k1 / k2
   uint32_t k1[50];               // framing masks of the fixed-schedule tail (challenge_masks)
   uint32_t k2[50];
+  int fast_ctx32 = 0;            // prefix[0] at the fixed position: 32-byte contexts take
+  uint32_t c32[3][50];           // challenge_fixed_ctx32 with these masks (challenge_masks_ctx32)
 };
 
 // Proof::from_bytes outcome codes (gadgets.rs:364-489); kept equal to CPZ_PARSE_* in cpz.h.
@@ -95,6 +97,7 @@ struct ProveArgs {
 hipError_t launch_transcript_prefix(const uint32_t* gh_words, StrobeSnap* out, hipStream_t st);
 hipError_t launch_challenge(const ChallengeArgs& a, hipStream_t st);
 bool challenge_prefix_is_fixed(const StrobeSnap& snap);  // the no-context fast path applies
+bool challenge_prefix_is_ctx32(const StrobeSnap& snap);  // prefix[0]: the 32-byte-context fast path applies
 hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, hipStream_t st);
 hipError_t launch_parse_proofs(const ParseArgs& a, hipStream_t st);
 // Fixed-base combs of 2 bases (g, h): bases_scratch holds 2 * kCombWindows ge_p3.

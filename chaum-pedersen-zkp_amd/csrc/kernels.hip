@@ -3,8 +3,11 @@
 //   k_transcript_prefix  one thread: Merlin state after Transcript::new() (S0) and after
 //                        append_parameters(g, h) (S1)          transcript.rs:29-50
 //   k_challenge          1 thread / proof: Fiat-Shamir challenge c (bit-exact merlin),
-//                        response-scalar checks (from_canonical_bytes, zero)
+//                        response-scalar checks (from_canonical_bytes, zero); entries
+//                        without a context or with a 32-byte one on fixed schedules in
+//                        registers, any other context length on an LDS sponge image
 //                        batch.rs:188-206, gadgets.rs:466-482
+//   k_challenge_noctx    the same for batches without contexts (registers only)
 //   k_build_niels        (k * B) for k = 1..128, B in {g, h, 2^128 g, 2^128 h}: affine
 //                        Niels tables
 //   k_verify_each        1 thread / proof: challenge split v c = u (mod l) with
@@ -12,8 +15,8 @@
 //                        [v s] B - [u] y - [v] r in E[4]  <=>  [s] B - [c] y == r
 //                        by a half-length Straus loop: radix-16 signed digits of u and |v|
 //                        against per-proof tables of 8 multiples of -y and -+r (HBM-backed
-//                        scratch), radix-256 digits of v s against the shared LDS tables
-//                        of B and 2^128 B.
+//                        scratch), then [v s mod l] B as 16 mixed additions from the
+//                        fixed-base comb of B in HBM (radix-2^16 digits).
 //                        batch.rs:185-231, verifier/mod.rs:144-171
 //   k_parse_proofs       bulk Proof::from_bytes (gadgets.rs:364-489) into SoA rows + codes
 //   k_prove_points /     synthetic-input generator: Prover::prove_with_transcript
@@ -96,12 +99,12 @@ __global__ void k_transcript_prefix(const uint32_t* __restrict__ gh_words, Strob
 
 constexpr int kChallengeBlock = 128;
 
-__global__ void __launch_bounds__(kChallengeBlock) k_challenge(ChallengeArgs a) {
-  __shared__ uint32_t lds[50 * kChallengeBlock];
-  const int64_t i = (int64_t)blockIdx.x * kChallengeBlock + threadIdx.x;
-  if (i >= a.n) return;
+// Generic transcript tail: the byte-wise STROBE code on this thread's dword-interleaved
+// image of the sponge in LDS (any context length).
+__device__ __forceinline__ sc challenge_generic(const ChallengeArgs& a, uint32_t* lds, bool has_ctx, uint64_t b0,
+                                                uint64_t b1, const uint32_t y1[8], const uint32_t y2[8],
+                                                const uint32_t r1[8], const uint32_t r2[8]) {
   LdsState st{lds, (int)threadIdx.x, kChallengeBlock};
-  const bool has_ctx = a.ctx_off != nullptr && (a.ctx_present == nullptr || a.ctx_present[i] != 0);
   const StrobeSnap& snap = a.prefix[has_ctx ? 0 : 1];
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(snap.state);
@@ -110,16 +113,40 @@ __global__ void __launch_bounds__(kChallengeBlock) k_challenge(ChallengeArgs a) 
   }
   Strobe<LdsState> s(st, snap.pos, snap.pos_begin, (uint8_t)snap.flags);
   if (has_ctx) {
-    const uint64_t b0 = a.ctx_off[i], b1 = a.ctx_off[i + 1];
     transcript_context(s, a.ctx_bytes + b0, (uint32_t)(b1 - b0));
     transcript_parameters(s, a.gh_words, a.gh_words + 8);
   }
+  return transcript_challenge(s, y1, y2, r1, r2);
+}
+
+__global__ void __launch_bounds__(kChallengeBlock) k_challenge(ChallengeArgs a) {
+  __shared__ uint32_t lds[50 * kChallengeBlock];
+  const int64_t i = (int64_t)blockIdx.x * kChallengeBlock + threadIdx.x;
+  if (i >= a.n) return;
+  const bool has_ctx = a.ctx_off != nullptr && (a.ctx_present == nullptr || a.ctx_present[i] != 0);
   uint32_t y1[8], y2[8], r1[8], r2[8];
   load_words8(y1, a.y1, i);
   load_words8(y2, a.y2, i);
   load_words8(r1, a.r1, i);
   load_words8(r2, a.r2, i);
-  const sc c = transcript_challenge(s, y1, y2, r1, r2);
+  const uint64_t b0 = has_ctx ? a.ctx_off[i] : 0, b1 = has_ctx ? a.ctx_off[i + 1] : 0;
+  // Entries on a fixed schedule skip the LDS sponge: no context (k_challenge_noctx's tail)
+  // or a 4-byte-aligned 32-byte context (the service's challenge ids).
+  const bool fixed_noctx = !has_ctx && a.fast_noctx;
+  const bool fixed_ctx32 = has_ctx && a.fast_ctx32 && b1 - b0 == 32 && (b0 & 3) == 0;
+  sc c;
+  if (fixed_noctx) {
+    c = challenge_fixed(reinterpret_cast<const uint32_t*>(a.prefix[1].state), a.k1, a.k2, y1, y2, r1, r2);
+  } else if (fixed_ctx32) {
+    uint32_t cw[8];
+    const uint4* cp = reinterpret_cast<const uint4*>(a.ctx_bytes + b0);
+    const uint4 lo = cp[0], hi = cp[1];
+    cw[0] = lo.x; cw[1] = lo.y; cw[2] = lo.z; cw[3] = lo.w;
+    cw[4] = hi.x; cw[5] = hi.y; cw[6] = hi.z; cw[7] = hi.w;
+    c = challenge_fixed_ctx32(reinterpret_cast<const uint32_t*>(a.prefix[0].state), a.c32, cw, y1, y2, r1, r2);
+  } else {
+    c = challenge_generic(a, lds, has_ctx, b0, b1, y1, y2, r1, r2);
+  }
   store_words8(a.c_out, i, c.w);
   if (a.s != nullptr) {
     uint32_t w[8];
@@ -127,7 +154,6 @@ __global__ void __launch_bounds__(kChallengeBlock) k_challenge(ChallengeArgs a) 
     a.status_out[i] = response_status(w);
   }
 }
-
 // No-context fast path (verify.h, challenge_fixed): the sponge in 50 registers, the
 // framing as two constant masks, two permutations, no LDS.  Chosen by the runtime when the
 // prefix snapshot sits at the fixed position.
@@ -362,6 +388,10 @@ hipError_t launch_transcript_prefix(const uint32_t* gh_words, StrobeSnap* out, h
 
 bool challenge_prefix_is_fixed(const StrobeSnap& snap) {
   return snap.pos == kTailPrefixPos && snap.pos_begin == kTailPrefixBegin && snap.flags == kTailPrefixFlags;
+}
+
+bool challenge_prefix_is_ctx32(const StrobeSnap& snap) {
+  return snap.pos == kC32PrefixPos && snap.pos_begin == kC32PrefixBegin && snap.flags == kC32PrefixFlags;
 }
 
 hipError_t launch_challenge(const ChallengeArgs& a, hipStream_t st) {

@@ -84,6 +84,8 @@ struct cpz_ctx {
   DevBuf prefix;    // 2 StrobeSnap
   bool prefix_fixed = false;  // prefix[1] at the fixed position: k_challenge_noctx applies
   uint32_t chal_k1[50], chal_k2[50];  // its framing masks
+  bool ctx32_fixed = false;   // prefix[0] at the fixed position: 32-byte contexts' fast path
+  uint32_t chal_c32[3][50];   // its framing masks (g and h folded in)
   DevBuf gh_words;  // 16 words
   DevBuf ok_flags;  // 2 ints
   // work buffers
@@ -142,6 +144,11 @@ struct StageTimer {
 };
 
 // Build (or reuse) the fixed-base tables and transcript prefix for (g, h).
+void words_from_bytes(uint32_t w[16], const uint8_t g[32], const uint8_t h[32]) {
+  std::memcpy(w, g, 32);
+  std::memcpy(w + 8, h, 32);
+}
+
 int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32]) {
   if (ctx->have_gh && std::memcmp(ctx->gh, g, 32) == 0 && std::memcmp(ctx->gh + 32, h, 32) == 0) return CPZ_OK;
   // Parameters::with_generators (gadgets.rs:77-103): valid, non-identity, distinct.
@@ -163,12 +170,16 @@ int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32]) {
   CPZ_HIP(cpz::launch_transcript_prefix(static_cast<const uint32_t*>(ctx->gh_words.p),
                                         static_cast<cpz::StrobeSnap*>(ctx->prefix.p), ctx->stream));
   int ok[2] = {0, 0};
-  cpz::StrobeSnap snap1;
+  cpz::StrobeSnap snap[2];
   CPZ_HIP(hipMemcpyAsync(ok, ctx->ok_flags.p, sizeof(ok), hipMemcpyDeviceToHost, ctx->stream));
-  CPZ_HIP(hipMemcpyAsync(&snap1, static_cast<cpz::StrobeSnap*>(ctx->prefix.p) + 1, sizeof(snap1),
-                         hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipMemcpyAsync(snap, ctx->prefix.p, sizeof(snap), hipMemcpyDeviceToHost, ctx->stream));
   CPZ_HIP(hipStreamSynchronize(ctx->stream));
-  ctx->prefix_fixed = cpz::challenge_prefix_is_fixed(snap1) && cpz::challenge_masks(ctx->chal_k1, ctx->chal_k2);
+  ctx->prefix_fixed = cpz::challenge_prefix_is_fixed(snap[1]) && cpz::challenge_masks(ctx->chal_k1, ctx->chal_k2);
+  {
+    uint32_t gw[16];
+    words_from_bytes(gw, g, h);
+    ctx->ctx32_fixed = cpz::challenge_prefix_is_ctx32(snap[0]) && cpz::challenge_masks_ctx32(ctx->chal_c32, gw, gw + 8);
+  }
   if (!ok[0] || !ok[1]) {
     ctx->have_gh = false;
     return fail(CPZ_EGENERATOR, "generator encoding does not decode to a ristretto255 point");
@@ -183,9 +194,13 @@ int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32]) {
   return CPZ_OK;
 }
 
-void words_from_bytes(uint32_t w[16], const uint8_t g[32], const uint8_t h[32]) {
-  std::memcpy(w, g, 32);
-  std::memcpy(w + 8, h, 32);
+// The fixed-schedule challenge paths and their masks (set per (g, h) by ensure_generators).
+void set_challenge_schedules(const cpz_ctx* ctx, cpz::ChallengeArgs& ca) {
+  ca.fast_noctx = ctx->prefix_fixed ? 1 : 0;
+  std::memcpy(ca.k1, ctx->chal_k1, sizeof(ca.k1));
+  std::memcpy(ca.k2, ctx->chal_k2, sizeof(ca.k2));
+  ca.fast_ctx32 = ctx->ctx32_fixed ? 1 : 0;
+  std::memcpy(ca.c32, ctx->chal_c32, sizeof(ca.c32));
 }
 
 int verify_grid(cpz_ctx* ctx, size_t n) {
@@ -201,9 +216,7 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   const int grid = verify_grid(ctx, n);
   CPZ_HIP(ctx->scratch.ensure((size_t)grid * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached)));
   cpz::ChallengeArgs ca;
-  ca.fast_noctx = ctx->prefix_fixed ? 1 : 0;
-  std::memcpy(ca.k1, ctx->chal_k1, sizeof(ca.k1));
-  std::memcpy(ca.k2, ctx->chal_k2, sizeof(ca.k2));
+  set_challenge_schedules(ctx, ca);
   ca.n = (int64_t)n;
   words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
   ca.y1 = static_cast<const uint32_t*>(y1);
@@ -353,9 +366,7 @@ int rlc_prepare(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const vo
   if (rc) return rc;
   CPZ_HIP(ctx->c.ensure(n * 32));
   cpz::ChallengeArgs ca;
-  ca.fast_noctx = ctx->prefix_fixed ? 1 : 0;
-  std::memcpy(ca.k1, ctx->chal_k1, sizeof(ca.k1));
-  std::memcpy(ca.k2, ctx->chal_k2, sizeof(ca.k2));
+  set_challenge_schedules(ctx, ca);
   ca.n = (int64_t)n;
   words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
   ca.y1 = static_cast<const uint32_t*>(y1);
@@ -753,9 +764,7 @@ int cpz_challenges(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_
   if (rc) return rc;
   CPZ_HIP(ctx->c.ensure(n * 32));
   cpz::ChallengeArgs ca;
-  ca.fast_noctx = ctx->prefix_fixed ? 1 : 0;
-  std::memcpy(ca.k1, ctx->chal_k1, sizeof(ca.k1));
-  std::memcpy(ca.k2, ctx->chal_k2, sizeof(ca.k2));
+  set_challenge_schedules(ctx, ca);
   ca.n = (int64_t)n;
   words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
   ca.y1 = static_cast<const uint32_t*>(dev[0]);
@@ -868,9 +877,7 @@ int cpz_prove_synthetic_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t 
   pa.s_out = static_cast<uint32_t*>(d_s);
   CPZ_HIP(cpz::launch_prove_points(pa, st));
   cpz::ChallengeArgs ca;
-  ca.fast_noctx = ctx->prefix_fixed ? 1 : 0;
-  std::memcpy(ca.k1, ctx->chal_k1, sizeof(ca.k1));
-  std::memcpy(ca.k2, ctx->chal_k2, sizeof(ca.k2));
+  set_challenge_schedules(ctx, ca);
   ca.n = (int64_t)n;
   words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
   ca.y1 = pa.y1;

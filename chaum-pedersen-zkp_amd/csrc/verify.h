@@ -63,16 +63,29 @@ CPZ_HD sc transcript_challenge(Strobe<Acc>& s, const uint32_t y1[8], const uint3
 constexpr int kTailPrefixPos = 32, kTailPrefixBegin = 0, kTailPrefixFlags = kFlagA;
 constexpr int kTailY1 = 42, kTailY2 = 84, kTailR1 = 126, kTailR2 = 2;
 
+// Fixed-schedule tail for entries whose context is exactly 32 bytes -- every entry of the
+// reference service, whose challenge ids are 32 random bytes (service.rs:294-295, appended
+// at :373 and in the batch path at :516).  The context follows Transcript::new directly,
+// so the sponge enters it at byte 96 (begin 68, flags A); from there every position is
+// fixed again: the context at byte 111 of segment 0, g and h (constants, folded into the
+// masks) straddle into segment 1, y1 / y2 at bytes 89 / 131 of segment 1, r1 / r2 at 7 / 49
+// of segment 2, and the challenge header's C flag forces the third permutation.
+constexpr int kC32PrefixPos = 96, kC32PrefixBegin = 68, kC32PrefixFlags = kFlagA;
+constexpr int kC32Ctx = 111, kC32Y1 = 89, kC32Y2 = 131, kC32R1 = 7, kC32R2 = 49;
+
+// XOR a 32-byte message into the word image of the sponge at byte offset OFF (any
+// alignment: a misaligned message is two funnel-shifted halves per word).
 template <int OFF>
 CPZ_HD void xor_message(uint32_t st[50], const uint32_t w[8]) {
-  static_assert(OFF % 2 == 0, "messages start on 16-bit boundaries in this schedule");
+  static_assert(OFF >= 0 && OFF + 32 <= kStrobeR, "a message must lie inside one sponge segment");
+  constexpr int sh = 8 * (OFF % 4);
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    if (OFF % 4 == 0) {
+    if (sh == 0) {
       st[OFF / 4 + k] ^= w[k];
     } else {
-      st[OFF / 4 + k] ^= w[k] << 16;
-      st[OFF / 4 + k + 1] ^= w[k] >> 16;
+      st[OFF / 4 + k] ^= w[k] << sh;
+      st[OFF / 4 + k + 1] ^= w[k] >> (32 - sh);
     }
   }
 }
@@ -105,9 +118,38 @@ CPZ_HD sc challenge_fixed(const uint32_t prefix[50], const uint32_t k1[50], cons
   return sc_reduce_wide(st);  // challenge bytes 0..63 = state words 0..15
 }
 
+// 32-byte-context tail: prefix = the state after Transcript::new, m = the three segments'
+// framing masks (challenge_masks_ctx32, g and h included), ctx = the context as 8 words.
+CPZ_HD sc challenge_fixed_ctx32(const uint32_t prefix[50], const uint32_t m[3][50], const uint32_t ctx[8],
+                                const uint32_t y1[8], const uint32_t y2[8], const uint32_t r1[8],
+                                const uint32_t r2[8]) {
+  uint32_t st[50];
+#pragma unroll
+  for (int w = 0; w < 50; w++) st[w] = prefix[w] ^ m[0][w];
+  xor_message<kC32Ctx>(st, ctx);
+  keccak_words(st);
+#pragma unroll
+  for (int w = 0; w < 50; w++) st[w] ^= m[1][w];
+  xor_message<kC32Y1>(st, y1);
+  xor_message<kC32Y2>(st, y2);
+  keccak_words(st);
+#pragma unroll
+  for (int w = 0; w < 50; w++) st[w] ^= m[2][w];
+  xor_message<kC32R1>(st, r1);
+  xor_message<kC32R2>(st, r2);
+  keccak_words(st);
+  return sc_reduce_wide(st);
+}
+
 template <class Acc>
 CPZ_HD sc transcript_challenge(Strobe<Acc>& s, const uint32_t y1[8], const uint32_t y2[8], const uint32_t r1[8],
                                const uint32_t r2[8]);
+
+CPZ_HD void mask_words(uint32_t out[50], const uint8_t m[200]) {
+  for (int w = 0; w < 50; w++)
+    out[w] = (uint32_t)m[4 * w] | ((uint32_t)m[4 * w + 1] << 8) | ((uint32_t)m[4 * w + 2] << 16) |
+             ((uint32_t)m[4 * w + 3] << 24);
+}
 
 // The constant masks of challenge_fixed, derived by running the generic tail over zero
 // messages with a recording accessor; false if the schedule is not the expected one (two
@@ -153,6 +195,24 @@ template <class Acc>
 CPZ_HD void transcript_parameters(Strobe<Acc>& s, const uint32_t g[8], const uint32_t h[8]) {
   s.merlin_append_words("generator-g", 11, g);
   s.merlin_append_words("generator-h", 11, h);
+}
+
+// The masks of challenge_fixed_ctx32 for generators (g, h): the generic code run from the
+// post-Transcript::new position over a zero context and zero messages, recording; false if
+// the schedule is not the expected one (three permutations before the challenge bytes).
+CPZ_HD bool challenge_masks_ctx32(uint32_t m[3][50], const uint32_t g[8], const uint32_t h[8]) {
+  MaskState ms;
+  for (int k = 0; k < 3; k++)
+    for (int i = 0; i < 200; i++) ms.m[k][i] = 0;
+  Strobe<MaskState> s(ms, kC32PrefixPos, kC32PrefixBegin, (uint8_t)kC32PrefixFlags);
+  const uint8_t zc[32] = {0};
+  const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  transcript_context(s, zc, 32);
+  transcript_parameters(s, g, h);
+  (void)transcript_challenge(s, z, z, z, z);
+  if (ms.seg != 3) return false;
+  for (int k = 0; k < 3; k++) mask_words(m[k], ms.m[k]);
+  return true;
 }
 
 // One equation, [s] B - [c] Y == R (ristretto equality), checked through the half-size

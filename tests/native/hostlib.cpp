@@ -295,6 +295,27 @@ int cpzt_challenge_fixed(uint8_t* out, const uint8_t* g, const uint8_t* h, const
   return 0;
 }
 
+// 32-byte-context fast path (challenge_fixed_ctx32) over the host build.
+int cpzt_challenge_ctx32(uint8_t* out, const uint8_t* g, const uint8_t* h, const uint8_t* ctx, const uint8_t* y1,
+                         const uint8_t* y2, const uint8_t* r1, const uint8_t* r2) {
+  ArrayState st;
+  Strobe<ArrayState> s = transcript_new(st);
+  if (s.pos != kC32PrefixPos || s.pos_begin != kC32PrefixBegin || s.cur_flags != kC32PrefixFlags) return -1;
+  uint32_t gw[8], hw[8], m[3][50], pre[50];
+  words_from(gw, g);
+  words_from(hw, h);
+  if (!challenge_masks_ctx32(m, gw, hw)) return -1;
+  std::memcpy(pre, st.b, 200);
+  uint32_t cw[8], a[8], b[8], c[8], d[8];
+  words_from(cw, ctx);
+  words_from(a, y1);
+  words_from(b, y2);
+  words_from(c, r1);
+  words_from(d, r2);
+  bytes_from(out, challenge_fixed_ctx32(pre, m, cw, a, b, c, d).w);
+  return 0;
+}
+
 // Half-size challenge split: u, |v| (16 bytes each, little-endian), sign of v.
 void cpzt_half_split(uint8_t* u_out, uint8_t* v_out, int* vneg, const uint8_t* c) {
   uint32_t cw[8], u[4], v[4];

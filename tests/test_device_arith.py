@@ -228,3 +228,22 @@ def test_challenge_fixed_schedule(lib, golden):
     lib.cpzt_challenge(want, h, g, *(bytes.fromhex(p[k]) for k in ("y1", "y2", "r1", "r2")), None, 0, 0)
     assert lib.cpzt_challenge_fixed(got, h, g, *(bytes.fromhex(p[k]) for k in ("y1", "y2", "r1", "r2"))) == 0
     assert got.raw == want.raw
+
+
+def test_challenge_ctx32_schedule(lib, golden):
+    """The 32-byte-context fast path (the service's challenge ids: three permutations over a
+    register sponge, g and h folded into the masks) equals the generic STROBE tail and the
+    oracle, for the default and for swapped generators."""
+    g, h = bytes.fromhex(golden["g"]), bytes.fromhex(golden["h"])
+    rnd = random.Random(12)
+    for t in range(40):
+        ctx, y1, y2, r1, r2 = (bytes(rnd.randrange(256) for _ in range(32)) for _ in range(5))
+        if t == 0:
+            ctx = y1 = y2 = r1 = r2 = bytes(32)
+        gg, hh = (g, h) if t % 2 == 0 else (h, g)
+        want = ctypes.create_string_buffer(32)
+        lib.cpzt_challenge(want, gg, hh, y1, y2, r1, r2, ctx, 32, 1)
+        got = ctypes.create_string_buffer(32)
+        assert lib.cpzt_challenge_ctx32(got, gg, hh, ctx, y1, y2, r1, r2) == 0
+        assert got.raw == want.raw, t
+        assert int.from_bytes(got.raw, "little") == O.challenge(gg, hh, y1, y2, r1, r2, ctx), t

@@ -236,3 +236,44 @@ def test_long_contexts_and_ragged_batch(gpu):
     assert not ok and list(st_b) == exp
     _, ok, st_b = gpu.verify_batch(*[r[1::3] for r in rows], seed=seed, contexts=ctx_n[1::3])
     assert ok and not st_b.any()
+
+
+def test_ctx32_fast_path_and_mixed_contexts(gpu):
+    """32-byte contexts (the service's challenge ids) take the register fixed-schedule
+    challenge; a batch that mixes them with no context, other lengths and 32-byte contexts
+    at unaligned offsets (generic LDS path) gives the oracle's challenges and verdicts."""
+    rng = np.random.default_rng(32)
+    n = 3000
+    sx, sk = bytes(range(32)), bytes(range(1, 33))
+    ctxs = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for _ in range(n)]
+    syn = gpu.prove_synthetic(n, sx, sk, contexts=ctxs)
+    args = [syn[k] for k in ("y1", "y2", "r1", "r2", "s")]
+    assert not gpu.verify_each(*args, contexts=ctxs).any()
+    c = gpu.challenges(*args[:4], contexts=ctxs)
+    for i in list(range(0, n, 397)) + [n - 1]:
+        exp = O.challenge(O.G_BYTES, O.H_BYTES, *(bytes(a[i]) for a in args[:4]), ctxs[i])
+        assert int.from_bytes(bytes(c[i]), "little") == exp, i
+    # wrong 32-byte context -> equation failure, exactly there
+    bad = list(ctxs)
+    for i in (5, 1000, 2999):
+        bad[i] = bytes(32)
+    st = gpu.verify_each(*args, contexts=bad)
+    assert np.nonzero(st)[0].tolist() == [5, 1000, 2999] and set(st[[5, 1000, 2999]].tolist()) == {1}
+    _, ok, st_b = gpu.verify_batch(*args, seed=bytes(32), contexts=bad)
+    assert not ok and np.nonzero(st_b)[0].tolist() == [5, 1000, 2999]
+    # mixed: entries 0..62 re-proved with None / empty / 31 / 33-byte contexts (1006 bytes in
+    # all) put every later 32-byte context off 4-byte alignment in the concatenated buffer
+    mixed = list(ctxs)
+    for i in range(63):
+        mixed[i] = [None, b"", bytes(31), bytes(33)][i % 4]
+    re = [_prove_oracle(700 + i, mixed[i]) for i in range(63)]
+    rows = [a.copy() for a in args]
+    for i, r in enumerate(re):
+        for a, k in zip(rows, ("y1", "y2", "r1", "r2", "s")):
+            a[i] = np.frombuffer(getattr(r, k), np.uint8)
+    assert sum(len(x) for x in mixed[:63] if x is not None) % 4 != 0
+    assert not gpu.verify_each(*rows, contexts=mixed).any()
+    c = gpu.challenges(*rows[:4], contexts=mixed)
+    for i in list(range(63)) + [63, 64, 65, 66, 1234, n - 1]:
+        exp = O.challenge(O.G_BYTES, O.H_BYTES, *(bytes(a[i]) for a in rows[:4]), mixed[i])
+        assert int.from_bytes(bytes(c[i]), "little") == exp, i
