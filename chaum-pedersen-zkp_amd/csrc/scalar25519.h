@@ -307,7 +307,94 @@ CPZ_HD bool half_below(const uint32_t r[8]) {
   return (r[4] | r[5] | r[6] | r[7]) == 0 && r[3] < 0x60000000u;  // r < 3 * 2^125
 }
 
+// Bit length of a 256-bit value (0 for 0).
+CPZ_HD int words8_bitlen(const uint32_t a[8]) {
+  int n = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++)
+    if (a[j]) n = 32 * j + 32 - __builtin_clz(a[j]);
+  return n;
+}
+
+// floor(a / 2^sh) mod 2^64 for 0 <= sh < 192 (selects, no dynamically indexed array).
+CPZ_HD uint64_t words8_extract64(const uint32_t a[8], int sh) {
+  const int w = sh >> 5, b = sh & 31;
+  uint32_t x0 = 0, x1 = 0, x2 = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    if (j == w) x0 = a[j];
+    if (j == w + 1) x1 = a[j];
+    if (j == w + 2) x2 = a[j];
+  }
+  const uint64_t lo = ((uint64_t)x1 << 32) | x0;
+  return b ? (lo >> b) | ((uint64_t)x2 << (64 - b)) : lo;
+}
+
+// out = a x - b y (mod 2^256) for 32-bit a, b; x, y two's complement.
+CPZ_HD void words8_mulsub2(uint32_t out[8], uint32_t a, const uint32_t x[8], uint32_t b, const uint32_t y[8]) {
+  uint64_t cx = 0, cy = 0;
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const uint64_t px = (uint64_t)x[j] * a + cx, py = (uint64_t)y[j] * b + cy;
+    cx = px >> 32;
+    cy = py >> 32;
+    const uint64_t d = (uint64_t)(uint32_t)px - (uint32_t)py - borrow;
+    out[j] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+}
+
+// out = u x + v y (mod 2^256) for a cofactor row (u, v): u v <= 0 and |u|, |v| < 2^31.
+CPZ_HD void words8_row(uint32_t out[8], int64_t u, int64_t v, const uint32_t x[8], const uint32_t y[8]) {
+  const uint32_t au = (uint32_t)(u < 0 ? -u : u), av = (uint32_t)(v < 0 ? -v : v);
+  if (u > 0 || v < 0)
+    words8_mulsub2(out, au, x, av, y);
+  else
+    words8_mulsub2(out, av, y, au, x);
+}
+
+// One exact Euclid step (r0, r1, t0, t1 as in sc_half_split), partial when the f64
+// quotient estimate is huge.
+CPZ_HD void half_split_step(uint32_t r0[8], uint32_t r1[8], uint32_t t0[8], uint32_t t1[8]) {
+  double qf = words8_to_f64(r0) / words8_to_f64(r1);
+  int k = 0;
+  if (qf >= 0x1p62) {
+    k = ilogb(qf) - 61;
+    qf = ldexp(qf, -k);
+  }
+  uint64_t q = (uint64_t)(qf * (1.0 - 0x1p-46));
+  if (q == 0) q = 1;
+  if (k) {
+    uint32_t xs[8], ts[8];
+    words8_shl(xs, r1, k);
+    words8_shl(ts, t1, k);
+    words8_submul(r0, xs, q);
+    words8_submul(t0, ts, q);
+  } else {
+    words8_submul(r0, r1, q);
+    words8_submul(t0, t1, q);
+  }
+  if (words8_lt(r0, r1)) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      uint32_t x = r0[j]; r0[j] = r1[j]; r1[j] = x;
+      x = t0[j]; t0[j] = t1[j]; t1[j] = x;
+    }
+  }
+}
+
 // c < l canonical.  u, vabs: 4 words each (128-bit); vneg: sign of v.
+//
+// Lehmer's acceleration of the Euclid loop: the quotients are computed on the top 63 bits
+// a = r0 >> sh, b = r1 >> sh with 64-bit integers, accumulating the cofactor matrix
+// (u0 v0; u1 v1), and applied to the 256-bit (r, t) once per batch (~30 bits of quotients,
+// 4-5 batches instead of ~75 multi-word steps).  A step is taken only while it is provably
+// the exact Euclid step of the full numbers: with A_k = u a + v b and |truncation| < 1,
+// the full remainder lies within |u| + |v| of 2^sh R, so R >= e2 (+ T >> sh) and
+// B - R >= e1 + e2 guarantee T <= r_full < previous r_full -- the quotient is the true
+// one and the batch never passes the first remainder below T.  The last steps (and any
+// huge quotient) go through the single-step path, so (u, v) is exactly the Euclid pair.
 CPZ_HD void sc_half_split(const uint32_t c[8], uint32_t u[4], uint32_t vabs[4], bool& vneg) {
   uint32_t r0[8], r1[8], t0[8], t1[8];
 #pragma unroll
@@ -319,29 +406,54 @@ CPZ_HD void sc_half_split(const uint32_t c[8], uint32_t u[4], uint32_t vabs[4], 
   }
 #pragma unroll 1
   while (!half_below(r1)) {
-    double qf = words8_to_f64(r0) / words8_to_f64(r1);
-    int k = 0;
-    if (qf >= 0x1p62) {
-      k = ilogb(qf) - 61;
-      qf = ldexp(qf, -k);
+    const int sh = words8_bitlen(r0) - 63;  // r0 >= r1 >= T > 2^126: sh > 63
+    uint64_t A = words8_extract64(r0, sh), B = words8_extract64(r1, sh);
+    const uint64_t tsh = sh <= 125 ? (3ull << (125 - sh)) : 0ull;  // T >> sh
+    int64_t u0 = 1, v0 = 0, u1 = 0, v1 = 1;
+    int steps = 0;
+#pragma unroll 1
+    while (B != 0) {
+      const double qf = (double)A / (double)B;
+      if (qf >= 0x1p30) break;
+      uint64_t q = (uint64_t)qf;
+      uint64_t qb = q * B;
+      while (qb > A) {
+        q--;
+        qb -= B;
+      }
+      uint64_t R = A - qb;
+      while (R >= B) {
+        q++;
+        R -= B;
+      }
+      const int64_t u2 = u0 - (int64_t)q * u1, v2 = v0 - (int64_t)q * v1;
+      const int64_t au2 = u2 < 0 ? -u2 : u2, av2 = v2 < 0 ? -v2 : v2;
+      const int64_t au1 = u1 < 0 ? -u1 : u1, av1 = v1 < 0 ? -v1 : v1;
+      if (au2 >= (1ll << 31) || av2 >= (1ll << 31)) break;
+      const uint64_t e2 = (uint64_t)(au2 + av2) + 1, e1 = (uint64_t)(au1 + av1) + 1;
+      if (R < e2 + tsh || B - R < e1 + e2) break;
+      A = B;
+      B = R;
+      u0 = u1;
+      v0 = v1;
+      u1 = u2;
+      v1 = v2;
+      steps++;
     }
-    uint64_t q = (uint64_t)(qf * (1.0 - 0x1p-46));
-    if (q == 0) q = 1;
-    if (k) {
-      uint32_t xs[8], ts[8];
-      words8_shl(xs, r1, k);
-      words8_shl(ts, t1, k);
-      words8_submul(r0, xs, q);
-      words8_submul(t0, ts, q);
+    if (steps == 0) {
+      half_split_step(r0, r1, t0, t1);
     } else {
-      words8_submul(r0, r1, q);
-      words8_submul(t0, t1, q);
-    }
-    if (words8_lt(r0, r1)) {
+      uint32_t nr0[8], nr1[8], nt0[8], nt1[8];
+      words8_row(nr0, u0, v0, r0, r1);
+      words8_row(nr1, u1, v1, r0, r1);
+      words8_row(nt0, u0, v0, t0, t1);
+      words8_row(nt1, u1, v1, t0, t1);
 #pragma unroll
       for (int j = 0; j < 8; j++) {
-        uint32_t x = r0[j]; r0[j] = r1[j]; r1[j] = x;
-        x = t0[j]; t0[j] = t1[j]; t1[j] = x;
+        r0[j] = nr0[j];
+        r1[j] = nr1[j];
+        t0[j] = nt0[j];
+        t1[j] = nt1[j];
       }
     }
   }

@@ -195,7 +195,13 @@ def test_half_split(lib):
     rng = random.Random(7)
     cases = [0, 1, 2, (3 << 125) - 1, 3 << 125, L - 1, L - 2, L // 2, L // 3, (L >> 70), (L >> 140) + 5,
              (L >> 126), (L >> 127) + 1, 2**252, (2**128 + 1) % L]
-    cases += [rng.randrange(L) for _ in range(300)]
+    cases += [rng.randrange(L) for _ in range(20000)]
+    # Values near rationals p/q of l: a few tiny-then-huge partial quotients, which stress
+    # the Lehmer batch's exactness conditions and the huge-quotient single steps.
+    for q in (2, 3, 5, 7, 1000, 65537, 2**31 - 1, 2**40 + 3, 2**64 + 13, 2**100 + 7):
+        for p in (1, q // 2 + 1, q - 1):
+            base = L * p // q
+            cases += [(base + d) % L for d in (-2, -1, 0, 1, 2, 1 << 20, rng.randrange(1 << 60))]
     u, v, neg = buf(16), buf(16), ctypes.c_int()
     for c in cases:
         lib.cpzt_half_split(u, v, ctypes.byref(neg), c.to_bytes(32, "little"))
