@@ -11,9 +11,9 @@
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return 1; } } while (0)
 
-enum Cheap { ADD32 = 0, LSHLADD64, ASHR64, BFE32, AND32, MUL_LO, ADD32_E64, ADD3, ANDLIT, ALIGNBIT, SUBCO, NCHEAP };
+enum Cheap { ADD32 = 0, LSHLADD64, ASHR64, BFE32, AND32, MUL_LO, ADD32_E64, ADD3, ANDLIT, ALIGNBIT, SUBCO, FMA64, MAD24, MULHI24, PKFMA32, MADU64, NCHEAP };
 static const char* kCheap[NCHEAP] = {"v_add_u32", "v_lshl_add_u64", "v_ashrrev_i64", "v_bfe_i32", "v_and_b32",
-                                     "v_mul_lo_u32", "v_add_u32_e64", "v_add3_u32", "v_and_b32(literal)", "v_alignbit_b32", "v_sub_co+v_subb_co"};
+                                     "v_mul_lo_u32", "v_add_u32_e64", "v_add3_u32", "v_and_b32(literal)", "v_alignbit_b32", "v_sub_co+v_subb_co", "v_fma_f64", "v_mad_u32_u24", "v_mul_hi_u32_u24", "v_pk_fma_f32", "v_mad_u64_u32"};
 
 template <int NM, int NA, int OP>
 __global__ void __launch_bounds__(256) kmix(int iters, uint64_t* out, uint32_t seed) {
@@ -67,6 +67,20 @@ __global__ void __launch_bounds__(256) kmix(int iters, uint64_t* out, uint32_t s
           uint32_t lo = (uint32_t)y, hi = (uint32_t)(y >> 32);
           asm volatile("v_sub_co_u32 %0, vcc, %0, %2\n\tv_subb_co_u32 %1, vcc, %1, %2, vcc" : "+v"(lo), "+v"(hi) : "v"(b) : "vcc");
           y = ((uint64_t)hi << 32) | lo;
+        } else if constexpr (OP == FMA64) {
+          asm volatile("v_fma_f64 %0, %0, %0, %0" : "+v"(y));
+        } else if constexpr (OP == MADU64) {
+          asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(y) : "v"(a), "v"(b) : "vcc");
+        } else if constexpr (OP == PKFMA32) {
+          asm volatile("v_pk_fma_f32 %0, %0, %0, %0" : "+v"(y));
+        } else if constexpr (OP == MAD24) {
+          uint32_t lo = (uint32_t)y;
+          asm volatile("v_mad_u32_u24 %0, %0, %1, %0" : "+v"(lo) : "v"(b));
+          y = lo;
+        } else if constexpr (OP == MULHI24) {
+          uint32_t lo = (uint32_t)y;
+          asm volatile("v_mul_hi_u32_u24 %0, %0, %1" : "+v"(lo) : "v"(b));
+          y = lo;
         } else if constexpr (OP == MUL_LO) {
           uint32_t lo = (uint32_t)y;
           asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(lo) : "v"(b));
@@ -116,6 +130,12 @@ int main() {
   CHECK(hipEventCreate(&e1));
   const int iters = 4000;
   for (int w : {2, 4}) {
+    RUN(0, 16, FMA64)
+    RUN(0, 16, MADU64)
+    RUN(0, 16, PKFMA32)
+    RUN(0, 16, MAD24)
+    RUN(0, 16, MULHI24)
+    RUN(8, 8, FMA64)
     RUN(0, 16, ADD32_E64)
     RUN(0, 16, ADD3)
     RUN(0, 16, ANDLIT)
