@@ -69,6 +69,9 @@ def main():
     ap.add_argument("--rlc-extra", type=int, default=1,
                     help="at N=1 in 'each' mode also time the RLC batch path on the same proofs (reported "
                          "under 'rlc', not in value)")
+    ap.add_argument("--host-e2e", type=int, default=1,
+                    help="at N=1 in 'each' mode also time the host-buffer entry point (PCIe included; "
+                         "reported under 'host_e2e', not in value)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -171,6 +174,24 @@ def main():
                      "proofs_per_s": n * args.steps / r_el, "ms_per_step": r_el * 1e3 / args.steps,
                      "kernel_ms_per_step": {k: v[0] / args.steps for k, v in r_st.items()}}
 
+    host_e2e = None
+    if args.mode == "each" and world == 1 and args.host_e2e:
+        # The drop-in boundary hands over HOST buffers (cpz_verify_each): time that path too,
+        # PCIe copies of 160 B/proof included (overlapped with the kernels chunk by chunk).
+        # Reported beside value, never as value.
+        hrows = {k: t[k].cpu().numpy() for k in t}
+        hst = gpu.verify_each(hrows["y1"], hrows["y2"], hrows["r1"], hrows["r2"], hrows["s"])
+        steps_h = max(1, min(args.steps, 5))
+        h0 = time.perf_counter()
+        for _ in range(steps_h):
+            hst = gpu.verify_each(hrows["y1"], hrows["y2"], hrows["r1"], hrows["r2"], hrows["s"])
+        h_el = time.perf_counter() - h0
+        if int((hst != 0).sum()):
+            raise SystemExit("bench: host-buffer path rejected valid proofs")
+        host_e2e = {"workload": "cpz_verify_each from pageable host arrays (H2D of 5 x 32 B/proof + D2H of statuses)",
+                    "proofs_per_s": n * steps_h / h_el, "ms_per_call": h_el * 1e3 / steps_h, "calls": steps_h}
+        del hrows
+
     total = world * n * args.steps
     value = total / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
@@ -181,7 +202,10 @@ def main():
     v_ms, v_cnt = stages.get("verify_each", (0.0, 0))
     c_ms, c_cnt = stages.get("challenge", (0.0, 0))
     v_avg_s = (v_ms / v_cnt) * 1e-3 if v_cnt else None
-    achieved = (mads * n / v_avg_s) / 1e12 if v_avg_s else None
+    # the runtime cuts a batch into launches of one proof per thread (2^17 on MI355X):
+    # achieved = algorithmic MADs of one launch / that launch's average duration
+    per_launch = (n * args.steps / v_cnt) if v_cnt else None
+    achieved = (mads * per_launch / v_avg_s) / 1e12 if v_avg_s else None
     pmc = _load_json("profiles/r01_verify_each_pmc.json") or {}
     roofline = {
         "kernel": "k_verify_each",
@@ -193,8 +217,10 @@ def main():
         "traffic": pmc.get("hbm_bytes_per_launch"),
         "algorithmic_mads_per_proof": mads,
         "kernel_ms": v_ms / v_cnt if v_cnt else None,
+        "proofs_per_launch": per_launch,
+        "verify_ms_per_step": v_ms / args.steps if v_cnt else None,
         "challenge_kernel_ms": c_ms / c_cnt if c_cnt else None,
-        "hbm_frac": ((194 * n / v_avg_s) / 8.0e12) if v_avg_s else None,
+        "hbm_frac": ((194 * per_launch / v_avg_s) / 8.0e12) if v_avg_s else None,
     }
 
     cpu = None
@@ -232,6 +258,8 @@ def main():
             line["roofline"] = None
         if rlc_extra:
             line["rlc"] = rlc_extra
+        if host_e2e:
+            line["host_e2e"] = host_e2e
         print(json.dumps(line), flush=True)
     gpu.close()
     if world > 1:

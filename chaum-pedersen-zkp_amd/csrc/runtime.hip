@@ -65,6 +65,9 @@ struct DevBuf {
   }
 };
 
+// Host-buffer pipeline chunk (proofs): 2^17 proofs = 20 MiB of inputs, ~2.8 ms of verify work.
+constexpr size_t kPipeChunk = size_t(1) << 17;
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 }  // namespace
@@ -95,6 +98,10 @@ struct cpz_ctx {
   // host-API staging
   DevBuf in[5];
   DevBuf ctxb, ctxo, ctxp;
+  // host-buffer pipeline (cpz_verify_each): H2D copies of chunk j+1 on their own stream
+  // while chunk j verifies on `stream`
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t copy_done = nullptr;
   // wire-format ingestion
   DevBuf pz_blob, pz_off, pz_rows, pz_code, pz_aux;
   // RLC / Pippenger buffers (sized for the largest batch seen)
@@ -209,12 +216,37 @@ int verify_grid(cpz_ctx* ctx, size_t n) {
   return (int)(want < cap ? want : cap);
 }
 
+// k_verify_each over va.n proofs as launches of one proof per thread: the grid is the
+// occupancy-limited size (verify_grid), so a batch larger than grid * kVerifyBlock proofs is
+// cut into that many proofs per launch rather than looping inside one launch.  Measured on
+// MI355X at 2^20 proofs: 8 launches of 2^17 take 19.96 ms, one grid-stride launch 21.59 ms
+// (tools/chunk_probe.py): the waves of a launch stay in the same phase of the (I-cache-
+// sized) kernel, while 8 grid-stride iterations let them drift apart.
+int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hipStream_t st) {
+  const int grid = verify_grid(ctx, (size_t)va.n);
+  CPZ_HIP(ctx->scratch.ensure((size_t)grid * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached)));
+  const int64_t per = (int64_t)grid * cpz::kVerifyBlock;
+  for (int64_t a = 0; a < va.n; a += per) {
+    cpz::VerifyArgs v = va;
+    v.n = (va.n - a) < per ? (va.n - a) : per;
+    v.y1 = va.y1 + 8 * a;
+    v.y2 = va.y2 + 8 * a;
+    v.r1 = va.r1 + 8 * a;
+    v.r2 = va.r2 + 8 * a;
+    v.s = va.s + 8 * a;
+    v.c = va.c + 8 * a;
+    v.status = va.status + a;
+    v.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p);
+    StageTimer t(ctx, stage, st);
+    CPZ_HIP(cpz::launch_verify_each(v, grid, st));
+  }
+  return CPZ_OK;
+}
+
 int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
                    const void* s, const void* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
                    uint8_t* status, hipStream_t st) {
   CPZ_HIP(ctx->c.ensure(n * 32));
-  const int grid = verify_grid(ctx, n);
-  CPZ_HIP(ctx->scratch.ensure((size_t)grid * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached)));
   cpz::ChallengeArgs ca;
   set_challenge_schedules(ctx, ca);
   ca.n = (int64_t)n;
@@ -244,12 +276,8 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   va.c = ca.c_out;
   va.status = status;
   va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
-  va.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p);
-  {
-    StageTimer t(ctx, 1, st);
-    CPZ_HIP(cpz::launch_verify_each(va, grid, st));
-  }
-  return CPZ_OK;
+  va.scratch = nullptr;  // set per launch
+  return launch_verify_chunks(ctx, va, 1, st);
 }
 
 // Stage host inputs on the device.  Returns device pointers through out[].
@@ -428,12 +456,8 @@ int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const voi
     va.c = static_cast<const uint32_t*>(ctx->c.p) + 8 * a;
     va.status = status + a;  // decode-level status in, final status out
     va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
-    const int grid = verify_grid(ctx, (size_t)(b - a));
-    CPZ_HIP(ctx->scratch.ensure((size_t)grid * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached)));
-    va.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p);
-    StageTimer t(ctx, 4, st);
-    CPZ_HIP(cpz::launch_verify_each(va, grid, st));
-    return CPZ_OK;
+    va.scratch = nullptr;  // set per launch
+    return launch_verify_chunks(ctx, va, 4, st);
   };
   if (hi - lo <= kLeaf || depth > 12) return per_proof(lo, hi);
   int64_t cuts[kFanout + 1];
@@ -689,6 +713,11 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->ctxb.release();
   ctx->ctxo.release();
   ctx->ctxp.release();
+  if (ctx->copy_done) (void)hipEventDestroy(ctx->copy_done);
+  if (ctx->copy_stream) {
+    (void)hipStreamSynchronize(ctx->copy_stream);
+    (void)hipStreamDestroy(ctx->copy_stream);
+  }
   for (DevBuf* b : {&ctx->pz_blob, &ctx->pz_off, &ctx->pz_rows, &ctx->pz_code, &ctx->pz_aux}) b->release();
   for (DevBuf* b : {&ctx->rl_pts, &ctx->rl_dig, &ctx->rl_bsum, &ctx->rl_counts, &ctx->rl_offsets, &ctx->rl_bhist,
                     &ctx->rl_idx, &ctx->rl_inter, &ctx->rl_buckets, &ctx->rl_heads, &ctx->rl_segs, &ctx->rl_segw, &ctx->rl_win, &ctx->rl_partial,
@@ -697,6 +726,51 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
+
+namespace {
+
+// Host-buffer per-proof verification in chunks of kPipeChunk proofs: the five input
+// arrays of chunk j + 1 are copied (pageable H2D, on ctx->copy_stream) while chunk j's
+// challenge + verify kernels run on ctx->stream, which waits on an event recorded after
+// each chunk's copies.  Each chunk lands at its own offset of the full-size device arrays,
+// so no copy overwrites data a queued kernel still reads.  Contexts (if any) are staged
+// whole first; chunk j passes its slice of the offsets / presence flags (the offsets stay
+// relative to the staged blob).  Statuses come back in one D2H copy at the end.
+int verify_each_pipelined(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], const uint8_t* ctx_bytes,
+                          const uint64_t* ctx_off, const uint8_t* ctx_present, uint8_t* status_out) {
+  const void* unused[5];
+  const void* dcb;
+  const uint64_t* dco;
+  const uint8_t* dcp;
+  int rc = stage_inputs(ctx, n, host, 0, ctx_bytes, ctx_off, ctx_present, unused, &dcb, &dco, &dcp);
+  if (rc) return rc;
+  for (int k = 0; k < 5; k++) CPZ_HIP(ctx->in[k].ensure(n * 32));
+  CPZ_HIP(ctx->st.ensure(n));
+  if (!ctx->copy_stream) CPZ_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+  if (!ctx->copy_done) CPZ_HIP(hipEventCreateWithFlags(&ctx->copy_done, hipEventDisableTiming));
+  uint8_t* st = static_cast<uint8_t*>(ctx->st.p);
+  for (size_t off = 0; off < n; off += kPipeChunk) {
+    const size_t m = (n - off) < kPipeChunk ? (n - off) : kPipeChunk;
+    uint8_t* d[5];
+    for (int k = 0; k < 5; k++) {
+      d[k] = static_cast<uint8_t*>(ctx->in[k].p) + off * 32;
+      CPZ_HIP(hipMemcpyAsync(d[k], host[k] + off * 32, m * 32, hipMemcpyHostToDevice, ctx->copy_stream));
+    }
+    CPZ_HIP(hipEventRecord(ctx->copy_done, ctx->copy_stream));
+    CPZ_HIP(hipStreamWaitEvent(ctx->stream, ctx->copy_done, 0));
+    rc = enqueue_verify(ctx, m, d[0], d[1], d[2], d[3], d[4], dcb, dco ? dco + off : nullptr,
+                        dcp ? dcp + off : nullptr, st + off, ctx->stream);
+    if (rc) {
+      (void)hipStreamSynchronize(ctx->stream);
+      return rc;
+    }
+  }
+  CPZ_HIP(hipMemcpyAsync(status_out, st, n, hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipStreamSynchronize(ctx->stream));
+  return CPZ_OK;
+}
+
+}  // namespace
 
 int cpz_verify_each_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, const void* d_y1,
                            const void* d_y2, const void* d_r1, const void* d_r2, const void* d_s,
@@ -730,6 +804,7 @@ int cpz_verify_each(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
   const uint8_t* host[5] = {y1, y2, r1, r2, s};
+  if (n > kPipeChunk) return verify_each_pipelined(ctx, n, host, ctx_bytes, ctx_off, ctx_present, status_out);
   const void* dev[5];
   const void* dcb;
   const uint64_t* dco;

@@ -277,3 +277,46 @@ def test_ctx32_fast_path_and_mixed_contexts(gpu):
     for i in list(range(63)) + [63, 64, 65, 66, 1234, n - 1]:
         exp = O.challenge(O.G_BYTES, O.H_BYTES, *(bytes(a[i]) for a in rows[:4]), mixed[i])
         assert int.from_bytes(bytes(c[i]), "little") == exp, i
+
+
+def test_host_pipeline_chunk_boundaries(gpu):
+    """cpz_verify_each on host buffers larger than one pipeline chunk (2^17 proofs): the
+    copies of chunk j + 1 overlap chunk j's kernels.  Three chunks, the last ragged; contexts
+    present on most entries (per-chunk slices of the offsets / presence flags); forgeries,
+    a wrong context and an undecodable point on both sides of each chunk boundary.  The
+    statuses must be exactly the expected ones and equal the single-launch device path."""
+    torch = pytest.importorskip("torch")
+    import chaum_pedersen as cp
+    chunk = 1 << 17
+    n = 2 * chunk + 12345
+    rng = np.random.default_rng(17)
+    ctxs = [None if i % 5 == 0 else rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for i in range(n)]
+    syn = gpu.prove_synthetic(n, bytes(range(32)), bytes(range(2, 34)), contexts=ctxs)
+    rows = [np.ascontiguousarray(syn[k]) for k in ("y1", "y2", "r1", "r2", "s")]
+    assert not gpu.verify_each(*rows, contexts=ctxs).any()
+    exp = np.zeros(n, np.uint8)
+    forged = [0, chunk - 1, chunk + 1, 2 * chunk - 1, n - 1]
+    for i in forged:
+        v = (int.from_bytes(rows[4][i].tobytes(), "little") + 1) % O.L
+        rows[4][i] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)
+        exp[i] = cp.STATUS_EQ_FAIL
+    bad_ctx = chunk + 2  # i % 5 != 0: has a context
+    ctxs[bad_ctx] = bytes(32)
+    exp[bad_ctx] = cp.STATUS_EQ_FAIL
+    bad_pt = 2 * chunk
+    rows[2][bad_pt] = np.frombuffer(bytes.fromhex("01" + "00" * 31), np.uint8)
+    exp[bad_pt] = cp.STATUS_BAD_POINT
+    st = gpu.verify_each(*rows, contexts=ctxs)
+    assert np.nonzero(st)[0].tolist() == np.nonzero(exp)[0].tolist()
+    assert np.array_equal(st, exp)
+    # the device path (one launch over everything) agrees
+    dev = torch.device("cuda:0")
+    d = [torch.from_numpy(r).to(dev) for r in rows]
+    blob, off, present = cp._ctx_arrays(ctxs, n)
+    d_blob = torch.from_numpy(blob).to(dev) if blob is not None and len(blob) else torch.zeros(16, dtype=torch.uint8, device=dev)
+    d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    d_present = torch.from_numpy(present).to(dev) if present is not None else None
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    gpu.verify_each_device(*d, status, ctx_bytes=d_blob, ctx_off=d_off, ctx_present=d_present)
+    torch.cuda.synchronize()
+    assert np.array_equal(status.cpu().numpy(), exp)

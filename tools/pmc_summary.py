@@ -6,7 +6,8 @@
 Per kernel: average duration (kernel trace), FETCH_SIZE / WRITE_SIZE (kB per launch, one
 counter per pass; FETCH doubled per MI355X_MICROARCH.md's gfx950 correction for wide
 coalesced reads) and the SQ counters.  k_verify_each also gets its per-proof figures
-(2^20 proofs per launch in the bench workload).
+(2^17 proofs per launch in the bench workload: the runtime cuts 2^20 into 8 launches of
+one proof per thread).
 """
 import csv
 import collections
@@ -55,10 +56,11 @@ for k, d in out.items():
         d["hbm_bytes_per_launch"] = 2 * d["FETCH_SIZE"] * 1024 + d["WRITE_SIZE"] * 1024
 ve = out.get("k_verify_each", {})
 if ve:
-    n = 1 << 20
+    n = int(os.environ.get("PROOFS_PER_LAUNCH", 1 << 17))
     if "SQ_INSTS_VALU" in ve:
         ve["valu_instructions_per_proof"] = ve["SQ_INSTS_VALU"] * 64 / n
-    ve["workload"] = "2^20 proofs per launch (bench.py default), rocprofv3 --pmc, one counter group per pass"
+    ve["workload"] = ("%d proofs per launch (bench.py default 2^20 per step = 8 launches), rocprofv3 --pmc, "
+                      "one counter group per pass" % n)
     ve["correction"] = ("gfx950: FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads "
                         "(MI355X_MICROARCH.md HBM) -> doubled; WRITE_SIZE as reported; units kB")
     ve["algorithmic_bytes_per_launch"] = 194 * n
