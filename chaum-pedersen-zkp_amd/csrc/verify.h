@@ -14,6 +14,15 @@
 #include "scalarmul.h"
 #include "transcript.h"
 
+// Loops over the two points of an equation and over the two equations: rolled by default
+// (one copy of the decode / Straus code); -DCPZ_VERIFY_UNROLLED unrolls them (4 inlined
+// decodes, 2 Straus loops) for side-by-side measurement.
+#if defined(CPZ_VERIFY_UNROLLED)
+#define CPZ_EQ_LOOP _Pragma("unroll 2")
+#else
+#define CPZ_EQ_LOOP _Pragma("unroll 1")
+#endif
+
 namespace cpz {
 
 constexpr uint8_t kStOk = 0, kStEqFail = 1, kStBadPoint = 2, kStBadScalar = 3, kStIdentityOrZero = 4;
@@ -227,15 +236,14 @@ template <class Comb>
 CPZ_HD bool check_equation(const uint32_t y[8], const uint32_t r[8], const uint32_t udig[4], const uint32_t vdig[4],
                            bool vneg, const uint32_t sdig[8], const Comb& comb, ge_cached* tab_y, ge_cached* tab_r,
                            bool& decoded, bool& r_identity) {
-  {
+  // One copy of the decode + table code for both points (a rolled loop): the kernel's
+  // instruction footprint, not its arithmetic, is what the 64 KB instruction cache sees.
+  decoded = true;
+CPZ_EQ_LOOP
+  for (int k = 0; k < 2; k++) {
     ge_p3 P;
-    decoded = ristretto_decode(P, y);
-    build_cached_table(tab_y, ge_neg(P));
-  }
-  {
-    ge_p3 R;
-    decoded = ristretto_decode(R, r) && decoded;
-    build_cached_table(tab_r, vneg ? R : ge_neg(R));
+    decoded = ristretto_decode(P, k ? r : y) && decoded;
+    build_cached_table(k ? tab_r : tab_y, (k && vneg) ? P : ge_neg(P));
   }
   r_identity = words8_zero(r);
   return ristretto_is_identity(straus_half_comb(tab_y, tab_r, comb, udig, vdig, sdig));
@@ -265,13 +273,20 @@ CPZ_HD uint8_t verify_proof(const uint32_t y1[8], const uint32_t y2[8], const ui
     if (vneg) sp = sc_neg(sp);
     sc_recode_radix65536(sdig, sp.w);
   }
-  bool dec1, dec2, id1, id2;
-  const bool eq1 = check_equation(y1, r1, udig, vdig, vneg, sdig, comb_g, tab_v, tab_v + kTableSlots, dec1, id1);
-  const bool eq2 = check_equation(y2, r2, udig, vdig, vneg, sdig, comb_h, tab_v, tab_v + kTableSlots, dec2, id2);
-  if (!(dec1 && dec2)) return kStBadPoint;
+  // The two equations share one copy of the code too (rolled loop over e).
+  bool dec = true, id = false, eq = true;
+CPZ_EQ_LOOP
+  for (int e = 0; e < 2; e++) {
+    bool d, r_id;
+    eq = check_equation(e ? y2 : y1, e ? r2 : r1, udig, vdig, vneg, sdig, e ? comb_h : comb_g, tab_v,
+                        tab_v + kTableSlots, d, r_id) && eq;
+    dec = dec && d;
+    id = id || r_id;
+  }
+  if (!dec) return kStBadPoint;
   if (st_s == kStBadScalar) return kStBadScalar;
-  if (id1 || id2 || st_s == kStIdentityOrZero) return kStIdentityOrZero;
-  return (eq1 && eq2) ? kStOk : kStEqFail;
+  if (id || st_s == kStIdentityOrZero) return kStIdentityOrZero;
+  return eq ? kStOk : kStEqFail;
 }
 
 }  // namespace cpz
