@@ -15,7 +15,10 @@ constexpr uint8_t kStatusIdentityOrZero = 4;
 
 constexpr int kNielsEntries = kTableB;   // radix-256 signed digits: |d| <= 128
 constexpr int kCachedEntries = 2 * kTableSlots;   // y and r tables (identity + 1..8): |d| <= 8
-constexpr int kVerifyBlock = 256;
+#ifndef CPZ_VERIFY_BLOCK
+#define CPZ_VERIFY_BLOCK 256
+#endif
+constexpr int kVerifyBlock = CPZ_VERIFY_BLOCK;  // threads per k_verify_each block
 
 // Merlin/STROBE sponge snapshot.
 struct StrobeSnap {
