@@ -27,7 +27,7 @@ __all__ = [
     "Error", "InvalidParams", "InvalidScalar", "InvalidGroupElement", "CpzError",
     "Parameters", "Statement", "Proof", "BatchVerifier", "Gpu", "VerifyResult",
     "MAX_BATCH_SIZE", "PROTOCOL_VERSION", "STATUS_OK", "STATUS_EQ_FAIL", "STATUS_BAD_POINT",
-    "STATUS_BAD_SCALAR", "STATUS_IDENTITY_OR_ZERO", "default_generators",
+    "STATUS_BAD_SCALAR", "STATUS_IDENTITY_OR_ZERO", "default_generators", "verify_each_multi", "verify_batch_multi",
 ]
 
 MAX_BATCH_SIZE = 1000          # batch.rs:48
@@ -438,6 +438,47 @@ class Gpu:
             self._h, params.g, params.h, n, first_index, bytes(seed_x), bytes(seed_k), dp(ctx_bytes), dp(ctx_off),
             dp(ctx_present), y1.data_ptr(), y2.data_ptr(), r1.data_ptr(), r2.data_ptr(), s.data_ptr(),
             _torch_stream(stream)))
+
+
+def _ctx_list(gpus: Sequence[Gpu]):
+    if not gpus:
+        raise InvalidParams("no GPU contexts")
+    return (ctypes.c_void_p * len(gpus))(*[g._h.value for g in gpus])
+
+
+def verify_each_multi(gpus: Sequence[Gpu], y1, y2, r1, r2, s, contexts=None,
+                      params: Optional[Parameters] = None) -> np.ndarray:
+    """Per-proof statuses with the proofs sharded over several contexts (one per GPU, in
+    shard order; cpz_verify_each_multi, one host thread per shard)."""
+    params = params or Parameters()
+    n = len(y1)
+    arrs = [_rows(a, n, nm) for a, nm in ((y1, "y1"), (y2, "y2"), (r1, "r1"), (r2, "r2"), (s, "s"))]
+    blob, off, present = _ctx_arrays(contexts, n)
+    out = np.empty(n, dtype=np.uint8)
+    lib = gpus[0]._lib if gpus else _native.load()
+    _native.check(lib.cpz_verify_each_multi(_ctx_list(gpus), len(gpus), params.g, params.h, n,
+                                            *[_ptr(a) for a in arrs], _ptr(blob), _ptr(off), _ptr(present), _ptr(out)))
+    return out
+
+
+def verify_batch_multi(gpus: Sequence[Gpu], y1, y2, r1, r2, s, seed: bytes, contexts=None,
+                       params: Optional[Parameters] = None, statuses: bool = True):
+    """RLC batch check sharded over several contexts (cpz_verify_batch_multi).  Returns
+    (partials: [bytes] per shard, total: bytes, batch_ok: bool, status: uint8[n] or None)."""
+    params = params or Parameters()
+    n = len(y1)
+    arrs = [_rows(a, n, nm) for a, nm in ((y1, "y1"), (y2, "y2"), (r1, "r1"), (r2, "r2"), (s, "s"))]
+    blob, off, present = _ctx_arrays(contexts, n)
+    k = len(gpus)
+    parts = ctypes.create_string_buffer(32 * max(k, 1))
+    total = ctypes.create_string_buffer(32)
+    ok = ctypes.c_int(0)
+    out = np.empty(n, dtype=np.uint8) if statuses else None
+    lib = gpus[0]._lib if gpus else _native.load()
+    _native.check(lib.cpz_verify_batch_multi(_ctx_list(gpus), k, params.g, params.h, n, *[_ptr(a) for a in arrs],
+                                             _ptr(blob), _ptr(off), _ptr(present), bytes(seed), parts, total,
+                                             ctypes.byref(ok), _ptr(out)))
+    return [parts.raw[32 * i:32 * i + 32] for i in range(k)], total.raw, bool(ok.value), out
 
 
 _default_gpu: Optional[Gpu] = None

@@ -30,7 +30,7 @@ EXPORTED = (
     "cpz_default_generators", "cpz_verify_each", "cpz_verify_each_device", "cpz_challenges",
     "cpz_prove_synthetic", "cpz_prove_synthetic_device", "cpz_ctx_set_timing", "cpz_ctx_stage_times",
     "cpz_verify_batch", "cpz_verify_batch_device", "cpz_combine_partials", "cpz_msm",
-    "cpz_parse_proofs", "cpz_parse_proofs_device",
+    "cpz_parse_proofs", "cpz_parse_proofs_device", "cpz_verify_each_multi", "cpz_verify_batch_multi",
 )
 NUM_STAGES = 8
 
@@ -75,6 +75,11 @@ def _declare(lib):
     lib.cpz_verify_batch.restype = ctypes.c_int
     lib.cpz_verify_batch.argtypes = ([_p, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p, _p, _p, ctypes.c_uint64,
                                      _p, ctypes.POINTER(ctypes.c_int), _p])
+    lib.cpz_verify_each_multi.restype = ctypes.c_int
+    lib.cpz_verify_each_multi.argtypes = [_p, ctypes.c_int, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p, _p, _p]
+    lib.cpz_verify_batch_multi.restype = ctypes.c_int
+    lib.cpz_verify_batch_multi.argtypes = ([_p, ctypes.c_int, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p, _p, _p,
+                                           _p, _p, ctypes.POINTER(ctypes.c_int), _p])
     lib.cpz_verify_batch_device.restype = ctypes.c_int
     lib.cpz_verify_batch_device.argtypes = ([_p, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p, _p, _p,
                                             ctypes.c_uint64, _p, ctypes.POINTER(ctypes.c_int), _p, ctypes.c_int, _p])

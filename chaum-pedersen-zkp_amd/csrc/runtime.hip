@@ -12,6 +12,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/cpz.h"
@@ -658,6 +659,101 @@ int cpz_combine_partials(cpz_ctx* ctx, size_t k, const uint8_t* partials, uint8_
   CPZ_HIP(hipStreamSynchronize(ctx->stream));
   if (!flags[0]) return fail(CPZ_EINVAL, "a partial does not decode");
   if (is_identity) *is_identity = flags[1];
+  return CPZ_OK;
+}
+
+// ---- single-process multi-GPU ------------------------------------------------------------
+}  // extern "C" (the helpers below are C++)
+
+namespace {
+
+constexpr size_t kShardAlign = cpz::kRlcPrepBlock;  // shard boundaries on weight blocks
+
+// [lo, hi) of shard k of nctx (chaum_pedersen/shard.py:shard_range).
+void shard_bounds(size_t n, int nctx, int k, size_t& lo, size_t& hi) {
+  const size_t units = (n + kShardAlign - 1) / kShardAlign;
+  lo = std::min(units * (size_t)k / (size_t)nctx * kShardAlign, n);
+  hi = std::min(units * (size_t)(k + 1) / (size_t)nctx * kShardAlign, n);
+}
+
+// Runs fn(k, lo, hi) for every non-empty shard on its own thread; returns the first failing
+// shard's code with its message moved to the calling thread.
+template <class Fn>
+int run_shards(int nctx, size_t n, Fn fn) {
+  std::vector<int> rc(nctx, CPZ_OK);
+  std::vector<std::string> msg(nctx);
+  std::vector<std::thread> th;
+  for (int k = 0; k < nctx; k++) {
+    size_t lo, hi;
+    shard_bounds(n, nctx, k, lo, hi);
+    if (hi <= lo) continue;
+    th.emplace_back([&, k, lo, hi] {
+      rc[k] = fn(k, lo, hi);
+      if (rc[k] != CPZ_OK) msg[k] = cpz_last_error();
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int k = 0; k < nctx; k++)
+    if (rc[k] != CPZ_OK) return fail(rc[k], "shard " + std::to_string(k) + ": " + msg[k]);
+  return CPZ_OK;
+}
+
+int check_multi(cpz_ctx* const* ctxs, int nctx) {
+  if (!ctxs || nctx <= 0) return fail(CPZ_EINVAL, "no contexts");
+  for (int k = 0; k < nctx; k++)
+    if (!ctxs[k]) return fail(CPZ_EINVAL, "null context in the list");
+  for (int a = 0; a < nctx; a++)
+    for (int b = a + 1; b < nctx; b++)
+      if (ctxs[a] == ctxs[b]) return fail(CPZ_EINVAL, "a context appears twice (one context per shard)");
+  return CPZ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cpz_verify_each_multi(cpz_ctx* const* ctxs, int nctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                          const uint8_t* y1, const uint8_t* y2, const uint8_t* r1, const uint8_t* r2,
+                          const uint8_t* s, const uint8_t* ctx_bytes, const uint64_t* ctx_off,
+                          const uint8_t* ctx_present, uint8_t* status_out) {
+  int rc = check_multi(ctxs, nctx);
+  if (rc) return rc;
+  if (!g || !h) return fail(CPZ_EINVAL, "null generators");
+  if (n == 0) return fail(CPZ_EEMPTY, "Cannot verify empty batch");
+  if (!y1 || !y2 || !r1 || !r2 || !s || !status_out) return fail(CPZ_EINVAL, "null input pointer");
+  return run_shards(nctx, n, [&](int k, size_t lo, size_t hi) {
+    // ctx_off keeps absolute offsets into ctx_bytes: the shard passes its n + 1 slice
+    return cpz_verify_each(ctxs[k], g, h, hi - lo, y1 + 32 * lo, y2 + 32 * lo, r1 + 32 * lo, r2 + 32 * lo,
+                           s + 32 * lo, ctx_bytes, ctx_off ? ctx_off + lo : nullptr,
+                           ctx_present ? ctx_present + lo : nullptr, status_out + lo);
+  });
+}
+
+int cpz_verify_batch_multi(cpz_ctx* const* ctxs, int nctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                           const uint8_t* y1, const uint8_t* y2, const uint8_t* r1, const uint8_t* r2,
+                           const uint8_t* s, const uint8_t* ctx_bytes, const uint64_t* ctx_off,
+                           const uint8_t* ctx_present, const uint8_t seed[32], uint8_t* partials_out,
+                           uint8_t total_out[32], int* batch_ok, uint8_t* status_out) {
+  int rc = check_multi(ctxs, nctx);
+  if (rc) return rc;
+  if (!g || !h || !seed || !partials_out || !total_out || !batch_ok) return fail(CPZ_EINVAL, "null argument");
+  if (n == 0) return fail(CPZ_EEMPTY, "Cannot verify empty batch");
+  if (!y1 || !y2 || !r1 || !r2 || !s) return fail(CPZ_EINVAL, "null input pointer");
+  std::memset(partials_out, 0, (size_t)nctx * 32);  // empty shards contribute the identity
+  std::vector<int> ok(nctx, 1);
+  rc = run_shards(nctx, n, [&](int k, size_t lo, size_t hi) {
+    return cpz_verify_batch(ctxs[k], g, h, hi - lo, y1 + 32 * lo, y2 + 32 * lo, r1 + 32 * lo, r2 + 32 * lo,
+                            s + 32 * lo, ctx_bytes, ctx_off ? ctx_off + lo : nullptr,
+                            ctx_present ? ctx_present + lo : nullptr, seed, (uint64_t)lo, partials_out + 32 * k,
+                            &ok[k], status_out ? status_out + lo : nullptr);
+  });
+  if (rc) return rc;
+  int ident = 0;
+  rc = cpz_combine_partials(ctxs[0], (size_t)nctx, partials_out, total_out, &ident);
+  if (rc) return rc;
+  int all = ident;
+  for (int k = 0; k < nctx; k++) all = all && ok[k];
+  *batch_ok = all ? 1 : 0;
   return CPZ_OK;
 }
 

@@ -173,6 +173,30 @@ int cpz_parse_proofs(cpz_ctx *ctx, size_t n, const uint8_t *blob, const uint64_t
 int cpz_parse_proofs_device(cpz_ctx *ctx, size_t n, const void *d_blob, const uint64_t *d_off, void *d_r1,
                             void *d_r2, void *d_s, void *d_code, void *d_aux, void *stream);
 
+/* Single-process multi-GPU forms: one context per GPU (e.g. the 8 GPUs of a node, or
+ * several contexts on one GPU), the n proofs cut into nctx contiguous shards whose
+ * boundaries are multiples of 256 proofs (the RLC weight-block granule), each shard
+ * verified by its own context on its own host thread -- what a single host process behind
+ * BatchVerifier::verify (batch.rs:171-183) uses instead of one process per GPU.
+ *   cpz_verify_each_multi   per-proof statuses for all n (no data exchange).
+ *   cpz_verify_batch_multi  per-shard RLC partials (weights keyed by the GLOBAL index, so
+ *                           they sum to the single-GPU partial) -> partials_out (nctx x 32,
+ *                           identity for an empty shard), combined on ctxs[0] ->
+ *                           total_out; batch_ok = 1 iff every entry decodes and the sum is
+ *                           the identity; status_out (optional, n) exact per entry, failing
+ *                           shards running their own fallback search.
+ * Contexts are given in shard order; the first failing shard's error is returned (its
+ * message via cpz_last_error on the calling thread). */
+int cpz_verify_each_multi(cpz_ctx *const *ctxs, int nctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                          const uint8_t *y1, const uint8_t *y2, const uint8_t *r1, const uint8_t *r2,
+                          const uint8_t *s, const uint8_t *ctx_bytes, const uint64_t *ctx_off,
+                          const uint8_t *ctx_present, uint8_t *status_out);
+int cpz_verify_batch_multi(cpz_ctx *const *ctxs, int nctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                           const uint8_t *y1, const uint8_t *y2, const uint8_t *r1, const uint8_t *r2,
+                           const uint8_t *s, const uint8_t *ctx_bytes, const uint64_t *ctx_off,
+                           const uint8_t *ctx_present, const uint8_t seed[32], uint8_t *partials_out,
+                           uint8_t total_out[32], int *batch_ok, uint8_t *status_out);
+
 /* Per-kernel timing (HIP events recorded on the launch stream around every kernel).
  * Stages: 0 = k_challenge, 1 = k_verify_each, 2 = RLC decode/weights, 3 = RLC MSM,
  * 4 = fallback.  cpz_ctx_stage_times synchronises, writes the summed milliseconds and

@@ -204,3 +204,43 @@ def test_c5_16m_batch_with_0p1pct_forged(gpu):
     got = np.nonzero(host)[0]
     assert np.array_equal(got, idx)
     assert set(host[idx].tolist()) == {1}
+
+
+def test_multi_context_shards(gpu):
+    """cpz_verify_each_multi / cpz_verify_batch_multi with three contexts (the single-process
+    multi-GPU entry points; here three contexts share the one GPU): statuses equal the
+    single-context ones, shard partials (weights keyed by the global index) sum to the
+    whole-batch partial, empty shards contribute the identity."""
+    import chaum_pedersen as cp
+    n = (1 << 16) + 77
+    rng = np.random.default_rng(5)
+    ctxs = [None if i % 3 else rng.integers(0, 256, 32, dtype=np.uint8).tobytes() for i in range(n)]
+    syn = gpu.prove_synthetic(n, bytes(range(32)), bytes(range(5, 37)), contexts=ctxs)
+    rows = [np.ascontiguousarray(syn[k]) for k in ("y1", "y2", "r1", "r2", "s")]
+    gpus = [cp.Gpu(0), cp.Gpu(0), cp.Gpu(0)]
+    try:
+        seed = bytes(range(100, 132))
+        st = cp.verify_each_multi(gpus, *rows, contexts=ctxs)
+        assert not st.any()
+        parts, total, ok, st_b = cp.verify_batch_multi(gpus, *rows, seed=seed, contexts=ctxs)
+        assert ok and total == bytes(32) and not st_b.any() and parts == [bytes(32)] * 3
+        forged = [3, 21845 + 10, 43690 + 300, n - 1]   # one in each shard, plus the ragged end
+        for i in forged:
+            v = (int.from_bytes(rows[4][i].tobytes(), "little") + 1) % O.L
+            rows[4][i] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)
+        st = cp.verify_each_multi(gpus, *rows, contexts=ctxs)
+        assert np.nonzero(st)[0].tolist() == forged and set(st[forged].tolist()) == {1}
+        parts, total, ok, st_b = cp.verify_batch_multi(gpus, *rows, seed=seed, contexts=ctxs)
+        assert not ok and np.array_equal(st_b, st)
+        whole, ok1, _ = gpu.verify_batch(*rows, seed=seed, contexts=ctxs, statuses=False)
+        assert not ok1 and total == whole
+        assert all(p != bytes(32) for p in parts)
+        # fewer weight blocks than contexts: empty shards, identity partials
+        small = [r[:300] for r in rows]
+        parts, total, ok, st_s = cp.verify_batch_multi(gpus, *small, seed=seed, contexts=ctxs[:300])
+        assert parts[0] == bytes(32) and not ok and np.nonzero(st_s)[0].tolist() == [3]
+        with pytest.raises(cp.CpzError):
+            cp.verify_each_multi([gpus[0], gpus[0]], *small, contexts=ctxs[:300])
+    finally:
+        for g in gpus:
+            g.close()
