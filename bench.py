@@ -202,10 +202,14 @@ def main():
     v_ms, v_cnt = stages.get("verify_each", (0.0, 0))
     c_ms, c_cnt = stages.get("challenge", (0.0, 0))
     v_avg_s = (v_ms / v_cnt) * 1e-3 if v_cnt else None
-    # the runtime cuts a batch into launches of one proof per thread (2^17 on MI355X):
-    # achieved = algorithmic MADs of one launch / that launch's average duration
+    # The runtime cuts a batch into launches of half the occupancy grid (2^16 proofs on
+    # MI355X) on two streams, so two launches are always in flight and their durations
+    # overlap: achieved = algorithmic MADs of the step's verify work / the verify span
+    # (first launch start to last launch end, HIP events on the launch stream).
     per_launch = (n * args.steps / v_cnt) if v_cnt else None
-    achieved = (mads * per_launch / v_avg_s) / 1e12 if v_avg_s else None
+    sp_ms, sp_cnt = stages.get("verify_span", (0.0, 0))
+    span_s = (sp_ms / args.steps) * 1e-3 if sp_cnt else None
+    achieved = (mads * n / span_s) / 1e12 if span_s else None
     pmc = _load_json("profiles/r01_verify_each_pmc.json") or {}
     roofline = {
         "kernel": "k_verify_each",
@@ -218,9 +222,10 @@ def main():
         "algorithmic_mads_per_proof": mads,
         "kernel_ms": v_ms / v_cnt if v_cnt else None,
         "proofs_per_launch": per_launch,
-        "verify_ms_per_step": v_ms / args.steps if v_cnt else None,
+        "launches_in_flight": 2,
+        "verify_span_ms_per_step": sp_ms / args.steps if sp_cnt else None,
         "challenge_kernel_ms": c_ms / c_cnt if c_cnt else None,
-        "hbm_frac": ((194 * per_launch / v_avg_s) / 8.0e12) if v_avg_s else None,
+        "hbm_frac": ((194 * n / span_s) / 8.0e12) if span_s else None,
     }
 
     cpu = None

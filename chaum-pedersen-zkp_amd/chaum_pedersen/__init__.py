@@ -298,7 +298,7 @@ class Gpu:
         self.close()
 
     # -- per-kernel timing (HIP events on the launch stream) -------------------------------
-    STAGES = ("challenge", "verify_each", "rlc_prepare", "rlc_msm", "fallback", "s5", "s6", "s7")
+    STAGES = ("challenge", "verify_each", "rlc_prepare", "rlc_msm", "fallback", "verify_span", "s6", "s7")
 
     def set_timing(self, enable: bool) -> None:
         _native.check(self._lib.cpz_ctx_set_timing(self._h, 1 if enable else 0))

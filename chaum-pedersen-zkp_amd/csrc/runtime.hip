@@ -8,6 +8,8 @@
 //   k_verify_each -> final status                         (decode + two equations)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -103,6 +105,10 @@ struct cpz_ctx {
   // while chunk j verifies on `stream`
   hipStream_t copy_stream = nullptr;
   hipEvent_t copy_done = nullptr;
+  // verify chunks round-robin over the launch stream and these (launch_verify_chunks)
+  hipStream_t aux_stream[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t aux_start = nullptr;
+  hipEvent_t aux_done[3] = {nullptr, nullptr, nullptr};
   // wire-format ingestion
   DevBuf pz_blob, pz_off, pz_rows, pz_code, pz_aux;
   // RLC / Pippenger buffers (sized for the largest batch seen)
@@ -221,13 +227,59 @@ int verify_grid(cpz_ctx* ctx, size_t n) {
 // occupancy-limited size (verify_grid), so a batch larger than grid * kVerifyBlock proofs is
 // cut into that many proofs per launch rather than looping inside one launch.  Measured on
 // MI355X at 2^20 proofs: 8 launches of 2^17 take 19.96 ms, one grid-stride launch 21.59 ms
-// (tools/chunk_probe.py): the waves of a launch stay in the same phase of the (I-cache-
-// sized) kernel, while 8 grid-stride iterations let them drift apart.
-int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hipStream_t st) {
-  const int grid = verify_grid(ctx, (size_t)va.n);
-  CPZ_HIP(ctx->scratch.ensure((size_t)grid * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached)));
+// (tools/chunk_probe.py).  (Not an instruction-cache effect: a 3x smaller kernel measured
+// the same.)
+//
+// The chunks go round-robin to CPZ_VERIFY_STREAMS streams (each with its own scratch slab),
+// and a chunk is 1 / CPZ_VERIFY_CHUNK_DIV of the occupancy grid, so several launches are in
+// flight and one launch's tail (waves finishing at different times) overlaps the next
+// launch's start.  A/B on one box (tools/variants.sh, 2^20 proofs): 1 stream / full grid
+// 49.5 M proofs/s, 2 / full 51.7 M, 3 / full 51.4 M, 4 / full 51.4 M, 2 / half 52.1 M,
+// 4 / half 51.5 M, 3 / third 47.3 M, 4 / quarter 48.8 M.
+#ifndef CPZ_VERIFY_STREAMS
+#define CPZ_VERIFY_STREAMS 2
+#endif
+#ifndef CPZ_VERIFY_CHUNK_DIV
+#define CPZ_VERIFY_CHUNK_DIV 2
+#endif
+// Round-robin position of the verify launches of one call that enqueues several batches
+// (the host-buffer pipeline): launches keep alternating streams across batches, and the
+// streams are joined once at the end.
+struct VerifyRR {
+  int64_t next = 0;
+};
+
+int join_verify_streams(cpz_ctx* ctx, hipStream_t st) {
+  for (int k = 0; k < CPZ_VERIFY_STREAMS - 1; k++) {
+    if (!ctx->aux_stream[k]) continue;
+    CPZ_HIP(hipEventRecord(ctx->aux_done[k], ctx->aux_stream[k]));
+    CPZ_HIP(hipStreamWaitEvent(st, ctx->aux_done[k], 0));
+  }
+  return CPZ_OK;
+}
+
+int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hipStream_t st, VerifyRR* rr,
+                         bool join) {
+  static_assert(CPZ_VERIFY_STREAMS >= 1 && CPZ_VERIFY_STREAMS <= 4, "1..4 verify streams");
+  const int full = (verify_grid(ctx, SIZE_MAX / 2) + CPZ_VERIFY_CHUNK_DIV - 1) / CPZ_VERIFY_CHUNK_DIV;
+  const int grid = std::min(full, verify_grid(ctx, (size_t)va.n));
+  // every stream owns a full-size slab at a fixed offset, whatever this call's grid
+  const size_t slab = (size_t)full * cpz::kVerifyBlock * cpz::kCachedEntries;
   const int64_t per = (int64_t)grid * cpz::kVerifyBlock;
-  for (int64_t a = 0; a < va.n; a += per) {
+  const int64_t chunks = (va.n + per - 1) / per;
+  const int nst = rr ? CPZ_VERIFY_STREAMS : (int)std::min<int64_t>(CPZ_VERIFY_STREAMS, chunks);
+  CPZ_HIP(ctx->scratch.ensure((size_t)CPZ_VERIFY_STREAMS * slab * sizeof(cpz::ge_cached)));
+  if (nst > 1) {
+    if (!ctx->aux_start) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_start, hipEventDisableTiming));
+    CPZ_HIP(hipEventRecord(ctx->aux_start, st));  // the aux streams start after st's prior work
+    for (int k = 0; k < nst - 1; k++) {
+      if (!ctx->aux_stream[k]) CPZ_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[k], hipStreamNonBlocking));
+      if (!ctx->aux_done[k]) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_done[k], hipEventDisableTiming));
+      CPZ_HIP(hipStreamWaitEvent(ctx->aux_stream[k], ctx->aux_start, 0));
+    }
+  }
+  for (int64_t c = 0; c < chunks; c++) {
+    const int64_t a = c * per;
     cpz::VerifyArgs v = va;
     v.n = (va.n - a) < per ? (va.n - a) : per;
     v.y1 = va.y1 + 8 * a;
@@ -237,17 +289,26 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
     v.s = va.s + 8 * a;
     v.c = va.c + 8 * a;
     v.status = va.status + a;
-    v.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p);
-    StageTimer t(ctx, stage, st);
-    CPZ_HIP(cpz::launch_verify_each(v, grid, st));
+    const int k = (int)((rr ? rr->next++ : c) % nst);  // stream k owns scratch slab k
+    v.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p) + (size_t)k * slab;
+    hipStream_t sc = k == 0 ? st : ctx->aux_stream[k - 1];
+    StageTimer t(ctx, stage, sc);
+    CPZ_HIP(cpz::launch_verify_each(v, grid, sc));
   }
+  if (join && nst > 1) return join_verify_streams(ctx, st);
   return CPZ_OK;
 }
 
+// Challenge + verify of n proofs on `st`.  c_buf: where the challenges go (default: the
+// context's buffer from offset 0); rr / join: see VerifyRR.
 int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
                    const void* s, const void* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
-                   uint8_t* status, hipStream_t st) {
-  CPZ_HIP(ctx->c.ensure(n * 32));
+                   uint8_t* status, hipStream_t st, uint32_t* c_buf = nullptr, VerifyRR* rr = nullptr,
+                   bool join = true) {
+  if (!c_buf) {
+    CPZ_HIP(ctx->c.ensure(n * 32));
+    c_buf = static_cast<uint32_t*>(ctx->c.p);
+  }
   cpz::ChallengeArgs ca;
   set_challenge_schedules(ctx, ca);
   ca.n = (int64_t)n;
@@ -261,7 +322,7 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   ca.ctx_off = ctx_off;
   ca.ctx_present = ctx_present;
   ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->prefix.p);
-  ca.c_out = static_cast<uint32_t*>(ctx->c.p);
+  ca.c_out = c_buf;
   ca.status_out = status;
   {
     StageTimer t(ctx, 0, st);
@@ -278,7 +339,8 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   va.status = status;
   va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
   va.scratch = nullptr;  // set per launch
-  return launch_verify_chunks(ctx, va, 1, st);
+  StageTimer span(ctx, 5, st);  // all chunks, all streams (the launches overlap)
+  return launch_verify_chunks(ctx, va, 1, st, rr, join);
 }
 
 // Stage host inputs on the device.  Returns device pointers through out[].
@@ -458,7 +520,7 @@ int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const voi
     va.status = status + a;  // decode-level status in, final status out
     va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
     va.scratch = nullptr;  // set per launch
-    return launch_verify_chunks(ctx, va, 4, st);
+    return launch_verify_chunks(ctx, va, 4, st, nullptr, true);
   };
   if (hi - lo <= kLeaf || depth > 12) return per_proof(lo, hi);
   int64_t cuts[kFanout + 1];
@@ -810,6 +872,14 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->ctxo.release();
   ctx->ctxp.release();
   if (ctx->copy_done) (void)hipEventDestroy(ctx->copy_done);
+  if (ctx->aux_start) (void)hipEventDestroy(ctx->aux_start);
+  for (auto& e : ctx->aux_done)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& a : ctx->aux_stream)
+    if (a) {
+      (void)hipStreamSynchronize(a);
+      (void)hipStreamDestroy(a);
+    }
   if (ctx->copy_stream) {
     (void)hipStreamSynchronize(ctx->copy_stream);
     (void)hipStreamDestroy(ctx->copy_stream);
@@ -842,6 +912,8 @@ int verify_each_pipelined(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], 
   if (rc) return rc;
   for (int k = 0; k < 5; k++) CPZ_HIP(ctx->in[k].ensure(n * 32));
   CPZ_HIP(ctx->st.ensure(n));
+  CPZ_HIP(ctx->c.ensure(n * 32));  // each chunk's challenges at its own offset
+  VerifyRR rr;
   if (!ctx->copy_stream) CPZ_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
   if (!ctx->copy_done) CPZ_HIP(hipEventCreateWithFlags(&ctx->copy_done, hipEventDisableTiming));
   uint8_t* st = static_cast<uint8_t*>(ctx->st.p);
@@ -855,12 +927,16 @@ int verify_each_pipelined(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], 
     CPZ_HIP(hipEventRecord(ctx->copy_done, ctx->copy_stream));
     CPZ_HIP(hipStreamWaitEvent(ctx->stream, ctx->copy_done, 0));
     rc = enqueue_verify(ctx, m, d[0], d[1], d[2], d[3], d[4], dcb, dco ? dco + off : nullptr,
-                        dcp ? dcp + off : nullptr, st + off, ctx->stream);
+                        dcp ? dcp + off : nullptr, st + off, ctx->stream,
+                        static_cast<uint32_t*>(ctx->c.p) + 8 * off, &rr, false);
     if (rc) {
+      (void)join_verify_streams(ctx, ctx->stream);
       (void)hipStreamSynchronize(ctx->stream);
       return rc;
     }
   }
+  rc = join_verify_streams(ctx, ctx->stream);
+  if (rc) return rc;
   CPZ_HIP(hipMemcpyAsync(status_out, st, n, hipMemcpyDeviceToHost, ctx->stream));
   CPZ_HIP(hipStreamSynchronize(ctx->stream));
   return CPZ_OK;

@@ -199,7 +199,8 @@ int cpz_verify_batch_multi(cpz_ctx *const *ctxs, int nctx, const uint8_t g[32], 
 
 /* Per-kernel timing (HIP events recorded on the launch stream around every kernel).
  * Stages: 0 = k_challenge, 1 = k_verify_each, 2 = RLC decode/weights, 3 = RLC MSM,
- * 4 = fallback.  cpz_ctx_stage_times synchronises, writes the summed milliseconds and
+ * 4 = fallback, 5 = the whole per-proof verify of one call (first to last k_verify_each,
+ * whose launches overlap on several streams).  cpz_ctx_stage_times synchronises, writes the summed milliseconds and
  * launch counts per stage since the last call, and resets them. */
 #define CPZ_NUM_STAGES 8
 int cpz_ctx_set_timing(cpz_ctx *ctx, int enable);
