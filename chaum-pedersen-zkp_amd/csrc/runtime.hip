@@ -98,6 +98,7 @@ struct cpz_ctx {
   DevBuf c;         // n x 32
   DevBuf st;        // n
   DevBuf scratch;   // grid x 256 x 8 ge_cached
+  DevBuf work;      // work-queue counter (CPZ_VERIFY_DYNAMIC)
   // host-API staging
   DevBuf in[5];
   DevBuf ctxb, ctxo, ctxp;
@@ -261,6 +262,20 @@ int join_verify_streams(cpz_ctx* ctx, hipStream_t st) {
 int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hipStream_t st, VerifyRR* rr,
                          bool join) {
   static_assert(CPZ_VERIFY_STREAMS >= 1 && CPZ_VERIFY_STREAMS <= 4, "1..4 verify streams");
+#if defined(CPZ_VERIFY_DYNAMIC)
+  if (va.n < (int64_t)1 << 31) {
+    const int g = verify_grid(ctx, (size_t)va.n);
+    CPZ_HIP(ctx->scratch.ensure((size_t)g * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached)));
+    CPZ_HIP(ctx->work.ensure(64));
+    cpz::VerifyArgs v = va;
+    v.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p);
+    StageTimer t(ctx, stage, st);
+    CPZ_HIP(cpz::launch_verify_each_queue(v, g, static_cast<unsigned*>(ctx->work.p), st));
+    (void)rr;
+    (void)join;
+    return CPZ_OK;
+  }
+#endif
   const int full = (verify_grid(ctx, SIZE_MAX / 2) + CPZ_VERIFY_CHUNK_DIV - 1) / CPZ_VERIFY_CHUNK_DIV;
   const int grid = std::min(full, verify_grid(ctx, (size_t)va.n));
   // every stream owns a full-size slab at a fixed offset, whatever this call's grid
@@ -867,6 +882,7 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->c.release();
   ctx->st.release();
   ctx->scratch.release();
+  ctx->work.release();
   for (auto& b : ctx->in) b.release();
   ctx->ctxb.release();
   ctx->ctxo.release();
