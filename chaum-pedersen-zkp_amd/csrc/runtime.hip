@@ -218,9 +218,12 @@ void set_challenge_schedules(const cpz_ctx* ctx, cpz::ChallengeArgs& ca) {
   std::memcpy(ca.c32, ctx->chal_c32, sizeof(ca.c32));
 }
 
+// Resident k_verify_each blocks on the whole chip (occupancy-limited).
+int occupancy_grid(const cpz_ctx* ctx) { return ctx->cus * ctx->verify_blocks_per_cu; }
+
 int verify_grid(cpz_ctx* ctx, size_t n) {
   const size_t want = (n + cpz::kVerifyBlock - 1) / cpz::kVerifyBlock;
-  const size_t cap = (size_t)ctx->cus * (size_t)ctx->verify_blocks_per_cu;
+  const size_t cap = (size_t)occupancy_grid(ctx);
   return (int)(want < cap ? want : cap);
 }
 
@@ -276,7 +279,7 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
     return CPZ_OK;
   }
 #endif
-  const int full = (verify_grid(ctx, SIZE_MAX / 2) + CPZ_VERIFY_CHUNK_DIV - 1) / CPZ_VERIFY_CHUNK_DIV;
+  const int full = (occupancy_grid(ctx) + CPZ_VERIFY_CHUNK_DIV - 1) / CPZ_VERIFY_CHUNK_DIV;
   const int grid = std::min(full, verify_grid(ctx, (size_t)va.n));
   // every stream owns a full-size slab at a fixed offset, whatever this call's grid
   const size_t slab = (size_t)full * cpz::kVerifyBlock * cpz::kCachedEntries;

@@ -1,5 +1,8 @@
-"""Probe: k_verify_each over 2^20 proofs as one grid-stride launch vs 2^k-proof launches
-(device tensors, slices).  Prints per-variant kernel ms (HIP-event stage timers)."""
+"""Probe: k_verify_each over 2^20 proofs as one call vs calls on 2^k-proof slices (device
+tensors).  Prints per-variant kernel ms (HIP-event stage timers).  The launch-size numbers in
+DESIGN.md were taken with a single-stream, one-launch-per-call runtime (today's equivalent:
+a library built with -DCPZ_VERIFY_STREAMS=1 -DCPZ_VERIFY_CHUNK_DIV=1 and a very large chunk);
+with the default runtime every call is itself cut into two-stream launches."""
 import os
 import sys
 
