@@ -240,6 +240,11 @@ int verify_grid(cpz_ctx* ctx, size_t n) {
 // launch's start.  A/B on one box (tools/variants.sh, 2^20 proofs): 1 stream / full grid
 // 49.5 M proofs/s, 2 / full 51.7 M, 3 / full 51.4 M, 4 / full 51.4 M, 2 / half 52.1 M,
 // 4 / half 51.5 M, 3 / third 47.3 M, 4 / quarter 48.8 M.
+// Challenges per verify chunk on the chunk's stream (hidden under the other stream's verify
+// work; +0.5-1.1 % A/B on one box against one up-front challenge launch).
+#ifndef CPZ_CHALLENGE_PER_CHUNK
+#define CPZ_CHALLENGE_PER_CHUNK 1
+#endif
 #ifndef CPZ_VERIFY_STREAMS
 #define CPZ_VERIFY_STREAMS 2
 #endif
@@ -262,8 +267,10 @@ int join_verify_streams(cpz_ctx* ctx, hipStream_t st) {
   return CPZ_OK;
 }
 
+// ca != nullptr: each chunk's challenges are computed on the chunk's own stream right before
+// its verify launch (so they overlap the other stream's verify work) instead of up front.
 int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hipStream_t st, VerifyRR* rr,
-                         bool join) {
+                         bool join, const cpz::ChallengeArgs* ca = nullptr) {
   static_assert(CPZ_VERIFY_STREAMS >= 1 && CPZ_VERIFY_STREAMS <= 4, "1..4 verify streams");
 #if defined(CPZ_VERIFY_DYNAMIC)
   if (va.n < (int64_t)1 << 31) {
@@ -310,6 +317,21 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
     const int k = (int)((rr ? rr->next++ : c) % nst);  // stream k owns scratch slab k
     v.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p) + (size_t)k * slab;
     hipStream_t sc = k == 0 ? st : ctx->aux_stream[k - 1];
+    if (ca) {
+      cpz::ChallengeArgs cc = *ca;
+      cc.n = v.n;
+      cc.y1 = v.y1;
+      cc.y2 = v.y2;
+      cc.r1 = v.r1;
+      cc.r2 = v.r2;
+      cc.s = v.s;
+      cc.c_out = ca->c_out + 8 * a;
+      cc.status_out = ca->status_out + a;
+      if (ca->ctx_off) cc.ctx_off = ca->ctx_off + a;  // absolute offsets into ctx_bytes
+      if (ca->ctx_present) cc.ctx_present = ca->ctx_present + a;
+      StageTimer tc(ctx, 0, sc);
+      CPZ_HIP(cpz::launch_challenge(cc, sc));
+    }
     StageTimer t(ctx, stage, sc);
     CPZ_HIP(cpz::launch_verify_each(v, grid, sc));
   }
@@ -342,10 +364,12 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->prefix.p);
   ca.c_out = c_buf;
   ca.status_out = status;
+#if !CPZ_CHALLENGE_PER_CHUNK
   {
     StageTimer t(ctx, 0, st);
     CPZ_HIP(cpz::launch_challenge(ca, st));
   }
+#endif
   cpz::VerifyArgs va;
   va.n = (int64_t)n;
   va.y1 = ca.y1;
@@ -358,7 +382,11 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
   va.scratch = nullptr;  // set per launch
   StageTimer span(ctx, 5, st);  // all chunks, all streams (the launches overlap)
+#if CPZ_CHALLENGE_PER_CHUNK
+  return launch_verify_chunks(ctx, va, 1, st, rr, join, &ca);
+#else
   return launch_verify_chunks(ctx, va, 1, st, rr, join);
+#endif
 }
 
 // Stage host inputs on the device.  Returns device pointers through out[].
