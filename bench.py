@@ -224,6 +224,7 @@ def main():
         "proofs_per_launch": per_launch,
         "launches_in_flight": 2,
         "verify_span_ms_per_step": sp_ms / args.steps if sp_cnt else None,
+        "span_covers": "all k_verify_each launches of a step and the per-chunk challenge launches between them",
         "challenge_kernel_ms": c_ms / c_cnt if c_cnt else None,
         "hbm_frac": ((194 * n / span_s) / 8.0e12) if span_s else None,
     }
