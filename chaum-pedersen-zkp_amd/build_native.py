@@ -64,6 +64,8 @@ def build_libcpz(force: bool = False, verbose: bool = False, out: str = LIBCPZ, 
     hipcc = _hipcc()
     common = [hipcc, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-I", CSRC,
               "-I", os.path.join(ROOT, "include")] + ["-D" + d for d in defines]
+    if defines and os.environ.get("CPZ_EXTRA_FLAGS"):  # tuning variants only, never the product build
+        common += os.environ["CPZ_EXTRA_FLAGS"].split()
 
     def compile_one(u):
         obj = os.path.join(objdir, u.replace(".hip", ".o"))
