@@ -72,6 +72,10 @@ def main():
     ap.add_argument("--host-e2e", type=int, default=1,
                     help="at N=1 in 'each' mode also time the host-buffer entry point (PCIe included; "
                          "reported under 'host_e2e', not in value)")
+    ap.add_argument("--backend", default="nccl",
+                    help="torch.distributed backend for N > 1 ('nccl' = RCCL over xGMI; 'gloo' only for rehearsals)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank uses cuda:0 (with --backend gloo); not a measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -83,7 +87,9 @@ def main():
     import torch.distributed as dist
 
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(args.backend, init_method="env://")
+    if args.same_device:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
