@@ -50,10 +50,13 @@ CPZ_HD ge_niels ge_niels_identity() {
   return r;
 }
 
+// Operand roles: fe_mul(f, g) derives 2 f (odd limbs) and 19 g from its operands, so X and
+// Z are always the left operand and T and Y the right one -- the derived limbs of each
+// coordinate are then computed once and shared by the products that use it.
 CPZ_HD ge_p2 p1p1_to_p2(const ge_p1p1& p) {
   ge_p2 r;
   r.X = fe_mul(p.X, p.T);
-  r.Y = fe_mul(p.Y, p.Z);
+  r.Y = fe_mul(p.Z, p.Y);
   r.Z = fe_mul(p.Z, p.T);
   return r;
 }
@@ -61,7 +64,7 @@ CPZ_HD ge_p2 p1p1_to_p2(const ge_p1p1& p) {
 CPZ_HD ge_p3 p1p1_to_p3(const ge_p1p1& p) {
   ge_p3 r;
   r.X = fe_mul(p.X, p.T);
-  r.Y = fe_mul(p.Y, p.Z);
+  r.Y = fe_mul(p.Z, p.Y);
   r.Z = fe_mul(p.Z, p.T);
   r.T = fe_mul(p.X, p.Y);
   return r;
