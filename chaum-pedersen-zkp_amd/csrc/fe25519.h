@@ -468,4 +468,28 @@ CPZ_HD bool fe_sqrt_ratio_m1(fe& out, const fe& u, const fe& v) {
   return correct || flipped;
 }
 
+// SQRT_RATIO_M1(1, v): the only form ristretto decode and encode use.  With u = 1 the
+// products by u vanish and the three comparisons of `check` (with 1, -1 and -sqrt(-1))
+// share one canonicalisation against constant words.
+CPZ_HD bool fe_invsqrt_m1(fe& out, const fe& v) {
+  const fe v3 = fe_mul(fe_sq(v), v);
+  const fe v7 = fe_mul(fe_sq(v3), v);
+  fe r = fe_mul(v3, fe_pow22523(v7));
+  uint32_t w[8];
+  fe_towords(w, fe_mul(v, fe_sq(r)));
+  const uint32_t kNegSqrtM1[8] = {0xb5f15f3du, 0x3b11e4d8u, 0x52d01b87u, 0xd0bce7f9u,
+                                  0xc2042858u, 0xd4b2ff66u, 0xb03e20f4u, 0x547cdb7fu};
+  uint32_t d_one = w[0] ^ 1u, d_neg = w[0] ^ 0xffffffecu, d_negi = w[0] ^ kNegSqrtM1[0];
+#pragma unroll
+  for (int k = 1; k < 8; k++) {
+    d_one |= w[k];
+    d_neg |= w[k] ^ (k == 7 ? 0x7fffffffu : 0xffffffffu);
+    d_negi |= w[k] ^ kNegSqrtM1[k];
+  }
+  const bool correct = d_one == 0, flipped = d_neg == 0, flipped_i = d_negi == 0;
+  r = fe_select(r, fe_mul(r, FE_SQRT_M1()), flipped || flipped_i);
+  out = fe_abs(r);
+  return correct || flipped;
+}
+
 }  // namespace cpz

@@ -196,7 +196,7 @@ CPZ_HD bool ristretto_decode(ge_p3& out, const uint32_t w[8]) {
   const fe u2_sqr = fe_sq(u2);
   const fe v = fe_sub(fe_neg(fe_mul(FE_D(), fe_sq(u1))), u2_sqr);
   fe invsqrt;
-  const bool was_square = fe_sqrt_ratio_m1(invsqrt, fe_one(), fe_mul(v, u2_sqr));
+  const bool was_square = fe_invsqrt_m1(invsqrt, fe_mul(v, u2_sqr));
   const fe den_x = fe_mul(invsqrt, u2);
   const fe den_y = fe_mul(fe_mul(invsqrt, den_x), v);
   const fe x = fe_abs(fe_mul(s, fe_add(den_x, den_x)));  // s limbs are < 2^26: double den_x
@@ -214,7 +214,7 @@ CPZ_HD void ristretto_encode(uint32_t w[8], const ge_p3& p) {
   const fe u1 = fe_mul(fe_add(p.Z, p.Y), fe_sub(p.Z, p.Y));
   const fe u2 = fe_mul(p.X, p.Y);
   fe invsqrt;
-  fe_sqrt_ratio_m1(invsqrt, fe_one(), fe_mul(u1, fe_sq(u2)));
+  fe_invsqrt_m1(invsqrt, fe_mul(u1, fe_sq(u2)));
   const fe den1 = fe_mul(invsqrt, u1);
   const fe den2 = fe_mul(invsqrt, u2);
   const fe z_inv = fe_mul(fe_mul(den1, den2), p.T);
