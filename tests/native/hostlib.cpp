@@ -101,6 +101,12 @@ int cpzt_fe_sqrt_ratio(uint8_t* out, const uint8_t* u, const uint8_t* v) {
   fe_out(out, r);
   return sq ? 1 : 0;
 }
+int cpzt_fe_invsqrt_m1(uint8_t* out, const uint8_t* v) {
+  fe r;
+  const bool sq = fe_invsqrt_m1(r, fe_from(v));
+  fe_out(out, r);
+  return sq ? 1 : 0;
+}
 
 // Decode then re-encode: returns 1 and writes the re-encoding when `in` decodes.
 int cpzt_decode_encode(uint8_t* out, const uint8_t* in) {

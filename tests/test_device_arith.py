@@ -76,6 +76,16 @@ def test_invert_pow_sqrt_ratio(lib):
     assert lib.cpzt_fe_sqrt_ratio(out, fb(3), fb(0)) == 0 and fi(out.raw) == 0
 
 
+def test_invsqrt_m1(lib):
+    # fe_invsqrt_m1 (decode / encode) is SQRT_RATIO_M1(1, v): all four values of v r^2
+    # (1, -1, sqrt(-1), -sqrt(-1)) occur for random v; v = 0, 1, -1 and p - 1 as edges.
+    rnd = random.Random(3)
+    out = buf()
+    for v in [0, 1, P - 1, 2, 5] + [rnd.randrange(1, P) for _ in range(60)]:
+        sq = lib.cpzt_fe_invsqrt_m1(out, fb(v))
+        assert (bool(sq), fi(out.raw)) == O.sqrt_ratio_m1(1, v), v
+
+
 def test_ristretto_decode_encode(lib, golden):
     rnd = random.Random(3)
     out = buf()
