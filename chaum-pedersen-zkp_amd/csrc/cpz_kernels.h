@@ -80,7 +80,7 @@ struct VerifyArgs {
   const uint32_t* c;
   uint8_t* status;               // in: response-scalar status; out: final status
   const ge_niels* comb;          // fixed-base combs of g then h, kCombPerBase entries each
-  ge_cached* scratch;            // grid * kVerifyBlock * kCachedEntries entries
+  char* scratch;                 // table slab: grid * kVerifyBlock threads x kCachedEntries ge_cached
 };
 
 struct ProveArgs {
@@ -106,7 +106,6 @@ hipError_t launch_parse_proofs(const ParseArgs& a, hipStream_t st);
 // Fixed-base combs of 2 bases (g, h): bases_scratch holds 2 * kCombWindows ge_p3.
 hipError_t launch_build_comb(const uint32_t* gh_words, ge_p3* bases_scratch, ge_niels* comb, hipStream_t st);
 hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st);
-hipError_t launch_verify_each_queue(const VerifyArgs& a, int grid, unsigned* work, hipStream_t st);
 int verify_each_blocks_per_cu();  // resident k_verify_each blocks per CU (occupancy API)
 hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st);
 hipError_t launch_prove_response(const ProveArgs& a, hipStream_t st);

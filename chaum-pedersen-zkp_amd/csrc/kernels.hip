@@ -318,44 +318,26 @@ __global__ void __launch_bounds__(256) k_parse_proofs(ParseArgs a) {
 #define CPZ_VERIFY_WAVES 2  // waves per SIMD (256 VGPRs each)
 #endif
 __device__ __forceinline__ void verify_one_row(const VerifyArgs& a, int64_t i, const CombTable& comb_g,
-                                               const CombTable& comb_h, ge_cached* tab_v) {
+                                               const CombTable& comb_h, const SlabTable& tab, uint32_t* dig) {
   // Rows are read where they are consumed (decode just before each equation) so only one
   // decoded point is live at a time.
   uint32_t sw[8], cw[8];
   load_words8(sw, a.s, i);
   load_words8(cw, a.c, i);
   a.status[i] = verify_proof(a.y1 + 8 * i, a.y2 + 8 * i, a.r1 + 8 * i, a.r2 + 8 * i, sw, cw, a.status[i], comb_g,
-                             comb_h, tab_v);
+                             comb_h, tab, dig, kVerifyBlock);
 }
 
 __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each(VerifyArgs a) {
   const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
   const int64_t gtid = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * kVerifyBlock;
-  ge_cached* tab_v = a.scratch + gtid * kCachedEntries;
-  for (int64_t i = gtid; i < a.n; i += stride) verify_one_row(a, i, comb_g, comb_h, tab_v);
+  // this thread's tables: kCachedEntries entries, contiguous (scalarmul.h, SlabTable)
+  const SlabTable tab{a.scratch, (uint32_t)gtid * (uint32_t)(kCachedEntries * sizeof(ge_cached)), 16u};
+  // digit words in LDS, one column per thread (scalarmul.h, DigitRef)
+  __shared__ uint32_t dig[16 * kVerifyBlock];
+  for (int64_t i = gtid; i < a.n; i += stride) verify_one_row(a, i, comb_g, comb_h, tab, dig + threadIdx.x);
 }
-
-#if defined(CPZ_VERIFY_DYNAMIC)
-// Work-queue form (rejected experiment, built only with -DCPZ_VERIFY_DYNAMIC): one launch
-// over the whole batch in which each wave takes the next 64 proofs from a global counter (one
-// vector-memory atomic per wave) until the batch is exhausted, so every wave exits once the
-// counter passes n.  Measured 21.2 ms per 2^20 against 19.6 ms for the two-stream launches.
-__global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each_queue(VerifyArgs a, unsigned* work) {
-  const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
-  const int64_t gtid = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
-  ge_cached* tab_v = a.scratch + gtid * kCachedEntries;
-  const int lane = threadIdx.x & 63;
-  for (;;) {
-    unsigned base = 0;
-    if (lane == 0) base = atomicAdd(work, 64u);
-    base = (unsigned)__shfl((int)base, 0, 64);
-    if ((int64_t)base >= a.n) break;
-    const int64_t i = (int64_t)base + lane;
-    if (i < a.n) verify_one_row(a, i, comb_g, comb_h, tab_v);
-  }
-}
-#endif
 
 // ---------------------------------------------------------------------------------------
 // Synthetic prover (input generator): x_i, k_i = wide(ChaCha20(seed_x / seed_k, block i)).
@@ -454,15 +436,6 @@ hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st) {
   return hipGetLastError();
 }
 
-#if defined(CPZ_VERIFY_DYNAMIC)
-hipError_t launch_verify_each_queue(const VerifyArgs& a, int grid, unsigned* work, hipStream_t st) {
-  if (a.n <= 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned), st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_verify_each_queue, dim3(grid), dim3(kVerifyBlock), 0, st, a, work);
-  return hipGetLastError();
-}
-#endif
 
 hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;

@@ -97,8 +97,7 @@ struct cpz_ctx {
   // work buffers
   DevBuf c;         // n x 32
   DevBuf st;        // n
-  DevBuf scratch;   // grid x 256 x 8 ge_cached
-  DevBuf work;      // work-queue counter (CPZ_VERIFY_DYNAMIC)
+  DevBuf scratch;   // per-stream table slabs (kCachedEntries ge_cached per thread)
   // host-API staging
   DevBuf in[5];
   DevBuf ctxb, ctxo, ctxp;
@@ -272,28 +271,14 @@ int join_verify_streams(cpz_ctx* ctx, hipStream_t st) {
 int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hipStream_t st, VerifyRR* rr,
                          bool join, const cpz::ChallengeArgs* ca = nullptr) {
   static_assert(CPZ_VERIFY_STREAMS >= 1 && CPZ_VERIFY_STREAMS <= 4, "1..4 verify streams");
-#if defined(CPZ_VERIFY_DYNAMIC)
-  if (va.n < (int64_t)1 << 31) {
-    const int g = verify_grid(ctx, (size_t)va.n);
-    CPZ_HIP(ctx->scratch.ensure((size_t)g * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached)));
-    CPZ_HIP(ctx->work.ensure(64));
-    cpz::VerifyArgs v = va;
-    v.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p);
-    StageTimer t(ctx, stage, st);
-    CPZ_HIP(cpz::launch_verify_each_queue(v, g, static_cast<unsigned*>(ctx->work.p), st));
-    (void)rr;
-    (void)join;
-    return CPZ_OK;
-  }
-#endif
   const int full = (occupancy_grid(ctx) + CPZ_VERIFY_CHUNK_DIV - 1) / CPZ_VERIFY_CHUNK_DIV;
   const int grid = std::min(full, verify_grid(ctx, (size_t)va.n));
   // every stream owns a full-size slab at a fixed offset, whatever this call's grid
-  const size_t slab = (size_t)full * cpz::kVerifyBlock * cpz::kCachedEntries;
+  const size_t slab = (size_t)full * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached);
   const int64_t per = (int64_t)grid * cpz::kVerifyBlock;
   const int64_t chunks = (va.n + per - 1) / per;
   const int nst = rr ? CPZ_VERIFY_STREAMS : (int)std::min<int64_t>(CPZ_VERIFY_STREAMS, chunks);
-  CPZ_HIP(ctx->scratch.ensure((size_t)CPZ_VERIFY_STREAMS * slab * sizeof(cpz::ge_cached)));
+  CPZ_HIP(ctx->scratch.ensure((size_t)CPZ_VERIFY_STREAMS * slab));
   if (nst > 1) {
     if (!ctx->aux_start) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_start, hipEventDisableTiming));
     CPZ_HIP(hipEventRecord(ctx->aux_start, st));  // the aux streams start after st's prior work
@@ -315,7 +300,7 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
     v.c = va.c + 8 * a;
     v.status = va.status + a;
     const int k = (int)((rr ? rr->next++ : c) % nst);  // stream k owns scratch slab k
-    v.scratch = static_cast<cpz::ge_cached*>(ctx->scratch.p) + (size_t)k * slab;
+    v.scratch = static_cast<char*>(ctx->scratch.p) + (size_t)k * slab;
     hipStream_t sc = k == 0 ? st : ctx->aux_stream[k - 1];
     if (ca) {
       cpz::ChallengeArgs cc = *ca;
@@ -913,7 +898,6 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->c.release();
   ctx->st.release();
   ctx->scratch.release();
-  ctx->work.release();
   for (auto& b : ctx->in) b.release();
   ctx->ctxb.release();
   ctx->ctxo.release();

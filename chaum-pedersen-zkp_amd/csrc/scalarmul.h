@@ -12,6 +12,11 @@
 
 namespace cpz {
 
+// Issue a window's two table loads before its four doublings (1) or at their additions (0).
+#ifndef CPZ_TABLE_PREFETCH
+#define CPZ_TABLE_PREFETCH 1
+#endif
+
 constexpr int kTableV = 8;     // cached multiples 1..8 of a variable base (radix-16 digits)
 constexpr int kTableSlots = kTableV + 1;  // + the identity at slot 0 (digit 0 needs no select)
 constexpr int kTableB = 128;   // Niels multiples 1..128 of a fixed base (radix-256 digits)
@@ -42,29 +47,64 @@ struct CombTable {
   }
 };
 
-CPZ_HD ge_cached cached_load(const ge_cached* p) {
-  ge_cached r;
-#if defined(__HIP_DEVICE_COMPILE__)
-  const uint4* s = reinterpret_cast<const uint4*>(p);
-  uint4* d = reinterpret_cast<uint4*>(&r);
-#pragma unroll
-  for (int v = 0; v < (int)(sizeof(ge_cached) / 16); v++) d[v] = s[v];
-#else
-  r = *p;
-#endif
-  return r;
-}
+// Per-proof table of cached points (tab[0] = identity, tab[k] = k P), addressed as a base
+// pointer plus 32-bit byte offsets: 16-byte vector v of entry e at col + (e * kCachedVecs + v)
+// * stride.  The verify kernel keeps each thread's entries contiguous (stride 16, col = the
+// thread's slab slot).  Measured against two interleaved layouts in which one wave-wide load
+// of a vector reads 1 KiB of consecutive slots (lane-interleaved over the whole slab, and
+// wave-interleaved: 64 lanes per 184 KB region): 48.0 M and 48.2 M against 51.8 M proofs/s for
+// the contiguous form (same gpurun call, two passes each) -- a lane's 9 entries in one 1.4 KB
+// run beat full-line wave accesses spread over 10 separate 1-KiB rows per lookup.
+constexpr int kCachedVecs = (int)(sizeof(ge_cached) / 16);
 
-CPZ_HD void cached_store(ge_cached* p, const ge_cached& c) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const uint4* s = reinterpret_cast<const uint4*>(&c);
-  uint4* d = reinterpret_cast<uint4*>(p);
+struct SlabTable {
+  char* base;       // slab (wave-uniform)
+  uint32_t col;     // this thread's column (t * 16) + the table's first entry
+  uint32_t stride;  // bytes between consecutive vectors of one thread
+  CPZ_HDM uint32_t off(int e, int v) const { return col + ((uint32_t)e * (uint32_t)kCachedVecs + (uint32_t)v) * stride; }
+    // the table that starts e0 entries further on
+  CPZ_HDM SlabTable shifted(int e0) const { return SlabTable{base, off(e0, 0), stride}; }
+  CPZ_HDM ge_cached load(int e) const {
+    ge_cached r;
+    uint32_t* d = reinterpret_cast<uint32_t*>(&r);
 #pragma unroll
-  for (int v = 0; v < (int)(sizeof(ge_cached) / 16); v++) d[v] = s[v];
+    for (int v = 0; v < kCachedVecs; v++) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      const uint4 x = *reinterpret_cast<const uint4*>(base + off(e, v));
+      d[4 * v] = x.x; d[4 * v + 1] = x.y; d[4 * v + 2] = x.z; d[4 * v + 3] = x.w;
 #else
-  *p = c;
+      const uint32_t* s = reinterpret_cast<const uint32_t*>(base + off(e, v));
+      for (int k = 0; k < 4; k++) d[4 * v + k] = s[k];
 #endif
-}
+    }
+    return r;
+  }
+  CPZ_HDM void store(int e, const ge_cached& c) const {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(&c);
+#pragma unroll
+    for (int v = 0; v < kCachedVecs; v++) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      *reinterpret_cast<uint4*>(base + off(e, v)) = make_uint4(s[4 * v], s[4 * v + 1], s[4 * v + 2], s[4 * v + 3]);
+#else
+      uint32_t* d = reinterpret_cast<uint32_t*>(base + off(e, v));
+      for (int k = 0; k < 4; k++) d[k] = s[4 * v + k];
+#endif
+    }
+  }
+};
+
+// Digit words of a scalar multiplication held outside the registers: word k at p[k * stride].
+// The verify kernel keeps them in LDS (one column per thread, conflict-free), which takes 16
+// words per proof out of the Straus loop's register budget; the host build uses a plain array.
+struct DigitRef {
+  const uint32_t* p;
+  int stride;
+  CPZ_HDM uint32_t operator[](int k) const { return p[k * stride]; }
+};
+CPZ_HD DigitRef host_digits(const uint32_t* a) { return DigitRef{a, 1}; }
+
+// A host array of cached points as a table (unit tests).
+CPZ_HD SlabTable host_table(ge_cached* p) { return SlabTable{reinterpret_cast<char*>(p), 0u, 16u}; }
 
 CPZ_HD ge_niels niels_lookup(const ge_niels* tab, int digit) {
   const int mag = digit < 0 ? -digit : digit;
@@ -74,9 +114,9 @@ CPZ_HD ge_niels niels_lookup(const ge_niels* tab, int digit) {
 }
 
 // tab[0] is the identity, tab[k] = k P: one load and a conditional negation.
-CPZ_HD ge_cached cached_lookup(const ge_cached* tab, int digit) {
+CPZ_HD ge_cached cached_lookup(const SlabTable& tab, int digit) {
   const int mag = digit < 0 ? -digit : digit;
-  return ge_cached_cneg(cached_load(tab + mag), digit < 0);
+  return ge_cached_cneg(tab.load(mag), digit < 0);
 }
 // Four doublings of a pending completed point.
 CPZ_HD ge_p1p1 dbl4(const ge_p1p1& cur) {
@@ -97,33 +137,33 @@ CPZ_HD ge_p1p1 p1p1_identity() {
 // cached addition).
 // (An unrolled 4-doubling / 3-addition schedule saves a few more multiplications but keeps
 // three extended points live and measured slower from the extra spills.)
-CPZ_HD void build_cached_table(ge_cached* tab, const ge_p3& P) {
+CPZ_HD void build_cached_table(const SlabTable& tab, const ge_p3& P) {
   ge_niels n1;
   n1.ypx = fe_add(P.Y, P.X);
   n1.ymx = fe_sub(P.Y, P.X);
   n1.xy2d = fe_mul(P.T, FE_D2());
-  cached_store(tab, ge_cached_identity());
+  tab.store(0, ge_cached_identity());
   {
     ge_cached c1;
     c1.YpX = n1.ypx;
     c1.YmX = n1.ymx;
     c1.Z = P.Z;
     c1.T2d = n1.xy2d;
-    cached_store(tab + 1, c1);
+    tab.store(1, c1);
   }
   ge_p3 acc = p1p1_to_p3(p3_dbl(P));
-  cached_store(tab + 2, p3_to_cached(acc));
+  tab.store(2, p3_to_cached(acc));
 #pragma unroll 1
   for (int k = 3; k <= kTableV; k++) {
     acc = p1p1_to_p3(ge_add_niels(acc, n1));
-    cached_store(tab + k, p3_to_cached(acc));
+    tab.store(k, p3_to_cached(acc));
   }
 }
 
 // Q = [s] B + [c] V.  tab_v: cached multiples 1..8 of V; tab_b: Niels multiples 1..128
 // of B; cdig: radix-16 signed digits of c; sdig: radix-256 signed digits of s.
 // 63 x 4 doublings, 64 cached additions, 32 Niels additions.
-CPZ_HD ge_p3 straus_vartime(const ge_cached* tab_v, const ge_niels* tab_b, const uint32_t cdig_in[8],
+CPZ_HD ge_p3 straus_vartime(const SlabTable& tab_v, const ge_niels* tab_b, const uint32_t cdig_in[8],
                             const uint32_t sdig_in[8]) {
   uint32_t cdig[8], sdig[8];
 #pragma unroll
@@ -151,16 +191,11 @@ CPZ_HD ge_p3 straus_vartime(const ge_cached* tab_v, const ge_niels* tab_b, const
 
 // Adds [s] B to a pending completed point through the comb (16 mixed additions).
 // sdig: 16 radix-2^16 signed digits (sc_recode_radix65536).
-template <class Comb>
-CPZ_HD ge_p1p1 comb_add(ge_p1p1 cur, const Comb& comb, const uint32_t sdig_in[8]) {
-  uint32_t sd[8];
-#pragma unroll
-  for (int j = 0; j < 8; j++) sd[j] = sdig_in[j];
+template <class Comb, class Dig>
+CPZ_HD ge_p1p1 comb_add(ge_p1p1 cur, const Comb& comb, const Dig& sd) {
 #pragma unroll 1
   for (int j = 0; j < 8; j++) {
-    const uint32_t w = sd[0];
-#pragma unroll
-    for (int t = 0; t < 7; t++) sd[t] = sd[t + 1];
+    const uint32_t w = sd[j];
     // (requesting both entries of the pair before the first addition measured 2 % slower:
     // 30 more live VGPRs)
 #pragma unroll
@@ -177,34 +212,29 @@ CPZ_HD ge_p1p1 comb_add(ge_p1p1 cur, const Comb& comb, const uint32_t sdig_in[8]
 // returned as a completed point (callers only test it for the identity).
 // tab_y / tab_r: cached multiples 1..8 of Y' / R'; udig, vdig: 32 radix-16 signed digits of
 // u, |v| < 6 * 2^124; sdig: 16 radix-2^16 signed digits of s' < 2^253.
-template <class Comb>
-CPZ_HD ge_p1p1 straus_half_comb(const ge_cached* tab_y, const ge_cached* tab_r, const Comb& comb,
-                              const uint32_t udig_in[4], const uint32_t vdig_in[4], const uint32_t sdig[8]) {
-  uint32_t ud[4], vd[4];
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    ud[j] = udig_in[j];
-    vd[j] = vdig_in[j];
-  }
+template <class Comb, class Dig>
+CPZ_HD ge_p1p1 straus_half_comb(const SlabTable& tab_y, const SlabTable& tab_r, const Comb& comb, const Dig& ud,
+                              const Dig& vd, const Dig& sdig) {
   ge_p1p1 cur = p1p1_identity();
 #pragma unroll 1
   for (int j = 3; j >= 0; j--) {
-    const uint32_t wu = ud[3], wv = vd[3];
-#pragma unroll
-    for (int t = 3; t > 0; t--) {
-      ud[t] = ud[t - 1];
-      vd[t] = vd[t - 1];
-    }
+    const uint32_t wu = ud[j], wv = vd[j];
 #pragma unroll 1
     for (int m = 7; m >= 0; m--) {
       const int du = ((int32_t)(wu << (28 - 4 * m))) >> 28;
       const int dv = ((int32_t)(wv << (28 - 4 * m))) >> 28;
+#if CPZ_TABLE_PREFETCH
       // both table loads issued before the four doublings, which hide their latency
       // (the tables live in the HBM-backed scratch slab; measured ~1 % faster)
       const ge_cached ey = cached_lookup(tab_y, du), er = cached_lookup(tab_r, dv);
       if (j != 3 || m != 7) cur = dbl4(cur);
       cur = ge_add_cached(p1p1_to_p3(cur), ey);
       cur = ge_add_cached(p1p1_to_p3(cur), er);
+#else
+      if (j != 3 || m != 7) cur = dbl4(cur);
+      cur = ge_add_cached(p1p1_to_p3(cur), cached_lookup(tab_y, du));
+      cur = ge_add_cached(p1p1_to_p3(cur), cached_lookup(tab_r, dv));
+#endif
     }
   }
   return comb_add(cur, comb, sdig);
@@ -213,7 +243,7 @@ CPZ_HD ge_p1p1 straus_half_comb(const ge_cached* tab_y, const ge_cached* tab_r, 
 // [s] B through the comb (prover path): 16 mixed additions.
 template <class Comb>
 CPZ_HD ge_p3 comb_mul(const Comb& comb, const uint32_t sdig[8]) {
-  return p1p1_to_p3(comb_add(p1p1_identity(), comb, sdig));
+  return p1p1_to_p3(comb_add(p1p1_identity(), comb, host_digits(sdig)));
 }
 
 // [s] B by Horner over radix-256 signed digits (prover path).

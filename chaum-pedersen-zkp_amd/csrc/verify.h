@@ -232,9 +232,9 @@ CPZ_HD bool challenge_masks_ctx32(uint32_t m[3][50], const uint32_t g[8], const 
 // [v s] B and [v s mod l] B differ by elements of E[4].)  [v s mod l] B comes from the
 // fixed-base comb of B (sdig: radix-2^16 digits).  Also reports whether Y and R decode
 // and whether R encodes the identity.
-template <class Comb>
-CPZ_HD bool check_equation(const uint32_t y[8], const uint32_t r[8], const uint32_t udig[4], const uint32_t vdig[4],
-                           bool vneg, const uint32_t sdig[8], const Comb& comb, ge_cached* tab_y, ge_cached* tab_r,
+template <class Comb, class Dig>
+CPZ_HD bool check_equation(const uint32_t y[8], const uint32_t r[8], const Dig& udig, const Dig& vdig, bool vneg,
+                           const Dig& sdig, const Comb& comb, const SlabTable& tab_y, const SlabTable& tab_r,
                            bool& decoded, bool& r_identity) {
   // One copy of the decode + table code for both points (a rolled loop): the kernel's
   // instruction footprint, not its arithmetic, is what the 64 KB instruction cache sees.
@@ -251,18 +251,19 @@ CPZ_EQ_LOOP
 
 // Full per-proof outcome given the challenge c (canonical) and the response status st_s.
 // comb_g / comb_h: fixed-base combs of g and h; tab_v: 2 * kTableSlots entries of per-proof
-// scratch.
+// scratch (the y table, then the r table); dig: 16 words of digit storage at stride dstride
+// (u: words 0-3, |v|: 4-7, v s mod l: 8-15).
 template <class Comb>
 CPZ_HD uint8_t verify_proof(const uint32_t y1[8], const uint32_t y2[8], const uint32_t r1[8], const uint32_t r2[8],
                             const uint32_t s[8], const uint32_t c[8], uint8_t st_s, const Comb& comb_g,
-                            const Comb& comb_h, ge_cached* tab_v) {
-  uint32_t udig[4], vdig[4], sdig[8];
+                            const Comb& comb_h, const SlabTable& tab_v, uint32_t* dig, int dstride) {
   bool vneg;
   {
-    uint32_t u[4], va[4];
+    uint32_t u[4], va[4], w[8];
     sc_half_split(c, u, va, vneg);
-    sc_recode_radix16_half(udig, u);
-    sc_recode_radix16_half(vdig, va);
+    sc_recode_radix16_half(w, u);
+    sc_recode_radix16_half(w + 4, va);
+    for (int k = 0; k < 8; k++) dig[k * dstride] = w[k];
     sc vs, ss;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
@@ -271,15 +272,17 @@ CPZ_HD uint8_t verify_proof(const uint32_t y1[8], const uint32_t y2[8], const ui
     }
     sc sp = sc_mul(vs, ss);
     if (vneg) sp = sc_neg(sp);
-    sc_recode_radix65536(sdig, sp.w);
+    sc_recode_radix65536(w, sp.w);
+    for (int k = 0; k < 8; k++) dig[(8 + k) * dstride] = w[k];
   }
+  const DigitRef udig{dig, dstride}, vdig{dig + 4 * dstride, dstride}, sdig{dig + 8 * dstride, dstride};
   // The two equations share one copy of the code too (rolled loop over e).
   bool dec = true, id = false, eq = true;
 CPZ_EQ_LOOP
   for (int e = 0; e < 2; e++) {
     bool d, r_id;
     eq = check_equation(e ? y2 : y1, e ? r2 : r1, udig, vdig, vneg, sdig, e ? comb_h : comb_g, tab_v,
-                        tab_v + kTableSlots, d, r_id) && eq;
+                        tab_v.shifted(kTableSlots), d, r_id) && eq;
     dec = dec && d;
     id = id || r_id;
   }

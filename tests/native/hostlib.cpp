@@ -156,12 +156,12 @@ int cpzt_straus(uint8_t* out, uint8_t* out_fixed, const uint8_t* base, const uin
   ge_p3 V;
   if (!ristretto_decode(V, w)) return 0;
   ge_cached tv[kTableSlots];
-  build_cached_table(tv, V);
+  build_cached_table(host_table(tv), V);
   words_from(sw, s);
   words_from(cw, c);
   sc_recode_radix256(sdig, sw);
   sc_recode_radix16(cdig, cw);
-  ristretto_encode(o, straus_vartime(tv, tab.data(), cdig, sdig));
+  ristretto_encode(o, straus_vartime(host_table(tv), tab.data(), cdig, sdig));
   bytes_from(out, o);
   ristretto_encode(o, fixed_base_mul(tab.data(), sdig));
   bytes_from(out_fixed, o);
@@ -253,9 +253,10 @@ int cpzt_verify_opcount(unsigned long long* mul, unsigned long long* sq, const u
   words_from(sw, s);
   words_from(cw, c);
   ge_cached tv[2 * kTableSlots];
+  uint32_t dig[16];
   unsigned long long m0, s0;
   cpzt_opcount(&m0, &s0);
-  const int st = verify_proof(a, b, cc, d, sw, cw, response_status(sw), gt.g, gt.h, tv);
+  const int st = verify_proof(a, b, cc, d, sw, cw, response_status(sw), gt.g, gt.h, host_table(tv), dig, 1);
   cpzt_opcount(mul, sq);
   return st;
 }
@@ -275,7 +276,8 @@ int cpzt_verify(const uint8_t* g, const uint8_t* h, const uint8_t* y1, const uin
   words_from(sw, s);
   words_from(cw, cb);
   ge_cached tv[2 * kTableSlots];
-  return verify_proof(a, b, c, d, sw, cw, response_status(sw), gt.g, gt.h, tv);
+  uint32_t dig[16];
+  return verify_proof(a, b, c, d, sw, cw, response_status(sw), gt.g, gt.h, host_table(tv), dig, 1);
 }
 
 // The fixed-schedule no-context challenge (k_challenge_noctx's arithmetic) from the prefix
