@@ -4,7 +4,13 @@ Mirrors the reference crate's public surface for the batch-verification path
 (kobby-pentangeli/chaum-pedersen-zkp: src/verifier/batch.rs, src/primitives/gadgets.rs)
 on top of the C ABI in include/cpz.h:
 
-    Parameters, Statement, Proof       gadgets.rs:25-489 (encodings kept as 32-byte strings)
+    Parameters, Statement, Proof       gadgets.rs:25-489 (encodings kept as 32-byte strings;
+                                       Proof.from_bytes runs the device parser, k_parse_proofs)
+    Transcript                         transcript.rs:25-72 (the optional context only)
+    Verifier                           verifier/mod.rs:42-172 (verify, verify_with_transcript,
+                                       verify_response)
+    Prover                             prover/mod.rs:25-132 (prove, prove_with_transcript,
+                                       commit, respond)
     BatchVerifier                      batch.rs:82-324 (same names, cap, errors, ordering)
     Gpu                                bulk / device-resident entry points (no 1000 cap)
 
@@ -21,17 +27,18 @@ import numpy as np
 
 from . import _native
 from ._native import (CpzError, STATUS_BAD_POINT, STATUS_BAD_SCALAR, STATUS_EQ_FAIL,
-                      STATUS_IDENTITY_OR_ZERO, STATUS_OK)
+                      STATUS_IDENTITY, STATUS_OK, STATUS_ZERO_S)
 
 __all__ = [
     "Error", "InvalidParams", "InvalidScalar", "InvalidGroupElement", "CpzError",
-    "Parameters", "Statement", "Proof", "BatchVerifier", "Gpu", "VerifyResult",
+    "Parameters", "Statement", "Proof", "BatchVerifier", "Gpu", "VerifyResult", "Transcript", "Verifier", "Prover",
     "MAX_BATCH_SIZE", "PROTOCOL_VERSION", "STATUS_OK", "STATUS_EQ_FAIL", "STATUS_BAD_POINT",
-    "STATUS_BAD_SCALAR", "STATUS_IDENTITY_OR_ZERO", "default_generators", "verify_each_multi", "verify_batch_multi",
+    "STATUS_BAD_SCALAR", "STATUS_IDENTITY", "STATUS_ZERO_S", "default_generators", "verify_each_multi", "verify_batch_multi",
 ]
 
 MAX_BATCH_SIZE = 1000          # batch.rs:48
 PROTOCOL_VERSION = 1           # gadgets.rs:12
+L = 2**252 + 27742317777372353535851937790883648493   # group order (ristretto.rs scalars)
 
 
 # --- error taxonomy (src/error.rs:5-17) -------------------------------------------------
@@ -55,7 +62,8 @@ _STATUS_ERR = {
     STATUS_EQ_FAIL: (InvalidParams, "Proof verification failed"),
     STATUS_BAD_POINT: (InvalidGroupElement, "Bytes do not represent a valid Ristretto point"),
     STATUS_BAD_SCALAR: (InvalidScalar, "Bytes do not represent a valid scalar"),
-    STATUS_IDENTITY_OR_ZERO: (InvalidParams, "Commitment contains identity element or response scalar is zero"),
+    STATUS_IDENTITY: (InvalidParams, "Commitment contains identity element"),
+    STATUS_ZERO_S: (InvalidParams, "Response scalar is zero"),
 }
 
 
@@ -140,6 +148,12 @@ class Statement:
         self.y1 = _b32(y1, "y1")
         self.y2 = _b32(y2, "y2")
 
+    @classmethod
+    def from_witness(cls, params: "Parameters", x, gpu: Optional["Gpu"] = None) -> "Statement":
+        """y1 = x g, y2 = x h (gadgets.rs:217-221), computed on the device (cpz_prove)."""
+        out = (gpu or _gpu()).prove([_scalar_bytes(x)], [_scalar_bytes(1)], params=params)
+        return cls(out["y1"][0].tobytes(), out["y2"][0].tobytes())
+
 
 class Proof:
     """Commitment (r1, r2) and response s (gadgets.rs:307-489)."""
@@ -160,34 +174,26 @@ class Proof:
         return bytes(out)
 
     @classmethod
-    def from_bytes(cls, b: bytes) -> "Proof":
-        """Structural checks of gadgets.rs:364-461 (version, lengths, truncation, trailing
-        bytes).  Whether r1/r2 decode, s is canonical/non-zero and r1/r2 are not the identity
-        is decided on the GPU and reported per entry by the verifiers (status 2/3/4)."""
-        b = bytes(b)
-        if len(b) < 1 + 4 + 1 + 4 + 1 + 4 + 1:
-            raise InvalidParams("Proof too small: %d bytes" % len(b))
-        if b[0] != PROTOCOL_VERSION:
-            raise InvalidParams("Unsupported proof version: %d" % b[0])
-        pos = 1
-        parts = []
-        for name, maxlen, err in (("r1", 4096, InvalidGroupElement), ("r2", 4096, InvalidGroupElement),
-                                  ("s", 512, InvalidScalar)):
-            if pos + 4 > len(b):
-                raise InvalidParams("Truncated proof: missing %s length" % name)
-            ln = struct.unpack(">I", b[pos:pos + 4])[0]
-            pos += 4
-            if ln == 0 or ln > maxlen:
-                raise InvalidParams("Invalid %s length: %d" % (name, ln))
-            if pos + ln > len(b):
-                raise InvalidParams("Truncated proof: incomplete %s data" % name)
-            if ln != 32:
-                raise err("Expected 32 bytes, got %d" % ln)
-            parts.append(b[pos:pos + ln])
-            pos += ln
-        if pos != len(b):
-            raise InvalidParams("Proof has %d trailing bytes" % (len(b) - pos))
-        return cls(*parts)
+    def from_bytes(cls, b: bytes, gpu: Optional["Gpu"] = None) -> "Proof":
+        """gadgets.rs:364-489, exactly: the blob goes through the device parser
+        (cpz_parse_proofs, one k_parse_proofs thread), which applies the reference's checks
+        in its order -- each field's structure, then its decode (element_from_bytes /
+        scalar_from_bytes), trailing bytes, identity commitment, zero s -- and the first
+        failing check raises the reference's error type and message."""
+        out = cls.from_bytes_many([b], gpu)[0]
+        if isinstance(out, Error):
+            raise out
+        return out
+
+    @classmethod
+    def from_bytes_many(cls, blobs: Sequence[bytes], gpu: Optional["Gpu"] = None) -> List:
+        """Proof::from_bytes for many blobs in one device pass: a Proof or the Error the
+        reference would return, per blob."""
+        if not blobs:
+            return []
+        r1, r2, s, codes, aux = (gpu or _gpu()).parse_proofs(blobs)
+        return [cls(r1[i].tobytes(), r2[i].tobytes(), s[i].tobytes()) if codes[i] == 0
+                else parse_error(int(codes[i]), int(aux[i])) for i in range(len(blobs))]
 
     def commitment(self):
         return self.r1, self.r2
@@ -228,6 +234,16 @@ def parse_error(code: int, aux: int = 0) -> Optional[Error]:
         return None
     cls, msg = PARSE_ERRORS[int(code)]
     return cls(msg.format(int(aux)))
+
+
+def _scalar_bytes(x) -> bytes:
+    """A scalar given as an int (taken mod l) or as 32 little-endian bytes."""
+    if isinstance(x, (bytes, bytearray, memoryview)):
+        b = bytes(x)
+        if len(b) != 32:
+            raise InvalidScalar("Expected 32 bytes, got %d" % len(b))
+        return b
+    return (int(x) % L).to_bytes(32, "little")
 
 
 def _rows(data, n: int, name: str) -> np.ndarray:
@@ -298,7 +314,7 @@ class Gpu:
         self.close()
 
     # -- per-kernel timing (HIP events on the launch stream) -------------------------------
-    STAGES = ("challenge", "verify_each", "rlc_prepare", "rlc_msm", "fallback", "verify_span", "s6", "s7")
+    STAGES = ("challenge", "verify_each", "rlc_prepare", "rlc_msm", "fallback", "verify_span", "prove", "s7")
 
     def set_timing(self, enable: bool) -> None:
         _native.check(self._lib.cpz_ctx_set_timing(self._h, 1 if enable else 0))
@@ -333,6 +349,42 @@ class Gpu:
             self._h, params.g, params.h, n, *[_ptr(a) for a in arrs], _ptr(blob), _ptr(off), _ptr(present),
             _ptr(out)))
         return out
+
+    def verify_response(self, y1, y2, r1, r2, s, c, params: Optional[Parameters] = None) -> np.ndarray:
+        """Status per proof with caller-supplied challenges c ((n, 32) canonical scalars):
+        Verifier::verify_response (verifier/mod.rs:144-171), cpz_verify_response."""
+        params = params or Parameters()
+        n = len(y1)
+        arrs = [_rows(a, n, nm) for a, nm in ((y1, "y1"), (y2, "y2"), (r1, "r1"), (r2, "r2"), (s, "s"), (c, "c"))]
+        out = np.empty(n, dtype=np.uint8)
+        _native.check(self._lib.cpz_verify_response(self._h, params.g, params.h, n, *[_ptr(a) for a in arrs],
+                                                    _ptr(out)))
+        return out
+
+    def prove(self, x, k, contexts=None, params: Optional[Parameters] = None):
+        """Proofs from caller witnesses x and nonces k (sequences of ints / 32-byte scalars, or
+        (n, 32) arrays): dict of (n, 32) arrays y1, y2, r1, r2, s (cpz_prove)."""
+        params = params or Parameters()
+        n = len(x)
+        xs = x if isinstance(x, np.ndarray) else np.frombuffer(b"".join(_scalar_bytes(v) for v in x), np.uint8)
+        ks = k if isinstance(k, np.ndarray) else np.frombuffer(b"".join(_scalar_bytes(v) for v in k), np.uint8)
+        xs, ks = _rows(xs, n, "x"), _rows(ks, n, "k")
+        outs = {q: np.empty((n, 32), dtype=np.uint8) for q in ("y1", "y2", "r1", "r2", "s")}
+        blob, off, present = _ctx_arrays(contexts, n)
+        _native.check(self._lib.cpz_prove(self._h, params.g, params.h, n, _ptr(xs), _ptr(ks), _ptr(blob), _ptr(off),
+                                          _ptr(present), *[_ptr(outs[q]) for q in ("y1", "y2", "r1", "r2", "s")]))
+        return outs
+
+    def decode_points(self, points):
+        """Bulk element_from_bytes + element_to_bytes (cpz_decode_points): (ok uint8[n],
+        re-encodings uint8[n, 32], zero where a point does not decode)."""
+        n = len(points)
+        arr = _rows(np.frombuffer(b"".join(bytes(p) for p in points), np.uint8) if not isinstance(points, np.ndarray)
+                    else points, n, "points")
+        ok = np.empty(n, dtype=np.uint8)
+        enc = np.empty((n, 32), dtype=np.uint8)
+        _native.check(self._lib.cpz_decode_points(self._h, n, _ptr(arr), _ptr(ok), _ptr(enc)))
+        return ok, enc
 
     def verify_batch(self, y1, y2, r1, r2, s, seed: bytes, first_index: int = 0, contexts=None,
                      params: Optional[Parameters] = None, statuses: bool = True):
@@ -429,6 +481,24 @@ class Gpu:
             self._h, params.g, params.h, n, dp(y1), dp(y2), dp(r1), dp(r2), dp(s), dp(ctx_bytes), dp(ctx_off),
             dp(ctx_present), dp(status_out), _torch_stream(stream)))
 
+    def verify_response_device(self, y1, y2, r1, r2, s, c, status_out, params: Optional[Parameters] = None,
+                               stream: Optional[int] = None) -> None:
+        """Enqueue verify_response of device tensors (uint8 (n, 32) rows, challenges c)."""
+        params = params or Parameters()
+        _native.check(self._lib.cpz_verify_response_device(
+            self._h, params.g, params.h, int(y1.shape[0]), y1.data_ptr(), y2.data_ptr(), r1.data_ptr(), r2.data_ptr(),
+            s.data_ptr(), c.data_ptr(), status_out.data_ptr(), _torch_stream(stream)))
+
+    def prove_device(self, x, k, y1, y2, r1, r2, s, params: Optional[Parameters] = None, stream: Optional[int] = None,
+                     ctx_bytes=None, ctx_off=None, ctx_present=None) -> None:
+        """Enqueue the prover on device tensors: witnesses x, nonces k ((n, 32) uint8) -> rows."""
+        params = params or Parameters()
+        dp = lambda t: None if t is None else t.data_ptr()
+        _native.check(self._lib.cpz_prove_device(
+            self._h, params.g, params.h, int(x.shape[0]), x.data_ptr(), k.data_ptr(), dp(ctx_bytes), dp(ctx_off),
+            dp(ctx_present), y1.data_ptr(), y2.data_ptr(), r1.data_ptr(), r2.data_ptr(), s.data_ptr(),
+            _torch_stream(stream)))
+
     def prove_synthetic_device(self, n: int, seed_x: bytes, seed_k: bytes, y1, y2, r1, r2, s, first_index: int = 0,
                                params: Optional[Parameters] = None, stream: Optional[int] = None,
                                ctx_bytes=None, ctx_off=None, ctx_present=None) -> None:
@@ -489,6 +559,97 @@ def _gpu() -> Gpu:
     if _default_gpu is None:
         _default_gpu = Gpu(0)
     return _default_gpu
+
+
+class Transcript:
+    """Mirror of `Transcript` (transcript.rs:25-72) as far as callers shape it: new() plus an
+    optional `append_context` (transcript.rs:42-44, once; the protocol appends parameters,
+    statement and commitment itself).  The sponge runs on the device."""
+
+    def __init__(self):
+        self.context: Optional[bytes] = None
+
+    @classmethod
+    def new(cls) -> "Transcript":
+        return cls()
+
+    def append_context(self, context: bytes) -> None:
+        if self.context is not None:
+            raise InvalidParams("the device transcript takes one context per proof")
+        self.context = bytes(context)
+
+
+def _raise_status(st: int) -> None:
+    if st != STATUS_OK:
+        raise VerifyResult(st).error()
+
+
+class Verifier:
+    """Mirror of `Verifier` (verifier/mod.rs:42-172): one statement, one proof at a time
+    (each call is a 1-entry device call; batches belong in BatchVerifier / Gpu)."""
+
+    def __init__(self, params: Parameters, statement: Statement, gpu: Optional[Gpu] = None):
+        self.params, self.statement, self._gpu = params, statement, gpu
+
+    def verify(self, proof: Proof) -> None:
+        """verifier/mod.rs:85-88: a fresh transcript."""
+        self.verify_with_transcript(proof, Transcript.new())
+
+    def verify_with_transcript(self, proof: Proof, transcript: Transcript) -> None:
+        """verifier/mod.rs:120-139; raises the reference's error, returns None on Ok(())."""
+        g = self._gpu or _gpu()
+        one = lambda b: np.frombuffer(b, np.uint8).reshape(1, 32)
+        st = g.verify_each(one(self.statement.y1), one(self.statement.y2), one(proof.r1), one(proof.r2),
+                           one(proof.s), contexts=[transcript.context], params=self.params)
+        _raise_status(int(st[0]))
+
+    def verify_response(self, challenge, proof: Proof) -> None:
+        """verifier/mod.rs:144-171: the caller's challenge (int mod l or 32 canonical bytes)."""
+        g = self._gpu or _gpu()
+        one = lambda b: np.frombuffer(b, np.uint8).reshape(1, 32)
+        st = g.verify_response(one(self.statement.y1), one(self.statement.y2), one(proof.r1), one(proof.r2),
+                               one(proof.s), one(_scalar_bytes(challenge)), params=self.params)
+        _raise_status(int(st[0]))
+
+
+class Prover:
+    """Mirror of `Prover` (prover/mod.rs:25-132) for one witness x; the point arithmetic
+    and the transcript run on the device (cpz_prove)."""
+
+    def __init__(self, params: Parameters, witness, gpu: Optional[Gpu] = None):
+        self.params, self._x, self._gpu = params, _scalar_bytes(witness), gpu
+
+    def statement(self) -> Statement:
+        return Statement.from_witness(self.params, self._x, self._gpu)
+
+    @staticmethod
+    def _random_nonce(rng=None) -> bytes:
+        import os
+        raw = rng.randbytes(64) if rng is not None else os.urandom(64)
+        return _scalar_bytes(int.from_bytes(raw, "little"))   # random_scalar: wide reduction
+
+    def prove(self, rng=None) -> Proof:
+        """prover/mod.rs:70-84: a fresh transcript."""
+        return self.prove_with_transcript(rng, Transcript.new())
+
+    def prove_with_transcript(self, rng, transcript: Transcript, nonce=None) -> Proof:
+        """prover/mod.rs:86-110 (commit, transcript challenge, respond); `nonce` fixes k."""
+        k = _scalar_bytes(nonce) if nonce is not None else self._random_nonce(rng)
+        out = (self._gpu or _gpu()).prove([self._x], [k], contexts=[transcript.context], params=self.params)
+        return Proof(out["r1"][0].tobytes(), out["r2"][0].tobytes(), out["s"][0].tobytes())
+
+    def commit(self, rng=None, nonce=None):
+        """prover/mod.rs:115-121: ((r1, r2), k) with r = (k g, k h)."""
+        k = _scalar_bytes(nonce) if nonce is not None else self._random_nonce(rng)
+        out = (self._gpu or _gpu()).prove([self._x], [k], params=self.params)
+        return (out["r1"][0].tobytes(), out["r2"][0].tobytes()), k
+
+    def respond(self, nonce, challenge) -> bytes:
+        """prover/mod.rs:126-131: s = k + c x (mod l), scalar arithmetic only."""
+        k = int.from_bytes(_scalar_bytes(nonce), "little")
+        c = int.from_bytes(_scalar_bytes(challenge), "little")
+        x = int.from_bytes(self._x, "little")
+        return ((k + c * x) % L).to_bytes(32, "little")
 
 
 class _Entry:

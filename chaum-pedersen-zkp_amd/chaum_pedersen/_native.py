@@ -23,7 +23,8 @@ STATUS_OK = 0
 STATUS_EQ_FAIL = 1
 STATUS_BAD_POINT = 2
 STATUS_BAD_SCALAR = 3
-STATUS_IDENTITY_OR_ZERO = 4
+STATUS_IDENTITY = 4
+STATUS_ZERO_S = 5
 
 EXPORTED = (
     "cpz_device_count", "cpz_ctx_create", "cpz_ctx_destroy", "cpz_last_error",
@@ -31,6 +32,7 @@ EXPORTED = (
     "cpz_prove_synthetic", "cpz_prove_synthetic_device", "cpz_ctx_set_timing", "cpz_ctx_stage_times",
     "cpz_verify_batch", "cpz_verify_batch_device", "cpz_combine_partials", "cpz_msm",
     "cpz_parse_proofs", "cpz_parse_proofs_device", "cpz_verify_each_multi", "cpz_verify_batch_multi",
+    "cpz_verify_response", "cpz_verify_response_device", "cpz_prove", "cpz_prove_device", "cpz_decode_points",
 )
 NUM_STAGES = 8
 
@@ -91,6 +93,16 @@ def _declare(lib):
     lib.cpz_parse_proofs_device.argtypes = [_p, ctypes.c_size_t, _p, _p, _p, _p, _p, _p, _p, _p]
     lib.cpz_combine_partials.restype = ctypes.c_int
     lib.cpz_combine_partials.argtypes = [_p, ctypes.c_size_t, _p, _p, ctypes.POINTER(ctypes.c_int)]
+    lib.cpz_verify_response.restype = ctypes.c_int
+    lib.cpz_verify_response.argtypes = [_p, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p]
+    lib.cpz_verify_response_device.restype = ctypes.c_int
+    lib.cpz_verify_response_device.argtypes = [_p, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p, _p]
+    lib.cpz_prove.restype = ctypes.c_int
+    lib.cpz_prove.argtypes = [_p, _p, _p, ctypes.c_size_t, _p, _p, _p, _p, _p] + [_p] * 5
+    lib.cpz_prove_device.restype = ctypes.c_int
+    lib.cpz_prove_device.argtypes = [_p, _p, _p, ctypes.c_size_t, _p, _p, _p, _p, _p] + [_p] * 5 + [_p]
+    lib.cpz_decode_points.restype = ctypes.c_int
+    lib.cpz_decode_points.argtypes = [_p, ctypes.c_size_t, _p, _p, _p]
     lib.cpz_prove_synthetic_device.restype = ctypes.c_int
     lib.cpz_prove_synthetic_device.argtypes = ([_p, _p, _p, ctypes.c_size_t, ctypes.c_uint64, _p, _p, _p, _p,
                                                 _p] + [_p] * 5 + [_p])

@@ -106,6 +106,8 @@ class MemoryState:
         self.clock = clock
 
     def register_user(self, user_id: str, y1: bytes, y2: bytes) -> None:
+        """state.rs:136-157 (the state's own checks only).  Requests go through `register`,
+        which validates the statement first as the handler does (service.rs:61-97)."""
         if user_id in self.users:
             raise InvalidParams("User '%s' already registered" % user_id)
         self.users[user_id] = (bytes(y1), bytes(y2))
@@ -132,6 +134,43 @@ class MemoryState:
                                 % (user_id, self.max_sessions_per_user))
         self.sessions[token] = user_id
         toks.append(token)
+
+
+MAX_STATEMENT_BYTES = 4096     # service.rs:78
+
+
+def register(state, user_id: str, y1: bytes, y2: bytes, gpu=None) -> None:
+    """The `register` handler (service.rs:61-131) minus rate limiting and metrics: user id
+    checks, sizes, element_from_bytes of y1 and y2 (on the device, cpz_decode_points),
+    identity statements rejected, then state.register_user.  Raises InvalidArgument with
+    the reference's status message (AlreadyExists for a taken id is InvalidArgument here,
+    with the reference's "Registration failed: ..." text)."""
+    msg = validate_user_id(user_id)
+    if msg:
+        raise InvalidArgument(msg)
+    y1, y2 = bytes(y1), bytes(y2)
+    if not y1 or not y2:
+        raise InvalidArgument("Empty y1 or y2 values")
+    if len(y1) > MAX_STATEMENT_BYTES or len(y2) > MAX_STATEMENT_BYTES:
+        raise InvalidArgument("y1 or y2 values too large")
+    from . import _gpu
+    pts = [p for p in (y1, y2) if len(p) == 32]
+    ok = (gpu or _gpu()).decode_points(pts)[0] if pts else []
+    j = 0
+    for name, v in (("y1", y1), ("y2", y2)):
+        if len(v) != 32:
+            raise InvalidArgument("Invalid %s: %s" % (name, error_display(
+                InvalidGroupElement("Expected 32 bytes, got %d" % len(v)))))
+        if not ok[j]:
+            raise InvalidArgument("Invalid %s: %s" % (name, error_display(
+                InvalidGroupElement("Bytes do not represent a valid Ristretto point"))))
+        j += 1
+    if y1 == bytes(32) or y2 == bytes(32):   # the identity's (only) encoding
+        raise InvalidArgument("Statement contains identity elements")
+    try:
+        state.register_user(user_id, y1, y2)
+    except Error as e:
+        raise InvalidArgument("Registration failed: %s" % error_display(e))
 
 
 def verify_proof_batch(state, user_ids: Sequence[str], challenge_ids: Sequence[bytes], proofs: Sequence[bytes],

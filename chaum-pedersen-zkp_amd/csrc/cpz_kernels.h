@@ -11,7 +11,8 @@ constexpr uint8_t kStatusOk = 0;
 constexpr uint8_t kStatusEqFail = 1;
 constexpr uint8_t kStatusBadPoint = 2;
 constexpr uint8_t kStatusBadScalar = 3;
-constexpr uint8_t kStatusIdentityOrZero = 4;
+constexpr uint8_t kStatusIdentity = 4;
+constexpr uint8_t kStatusZeroS = 5;
 
 constexpr int kNielsEntries = kTableB;   // radix-256 signed digits: |d| <= 128
 constexpr int kCachedEntries = 2 * kTableSlots;   // y and r tables (identity + 1..8): |d| <= 8
@@ -88,6 +89,8 @@ struct ProveArgs {
   uint64_t first_index;
   uint32_t seed_x[8];
   uint32_t seed_k[8];
+  const uint32_t* x_in;          // caller witnesses / nonces (n x 8 words, taken mod l), or null:
+  const uint32_t* k_in;          // derived from seed_x / seed_k (synthetic inputs)
   const ge_niels* comb;          // fixed-base combs of g then h
   uint32_t* y1;
   uint32_t* y2;
@@ -109,5 +112,10 @@ hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st);
 int verify_each_blocks_per_cu();  // resident k_verify_each blocks per CU (occupancy API)
 hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st);
 hipError_t launch_prove_response(const ProveArgs& a, hipStream_t st);
+// Bulk decode (+ re-encode when out != null) of n encodings.
+hipError_t launch_decode_encode(int64_t n, const uint32_t* pts, uint8_t* ok, uint32_t* out, hipStream_t st);
+// cpz_verify_response: response status of s and the caller's challenge (sanitised copy to c_out).
+hipError_t launch_response_prep(int64_t n, const uint32_t* s, const uint32_t* c_in, uint32_t* c_out, uint8_t* status,
+                                hipStream_t st);
 
 }  // namespace cpz

@@ -23,7 +23,7 @@
 //   k_prove_response     (prover/mod.rs:86-131) with ChaCha20-derived witnesses/nonces
 //
 // Status codes (uint8 per proof): 0 valid, 1 equation failed, 2 undecodable point,
-// 3 non-canonical s, 4 identity commitment or zero s.
+// 3 non-canonical s, 4 identity commitment, 5 zero s.
 #include <hip/hip_runtime.h>
 
 #include "cpz_kernels.h"
@@ -133,16 +133,17 @@ __global__ void __launch_bounds__(kChallengeBlock) k_challenge(ChallengeArgs a) 
   // Entries on a fixed schedule skip the LDS sponge: no context (k_challenge_noctx's tail)
   // or a 4-byte-aligned 32-byte context (the service's challenge ids).
   const bool fixed_noctx = !has_ctx && a.fast_noctx;
-  const bool fixed_ctx32 = has_ctx && a.fast_ctx32 && b1 - b0 == 32 && (b0 & 3) == 0;
+  // (the context's own address must be 4-byte aligned: the base pointer is the caller's)
+  const bool fixed_ctx32 = has_ctx && a.fast_ctx32 && b1 - b0 == 32 &&
+                           ((reinterpret_cast<uintptr_t>(a.ctx_bytes) + b0) & 3) == 0;
   sc c;
   if (fixed_noctx) {
     c = challenge_fixed(reinterpret_cast<const uint32_t*>(a.prefix[1].state), a.k1, a.k2, y1, y2, r1, r2);
   } else if (fixed_ctx32) {
     uint32_t cw[8];
-    const uint4* cp = reinterpret_cast<const uint4*>(a.ctx_bytes + b0);
-    const uint4 lo = cp[0], hi = cp[1];
-    cw[0] = lo.x; cw[1] = lo.y; cw[2] = lo.z; cw[3] = lo.w;
-    cw[4] = hi.x; cw[5] = hi.y; cw[6] = hi.z; cw[7] = hi.w;
+    const uint32_t* cp = reinterpret_cast<const uint32_t*>(a.ctx_bytes + b0);  // 4-byte aligned (above)
+#pragma unroll
+    for (int k = 0; k < 8; k++) cw[k] = cp[k];
     c = challenge_fixed_ctx32(reinterpret_cast<const uint32_t*>(a.prefix[0].state), a.c32, cw, y1, y2, r1, r2);
   } else {
     c = challenge_generic(a, lds, has_ctx, b0, b1, y1, y2, r1, r2);
@@ -348,6 +349,16 @@ __device__ __forceinline__ sc chacha_scalar(const uint32_t key[8], uint64_t coun
   return sc_reduce_wide(blk);
 }
 
+// Witness / nonce of proof i: the caller's scalar (mod l), or the synthetic ChaCha20 one.
+__device__ __forceinline__ sc prove_scalar(const uint32_t* in, const uint32_t seed[8], uint64_t idx, int64_t i) {
+  if (in == nullptr) return chacha_scalar(seed, idx);
+  uint32_t wide[16];
+  load_words8(wide, in, i);
+#pragma unroll
+  for (int k = 8; k < 16; k++) wide[k] = 0;
+  return sc_reduce_wide(wide);
+}
+
 __global__ void __launch_bounds__(kVerifyBlock, 2) k_prove_points(ProveArgs a) {
   const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
   const int64_t i = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
@@ -355,7 +366,7 @@ __global__ void __launch_bounds__(kVerifyBlock, 2) k_prove_points(ProveArgs a) {
   const uint64_t idx = a.first_index + (uint64_t)i;
   uint32_t d[8], w[8];
   {
-    const sc x = chacha_scalar(a.seed_x, idx);
+    const sc x = prove_scalar(a.x_in, a.seed_x, idx, i);
     sc_recode_radix65536(d, x.w);
   }
   ristretto_encode(w, comb_mul(comb_g, d));
@@ -363,7 +374,7 @@ __global__ void __launch_bounds__(kVerifyBlock, 2) k_prove_points(ProveArgs a) {
   ristretto_encode(w, comb_mul(comb_h, d));
   store_words8(a.y2, i, w);
   {
-    const sc k = chacha_scalar(a.seed_k, idx);
+    const sc k = prove_scalar(a.k_in, a.seed_k, idx, i);
     sc_recode_radix65536(d, k.w);
   }
   ristretto_encode(w, comb_mul(comb_g, d));
@@ -376,12 +387,62 @@ __global__ void k_prove_response(ProveArgs a) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
   const uint64_t idx = a.first_index + (uint64_t)i;
-  const sc x = chacha_scalar(a.seed_x, idx);
-  const sc k = chacha_scalar(a.seed_k, idx);
+  const sc x = prove_scalar(a.x_in, a.seed_x, idx, i);
+  const sc k = prove_scalar(a.k_in, a.seed_k, idx, i);
   sc c;
   load_words8(c.w, a.c, i);
   const sc s = sc_add(k, sc_mul(c, x));  // s = k + c x   (prover/mod.rs:126-131)
   store_words8(a.s_out, i, s.w);
+}
+
+// ---------------------------------------------------------------------------------------
+// Bulk element_from_bytes (ristretto.rs:120-138) + element_to_bytes (:141-143): ok[i] = 1 iff
+// point i decodes; out[i] = the encoding of the decoded point (equal to the input for every
+// valid encoding -- ristretto encodings are canonical), zero when it does not decode.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_decode_encode(int64_t n, const uint32_t* __restrict__ pts,
+                                                       uint8_t* __restrict__ ok, uint32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[8];
+  load_words8(w, pts, i);
+  ge_p3 P;
+  const bool dec = ristretto_decode(P, w);
+  ok[i] = dec ? 1 : 0;
+  if (out != nullptr) {
+    ristretto_encode(w, P);
+#pragma unroll
+    for (int k = 0; k < 8; k++) w[k] = dec ? w[k] : 0u;
+    store_words8(out, i, w);
+  }
+}
+
+hipError_t launch_decode_encode(int64_t n, const uint32_t* pts, uint8_t* ok, uint32_t* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_decode_encode, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, pts, ok, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// cpz_verify_response (Verifier::verify_response, verifier/mod.rs:144-171): the challenge is
+// the caller's, so there is no transcript; only the response checks and a canonical copy of
+// the challenge (a non-canonical one is reported, and zeroed so the split stays in range).
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_response_prep(int64_t n, const uint32_t* __restrict__ s,
+                                                       const uint32_t* __restrict__ c_in, uint32_t* __restrict__ c_out,
+                                                       uint8_t* __restrict__ status) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[8], c[8];
+  load_words8(w, s, i);
+  load_words8(c, c_in, i);
+  uint8_t st = response_status(w);
+  const bool c_ok = sc_is_canonical(c);
+  if (st == kStOk && !c_ok) st = kStBadChallenge;
+#pragma unroll
+  for (int k = 0; k < 8; k++) c[k] = c_ok ? c[k] : 0u;
+  store_words8(c_out, i, c);
+  status[i] = st;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -447,6 +508,13 @@ hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st) {
 hipError_t launch_parse_proofs(const ParseArgs& a, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_parse_proofs, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_response_prep(int64_t n, const uint32_t* s, const uint32_t* c_in, uint32_t* c_out, uint8_t* status,
+                                hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_response_prep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, s, c_in, c_out, status);
   return hipGetLastError();
 }
 

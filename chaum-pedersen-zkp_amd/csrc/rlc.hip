@@ -171,7 +171,8 @@ __global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_prepare(RlcPrepArgs a)
     uint8_t st;
     if (!ok) st = kStBadPoint;
     else if (st_s == kStBadScalar) st = kStBadScalar;
-    else if (ident || st_s == kStIdentityOrZero) st = kStIdentityOrZero;
+    else if (ident) st = kStIdentity;
+    else if (st_s == kStZeroS) st = kStZeroS;
     else st = kStOk;
     a.status[i] = st;
     if (st == kStOk) {

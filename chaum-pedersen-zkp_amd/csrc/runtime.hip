@@ -98,8 +98,8 @@ struct cpz_ctx {
   DevBuf c;         // n x 32
   DevBuf st;        // n
   DevBuf scratch;   // per-stream table slabs (kCachedEntries ge_cached per thread)
-  // host-API staging
-  DevBuf in[5];
+  // host-API staging (y1, y2, r1, r2, s, and challenges / witnesses / nonces)
+  DevBuf in[7];
   DevBuf ctxb, ctxo, ctxp;
   // host-buffer pipeline (cpz_verify_each): H2D copies of chunk j+1 on their own stream
   // while chunk j verifies on `stream`
@@ -116,6 +116,11 @@ struct cpz_ctx {
       rl_segw, rl_win,
       rl_partial, rl_flags, rl_parts;
   int64_t rl_cap = 0;  // proofs
+  // Completion of the last call's work on whatever stream it used: the *_device entry points
+  // return without synchronising, and their kernels read context buffers (comb, tab, prefix,
+  // c, scratch, RLC buffers) that the next call may rewrite on another stream.
+  hipEvent_t last_done = nullptr;
+  bool have_last = false;
   // optional per-kernel timing
   bool timing = false;
   struct Mark { int stage; hipEvent_t a, b; };
@@ -134,6 +139,21 @@ hipEvent_t take_event(cpz_ctx* ctx) {
   hipEvent_t e = nullptr;
   if (hipEventCreate(&e) != hipSuccess) return nullptr;
   return e;
+}
+
+// Order the work this call enqueues on `st` after everything the previous call enqueued on
+// its stream(s) (which may differ from `st`): the context's buffers are shared by all calls.
+int order_after_last(cpz_ctx* ctx, hipStream_t st) {
+  if (ctx->have_last) CPZ_HIP(hipStreamWaitEvent(st, ctx->last_done, 0));
+  return CPZ_OK;
+}
+
+// Mark the end of this call's work on `st` (every aux stream already joined into it).
+int record_last(cpz_ctx* ctx, hipStream_t st) {
+  if (!ctx->last_done) CPZ_HIP(hipEventCreateWithFlags(&ctx->last_done, hipEventDisableTiming));
+  CPZ_HIP(hipEventRecord(ctx->last_done, st));
+  ctx->have_last = true;
+  return CPZ_OK;
 }
 
 // RAII bracket: records events around one kernel launch on `st` when timing is enabled.
@@ -170,6 +190,8 @@ int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32]) {
   if (std::memcmp(g, zero, 32) == 0 || std::memcmp(h, zero, 32) == 0)
     return fail(CPZ_EGENERATOR, "generator cannot be identity");
   if (std::memcmp(g, h, 32) == 0) return fail(CPZ_EGENERATOR, "generators g and h must be different");
+  // the tables are about to be rebuilt: no earlier call's kernels may still be reading them
+  if (ctx->have_last) CPZ_HIP(hipEventSynchronize(ctx->last_done));
   CPZ_HIP(ctx->tab.ensure(4 * cpz::kNielsEntries * sizeof(cpz::ge_niels)));  // g, h, 2^128 g, 2^128 h
   CPZ_HIP(ctx->prefix.ensure(2 * sizeof(cpz::StrobeSnap)));
   CPZ_HIP(ctx->gh_words.ensure(64));
@@ -665,6 +687,7 @@ int cpz_verify_batch(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], siz
   CPZ_HIP(hipSetDevice(ctx->device));
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
+  if ((rc = order_after_last(ctx, ctx->stream))) return rc;
   const uint8_t* host[5] = {y1, y2, r1, r2, s};
   const void* dev[5];
   const void* dcb;
@@ -693,9 +716,12 @@ int cpz_verify_batch_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[3
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  return verify_batch_impl(ctx, n, d_y1, d_y2, d_r1, d_r2, d_s, d_ctx_bytes, d_ctx_off, d_ctx_present,
-                           static_cast<uint8_t*>(d_status_out), seed, first_index, partial_out, batch_ok, fallback,
-                           nullptr, st);
+  if ((rc = order_after_last(ctx, st))) return rc;
+  rc = verify_batch_impl(ctx, n, d_y1, d_y2, d_r1, d_r2, d_s, d_ctx_bytes, d_ctx_off, d_ctx_present,
+                         static_cast<uint8_t*>(d_status_out), seed, first_index, partial_out, batch_ok, fallback,
+                         nullptr, st);
+  if (rc) return rc;
+  return record_last(ctx, st);
 }
 
 int cpz_msm(cpz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalars, uint8_t out[32]) {
@@ -709,6 +735,7 @@ int cpz_msm(cpz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalar
   cpz_default_generators(g, h);
   int rc = ctx->have_gh ? CPZ_OK : ensure_generators(ctx, g, h);
   if (rc) return rc;
+  if ((rc = order_after_last(ctx, ctx->stream))) return rc;
   const int64_t nproofs = (int64_t)(n + 3) / 4;
   rc = rlc_reserve(ctx, nproofs);
   if (rc) return rc;
@@ -736,10 +763,34 @@ int cpz_msm(cpz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalar
   return CPZ_OK;
 }
 
+int cpz_decode_points(cpz_ctx* ctx, size_t n, const uint8_t* points, uint8_t* ok_out, uint8_t* reencoded_out) {
+  if (!ctx || !points || !ok_out) return fail(CPZ_EINVAL, "null argument");
+  if (n == 0) return fail(CPZ_EEMPTY, "empty input");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  int rc = order_after_last(ctx, ctx->stream);
+  if (rc) return rc;
+  CPZ_HIP(ctx->in[0].ensure(n * 32));
+  CPZ_HIP(ctx->in[1].ensure(n * 32));
+  CPZ_HIP(ctx->st.ensure(n));
+  CPZ_HIP(hipMemcpyAsync(ctx->in[0].p, points, n * 32, hipMemcpyHostToDevice, ctx->stream));
+  CPZ_HIP(cpz::launch_decode_encode((int64_t)n, static_cast<const uint32_t*>(ctx->in[0].p),
+                                    static_cast<uint8_t*>(ctx->st.p),
+                                    reencoded_out ? static_cast<uint32_t*>(ctx->in[1].p) : nullptr, ctx->stream));
+  CPZ_HIP(hipMemcpyAsync(ok_out, ctx->st.p, n, hipMemcpyDeviceToHost, ctx->stream));
+  if (reencoded_out) CPZ_HIP(hipMemcpyAsync(reencoded_out, ctx->in[1].p, n * 32, hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipStreamSynchronize(ctx->stream));
+  return CPZ_OK;
+}
+
 int cpz_combine_partials(cpz_ctx* ctx, size_t k, const uint8_t* partials, uint8_t out[32], int* is_identity) {
   if (!ctx || !partials || !out || k == 0 || k > 4096) return fail(CPZ_EINVAL, "bad arguments");
   std::lock_guard<std::mutex> lock(ctx->mu);
   CPZ_HIP(hipSetDevice(ctx->device));
+  {
+    int rc = order_after_last(ctx, ctx->stream);  // rl_flags is shared with the batch path
+    if (rc) return rc;
+  }
   CPZ_HIP(ctx->rl_parts.ensure(k * 32 + 64));
   CPZ_HIP(ctx->rl_flags.ensure(4 * sizeof(int)));
   CPZ_HIP(hipMemcpyAsync(ctx->rl_parts.p, partials, k * 32, hipMemcpyHostToDevice, ctx->stream));
@@ -990,8 +1041,11 @@ int cpz_verify_each_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  return enqueue_verify(ctx, n, d_y1, d_y2, d_r1, d_r2, d_s, d_ctx_bytes, d_ctx_off, d_ctx_present,
-                        static_cast<uint8_t*>(d_status_out), st);
+  if ((rc = order_after_last(ctx, st))) return rc;
+  rc = enqueue_verify(ctx, n, d_y1, d_y2, d_r1, d_r2, d_s, d_ctx_bytes, d_ctx_off, d_ctx_present,
+                      static_cast<uint8_t*>(d_status_out), st);
+  if (rc) return rc;
+  return record_last(ctx, st);
 }
 
 int cpz_verify_each(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, const uint8_t* y1,
@@ -1006,6 +1060,7 @@ int cpz_verify_each(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size
   CPZ_HIP(hipSetDevice(ctx->device));
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
+  if ((rc = order_after_last(ctx, ctx->stream))) return rc;
   const uint8_t* host[5] = {y1, y2, r1, r2, s};
   if (n > kPipeChunk) return verify_each_pipelined(ctx, n, host, ctx_bytes, ctx_off, ctx_present, status_out);
   const void* dev[5];
@@ -1033,6 +1088,7 @@ int cpz_challenges(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_
   CPZ_HIP(hipSetDevice(ctx->device));
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
+  if ((rc = order_after_last(ctx, ctx->stream))) return rc;
   const uint8_t* host[5] = {y1, y2, r1, r2, nullptr};
   const void* dev[5];
   const void* dcb;
@@ -1126,26 +1182,28 @@ int cpz_parse_proofs(cpz_ctx* ctx, size_t n, const uint8_t* blob, const uint64_t
   return CPZ_OK;
 }
 
-int cpz_prove_synthetic_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
-                               uint64_t first_index, const uint8_t seed_x[32], const uint8_t seed_k[32],
-                               const void* d_ctx_bytes, const uint64_t* d_ctx_off, const uint8_t* d_ctx_present,
-                               void* d_y1, void* d_y2, void* d_r1, void* d_r2, void* d_s, void* stream) {
-  if (!ctx || !g || !h || !seed_x || !seed_k) return fail(CPZ_EINVAL, "null argument");
-  if (n == 0) return fail(CPZ_EEMPTY, "empty input");
-  if (!d_y1 || !d_y2 || !d_r1 || !d_r2 || !d_s) return fail(CPZ_EINVAL, "null output pointer");
-  if (!aligned16(d_y1) || !aligned16(d_y2) || !aligned16(d_r1) || !aligned16(d_r2) || !aligned16(d_s))
-    return fail(CPZ_EINVAL, "device outputs must be 16-byte aligned");
-  std::lock_guard<std::mutex> lock(ctx->mu);
-  CPZ_HIP(hipSetDevice(ctx->device));
-  int rc = ensure_generators(ctx, g, h);
-  if (rc) return rc;
-  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+}  // extern "C"
+
+namespace {
+
+// Prover::prove_with_transcript (prover/mod.rs:86-131) for n proofs on the device: x_i, k_i
+// from the caller (d_x / d_k, mod l) or, when those are null, from ChaCha20(seed, first_index
+// + i) (synthetic inputs).  y = x g, x h (gadgets.rs:217-221); r = k g, k h (commit,
+// :115-121); c from the transcript (contexts as in verify); s = k + c x (respond, :126-131).
+int prove_impl(cpz_ctx* ctx, size_t n, uint64_t first_index, const uint8_t* seed_x, const uint8_t* seed_k,
+               const void* d_x, const void* d_k, const void* d_ctx_bytes, const uint64_t* d_ctx_off,
+               const uint8_t* d_ctx_present, void* d_y1, void* d_y2, void* d_r1, void* d_r2, void* d_s,
+               hipStream_t st) {
   CPZ_HIP(ctx->c.ensure(n * 32));
   cpz::ProveArgs pa;
   pa.n = (int64_t)n;
   pa.first_index = first_index;
-  std::memcpy(pa.seed_x, seed_x, 32);
-  std::memcpy(pa.seed_k, seed_k, 32);
+  std::memset(pa.seed_x, 0, 32);
+  std::memset(pa.seed_k, 0, 32);
+  if (seed_x) std::memcpy(pa.seed_x, seed_x, 32);
+  if (seed_k) std::memcpy(pa.seed_k, seed_k, 32);
+  pa.x_in = static_cast<const uint32_t*>(d_x);
+  pa.k_in = static_cast<const uint32_t*>(d_k);
   pa.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
   pa.y1 = static_cast<uint32_t*>(d_y1);
   pa.y2 = static_cast<uint32_t*>(d_y2);
@@ -1153,7 +1211,10 @@ int cpz_prove_synthetic_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t 
   pa.r2 = static_cast<uint32_t*>(d_r2);
   pa.c = static_cast<const uint32_t*>(ctx->c.p);
   pa.s_out = static_cast<uint32_t*>(d_s);
-  CPZ_HIP(cpz::launch_prove_points(pa, st));
+  {
+    StageTimer t(ctx, 6, st);
+    CPZ_HIP(cpz::launch_prove_points(pa, st));
+  }
   cpz::ChallengeArgs ca;
   set_challenge_schedules(ctx, ca);
   ca.n = (int64_t)n;
@@ -1169,51 +1230,194 @@ int cpz_prove_synthetic_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t 
   ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->prefix.p);
   ca.c_out = static_cast<uint32_t*>(ctx->c.p);
   ca.status_out = nullptr;
+  StageTimer t(ctx, 6, st);
   CPZ_HIP(cpz::launch_challenge(ca, st));
   CPZ_HIP(cpz::launch_prove_response(pa, st));
   return CPZ_OK;
+}
+
+bool rows_aligned(const void* const* p, int k) {
+  for (int i = 0; i < k; i++)
+    if (!aligned16(p[i])) return false;
+  return true;
+}
+
+// Host-buffer prover: stage witnesses / nonces (or none) and contexts, prove on the device,
+// copy the five rows back.
+int prove_host(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, uint64_t first_index,
+               const uint8_t* seed_x, const uint8_t* seed_k, const uint8_t* x, const uint8_t* k,
+               const uint8_t* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present, uint8_t* y1, uint8_t* y2,
+               uint8_t* r1, uint8_t* r2, uint8_t* s) {
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  int rc = ensure_generators(ctx, g, h);
+  if (rc) return rc;
+  if ((rc = order_after_last(ctx, ctx->stream))) return rc;
+  const void* dcb = nullptr;
+  const uint64_t* dco = nullptr;
+  const uint8_t* dcp = nullptr;
+  const void* unused[5];
+  const uint8_t* none[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  rc = stage_inputs(ctx, n, none, 0, ctx_bytes, ctx_off, ctx_present, unused, &dcb, &dco, &dcp);
+  if (rc) return rc;
+  for (int q = 0; q < 5; q++) CPZ_HIP(ctx->in[q].ensure(n * 32));
+  const void* dx = nullptr;
+  const void* dk = nullptr;
+  if (x) {
+    CPZ_HIP(ctx->in[5].ensure(n * 32));
+    CPZ_HIP(ctx->in[6].ensure(n * 32));
+    CPZ_HIP(hipMemcpyAsync(ctx->in[5].p, x, n * 32, hipMemcpyHostToDevice, ctx->stream));
+    CPZ_HIP(hipMemcpyAsync(ctx->in[6].p, k, n * 32, hipMemcpyHostToDevice, ctx->stream));
+    dx = ctx->in[5].p;
+    dk = ctx->in[6].p;
+  }
+  rc = prove_impl(ctx, n, first_index, seed_x, seed_k, dx, dk, dcb, dco, dcp, ctx->in[0].p, ctx->in[1].p,
+                  ctx->in[2].p, ctx->in[3].p, ctx->in[4].p, ctx->stream);
+  if (rc) return rc;
+  uint8_t* outs[5] = {y1, y2, r1, r2, s};
+  for (int q = 0; q < 5; q++)
+    CPZ_HIP(hipMemcpyAsync(outs[q], ctx->in[q].p, n * 32, hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipStreamSynchronize(ctx->stream));
+  return CPZ_OK;
+}
+
+// Verifier::verify_response (verifier/mod.rs:144-171) with caller challenges c (device rows).
+int verify_response_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
+                         const void* s, const void* c, uint8_t* status, hipStream_t st) {
+  CPZ_HIP(ctx->c.ensure(n * 32));
+  CPZ_HIP(cpz::launch_response_prep((int64_t)n, static_cast<const uint32_t*>(s), static_cast<const uint32_t*>(c),
+                                    static_cast<uint32_t*>(ctx->c.p), status, st));
+  cpz::VerifyArgs va;
+  va.n = (int64_t)n;
+  va.y1 = static_cast<const uint32_t*>(y1);
+  va.y2 = static_cast<const uint32_t*>(y2);
+  va.r1 = static_cast<const uint32_t*>(r1);
+  va.r2 = static_cast<const uint32_t*>(r2);
+  va.s = static_cast<const uint32_t*>(s);
+  va.c = static_cast<const uint32_t*>(ctx->c.p);
+  va.status = status;
+  va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
+  va.scratch = nullptr;  // set per launch
+  StageTimer span(ctx, 5, st);
+  return launch_verify_chunks(ctx, va, 1, st, nullptr, true);
+}
+
+}  // namespace
+
+extern "C" {
+
+int cpz_prove_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, const void* d_x,
+                     const void* d_k, const void* d_ctx_bytes, const uint64_t* d_ctx_off, const uint8_t* d_ctx_present,
+                     void* d_y1, void* d_y2, void* d_r1, void* d_r2, void* d_s, void* stream) {
+  if (!ctx || !g || !h) return fail(CPZ_EINVAL, "null context or generators");
+  if (n == 0) return fail(CPZ_EEMPTY, "empty input");
+  const void* rows[7] = {d_x, d_k, d_y1, d_y2, d_r1, d_r2, d_s};
+  for (const void* p : rows)
+    if (!p) return fail(CPZ_EINVAL, "null input or output pointer");
+  if (!rows_aligned(rows, 7)) return fail(CPZ_EINVAL, "device rows must be 16-byte aligned");
+  if (d_ctx_off && !d_ctx_bytes) return fail(CPZ_EINVAL, "ctx_off given without ctx_bytes");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  int rc = ensure_generators(ctx, g, h);
+  if (rc) return rc;
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if ((rc = order_after_last(ctx, st))) return rc;
+  rc = prove_impl(ctx, n, 0, nullptr, nullptr, d_x, d_k, d_ctx_bytes, d_ctx_off, d_ctx_present, d_y1, d_y2, d_r1,
+                  d_r2, d_s, st);
+  if (rc) return rc;
+  return record_last(ctx, st);
+}
+
+int cpz_prove(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, const uint8_t* x, const uint8_t* k,
+              const uint8_t* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present, uint8_t* y1, uint8_t* y2,
+              uint8_t* r1, uint8_t* r2, uint8_t* s) {
+  if (!ctx || !g || !h) return fail(CPZ_EINVAL, "null context or generators");
+  if (n == 0) return fail(CPZ_EEMPTY, "empty input");
+  if (!x || !k || !y1 || !y2 || !r1 || !r2 || !s) return fail(CPZ_EINVAL, "null input or output pointer");
+  if (ctx_off && !ctx_bytes && ctx_off[n] != ctx_off[0]) return fail(CPZ_EINVAL, "ctx_off given without ctx_bytes");
+  return prove_host(ctx, g, h, n, 0, nullptr, nullptr, x, k, ctx_bytes, ctx_off, ctx_present, y1, y2, r1, r2, s);
+}
+
+int cpz_prove_synthetic_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                               uint64_t first_index, const uint8_t seed_x[32], const uint8_t seed_k[32],
+                               const void* d_ctx_bytes, const uint64_t* d_ctx_off, const uint8_t* d_ctx_present,
+                               void* d_y1, void* d_y2, void* d_r1, void* d_r2, void* d_s, void* stream) {
+  if (!ctx || !g || !h || !seed_x || !seed_k) return fail(CPZ_EINVAL, "null argument");
+  if (n == 0) return fail(CPZ_EEMPTY, "empty input");
+  if (!d_y1 || !d_y2 || !d_r1 || !d_r2 || !d_s) return fail(CPZ_EINVAL, "null output pointer");
+  const void* rows[5] = {d_y1, d_y2, d_r1, d_r2, d_s};
+  if (!rows_aligned(rows, 5)) return fail(CPZ_EINVAL, "device outputs must be 16-byte aligned");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  int rc = ensure_generators(ctx, g, h);
+  if (rc) return rc;
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if ((rc = order_after_last(ctx, st))) return rc;
+  rc = prove_impl(ctx, n, first_index, seed_x, seed_k, nullptr, nullptr, d_ctx_bytes, d_ctx_off, d_ctx_present, d_y1,
+                  d_y2, d_r1, d_r2, d_s, st);
+  if (rc) return rc;
+  return record_last(ctx, st);
 }
 
 int cpz_prove_synthetic(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, uint64_t first_index,
                         const uint8_t seed_x[32], const uint8_t seed_k[32], const uint8_t* ctx_bytes,
                         const uint64_t* ctx_off, const uint8_t* ctx_present, uint8_t* y1, uint8_t* y2,
                         uint8_t* r1, uint8_t* r2, uint8_t* s) {
-  if (!ctx) return fail(CPZ_EINVAL, "null context");
+  if (!ctx || !g || !h || !seed_x || !seed_k) return fail(CPZ_EINVAL, "null argument");
   if (n == 0) return fail(CPZ_EEMPTY, "empty input");
   if (!y1 || !y2 || !r1 || !r2 || !s) return fail(CPZ_EINVAL, "null output pointer");
-  void* outs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-  for (int k = 0; k < 5; k++) {
-    hipError_t e = hipMalloc(&outs[k], n * 32);
-    if (e != hipSuccess) {
-      for (int j = 0; j < k; j++) (void)hipFree(outs[j]);
-      return fail(CPZ_ENOMEM, "device allocation failed");
-    }
-  }
-  const void* dcb = nullptr;
-  const uint64_t* dco = nullptr;
-  const uint8_t* dcp = nullptr;
-  int rc = CPZ_OK;
-  {
-    std::lock_guard<std::mutex> lock(ctx->mu);
-    (void)hipSetDevice(ctx->device);
-    const uint8_t* host[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-    const void* dev[5];
-    rc = stage_inputs(ctx, n, host, 0, ctx_bytes, ctx_off, ctx_present, dev, &dcb, &dco, &dcp);
-  }
-  if (rc == CPZ_OK)
-    rc = cpz_prove_synthetic_device(ctx, g, h, n, first_index, seed_x, seed_k, dcb, dco, dcp, outs[0], outs[1],
-                                    outs[2], outs[3], outs[4], nullptr);
-  if (rc == CPZ_OK) {
-    uint8_t* hosts[5] = {y1, y2, r1, r2, s};
-    for (int k = 0; k < 5 && rc == CPZ_OK; k++) {
-      hipError_t e = hipMemcpyAsync(hosts[k], outs[k], n * 32, hipMemcpyDeviceToHost, ctx->stream);
-      if (e != hipSuccess) rc = fail(CPZ_EHIP, hipGetErrorString(e));
-    }
-    hipError_t e = hipStreamSynchronize(ctx->stream);
-    if (rc == CPZ_OK && e != hipSuccess) rc = fail(CPZ_EHIP, hipGetErrorString(e));
-  }
-  for (int k = 0; k < 5; k++) (void)hipFree(outs[k]);
-  return rc;
+  return prove_host(ctx, g, h, n, first_index, seed_x, seed_k, nullptr, nullptr, ctx_bytes, ctx_off, ctx_present, y1,
+                    y2, r1, r2, s);
+}
+
+int cpz_verify_response_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, const void* d_y1,
+                               const void* d_y2, const void* d_r1, const void* d_r2, const void* d_s, const void* d_c,
+                               void* d_status_out, void* stream) {
+  if (!ctx || !g || !h) return fail(CPZ_EINVAL, "null context or generators");
+  if (n == 0) return fail(CPZ_EEMPTY, "Cannot verify empty batch");
+  const void* rows[6] = {d_y1, d_y2, d_r1, d_r2, d_s, d_c};
+  for (const void* p : rows)
+    if (!p) return fail(CPZ_EINVAL, "null input pointer");
+  if (!d_status_out) return fail(CPZ_EINVAL, "null output pointer");
+  if (!rows_aligned(rows, 6)) return fail(CPZ_EINVAL, "device inputs must be 16-byte aligned");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  int rc = ensure_generators(ctx, g, h);
+  if (rc) return rc;
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if ((rc = order_after_last(ctx, st))) return rc;
+  rc = verify_response_impl(ctx, n, d_y1, d_y2, d_r1, d_r2, d_s, d_c, static_cast<uint8_t*>(d_status_out), st);
+  if (rc) return rc;
+  return record_last(ctx, st);
+}
+
+int cpz_verify_response(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, const uint8_t* y1,
+                        const uint8_t* y2, const uint8_t* r1, const uint8_t* r2, const uint8_t* s, const uint8_t* c,
+                        uint8_t* status_out) {
+  if (!ctx || !g || !h) return fail(CPZ_EINVAL, "null context or generators");
+  if (n == 0) return fail(CPZ_EEMPTY, "Cannot verify empty batch");
+  if (!y1 || !y2 || !r1 || !r2 || !s || !c || !status_out) return fail(CPZ_EINVAL, "null input pointer");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  int rc = ensure_generators(ctx, g, h);
+  if (rc) return rc;
+  if ((rc = order_after_last(ctx, ctx->stream))) return rc;
+  const uint8_t* host[5] = {y1, y2, r1, r2, s};
+  const void* dev[5];
+  const void* dcb;
+  const uint64_t* dco;
+  const uint8_t* dcp;
+  rc = stage_inputs(ctx, n, host, 5, nullptr, nullptr, nullptr, dev, &dcb, &dco, &dcp);
+  if (rc) return rc;
+  CPZ_HIP(ctx->in[5].ensure(n * 32));
+  CPZ_HIP(hipMemcpyAsync(ctx->in[5].p, c, n * 32, hipMemcpyHostToDevice, ctx->stream));
+  CPZ_HIP(ctx->st.ensure(n));
+  rc = verify_response_impl(ctx, n, dev[0], dev[1], dev[2], dev[3], dev[4], ctx->in[5].p,
+                            static_cast<uint8_t*>(ctx->st.p), ctx->stream);
+  if (rc) return rc;
+  CPZ_HIP(hipMemcpyAsync(status_out, ctx->st.p, n, hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipStreamSynchronize(ctx->stream));
+  return CPZ_OK;
 }
 
 }  // extern "C"

@@ -6,8 +6,9 @@
 //   1. statement / commitment points must decode     -> 2  (Statement built at
 //      registration, service.rs:82-86; Proof::from_bytes r1/r2, gadgets.rs:410, 437)
 //   2. s must be canonical                           -> 3  (gadgets.rs:460, ristretto.rs:94-112)
-//   3. r1, r2 not identity; s != 0                   -> 4  (gadgets.rs:474-482)
-//   4. g^s == r1 y1^c  and  h^s == r2 y2^c           -> 0 / 1 (batch.rs:216-228)
+//   3. r1, r2 not identity                           -> 4  (gadgets.rs:474-478)
+//   4. s != 0                                        -> 5  (gadgets.rs:480-482)
+//   5. g^s == r1 y1^c  and  h^s == r2 y2^c           -> 0 / 1 (batch.rs:216-228)
 #pragma once
 #include "ristretto.h"
 #include "scalar25519.h"
@@ -25,7 +26,11 @@
 
 namespace cpz {
 
-constexpr uint8_t kStOk = 0, kStEqFail = 1, kStBadPoint = 2, kStBadScalar = 3, kStIdentityOrZero = 4;
+constexpr uint8_t kStOk = 0, kStEqFail = 1, kStBadPoint = 2, kStBadScalar = 3, kStIdentity = 4, kStZeroS = 5;
+// Internal response status (never reported): the caller-supplied challenge of
+// cpz_verify_response is not canonical.  It reports kStBadScalar, but only after the entry's
+// own decode-level checks (pyoracle.verify_response).
+constexpr uint8_t kStBadChallenge = 0x80;
 
 CPZ_HD bool words8_zero(const uint32_t w[8]) {
   uint32_t acc = 0;
@@ -37,7 +42,7 @@ CPZ_HD bool words8_zero(const uint32_t w[8]) {
 // Status contributed by the response scalar alone.
 CPZ_HD uint8_t response_status(const uint32_t s[8]) {
   if (!sc_is_canonical(s)) return kStBadScalar;
-  if (sc_is_zero(s)) return kStIdentityOrZero;
+  if (sc_is_zero(s)) return kStZeroS;
   return kStOk;
 }
 
@@ -288,7 +293,9 @@ CPZ_EQ_LOOP
   }
   if (!dec) return kStBadPoint;
   if (st_s == kStBadScalar) return kStBadScalar;
-  if (id || st_s == kStIdentityOrZero) return kStIdentityOrZero;
+  if (id) return kStIdentity;
+  if (st_s == kStZeroS) return kStZeroS;
+  if (st_s == kStBadChallenge) return kStBadScalar;
   return eq ? kStOk : kStEqFail;
 }
 

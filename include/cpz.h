@@ -21,8 +21,10 @@
  *   CPZ_STATUS_EQ_FAIL          Err(InvalidParams("Proof verification failed"))  batch.rs:224-228
  *   CPZ_STATUS_BAD_POINT        a point fails to decode (InvalidGroupElement)    ristretto.rs:120-138
  *   CPZ_STATUS_BAD_SCALAR       s is not canonical (InvalidScalar)                ristretto.rs:94-112
- *   CPZ_STATUS_IDENTITY_OR_ZERO identity commitment or zero s (InvalidParams)     gadgets.rs:474-482
- * Codes 2-4 are rejected by the reference before an entry can reach the batch
+ *   CPZ_STATUS_IDENTITY         r1 or r2 is the identity (InvalidParams            gadgets.rs:474-478
+ *                               "Commitment contains identity element")
+ *   CPZ_STATUS_ZERO_S           s is zero (InvalidParams "Response scalar is zero")  gadgets.rs:480-482
+ * Codes 2-5 are rejected by the reference before an entry can reach the batch
  * (`Proof::from_bytes`, service.rs:501-507); the bulk path reports them per entry.
  */
 #ifndef CPZ_H_
@@ -46,7 +48,8 @@ extern "C" {
 #define CPZ_STATUS_EQ_FAIL 1
 #define CPZ_STATUS_BAD_POINT 2
 #define CPZ_STATUS_BAD_SCALAR 3
-#define CPZ_STATUS_IDENTITY_OR_ZERO 4
+#define CPZ_STATUS_IDENTITY 4
+#define CPZ_STATUS_ZERO_S 5
 
 typedef struct cpz_ctx cpz_ctx;
 
@@ -76,7 +79,9 @@ int cpz_verify_each(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size
 
 /* Same with device-resident, 16-byte aligned inputs/outputs, enqueued on `stream`
  * (a hipStream_t, or NULL for the context's own stream, which is a blocking stream and so
- * is ordered with the legacy default stream).  Does not synchronise. */
+ * is ordered with the legacy default stream).  Does not synchronise.  Any later call on the
+ * same context, on any stream, is ordered after this call's kernels (they read the context's
+ * cached tables and work buffers). */
 int cpz_verify_each_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
                            const void *d_y1, const void *d_y2, const void *d_r1, const void *d_r2,
                            const void *d_s, const void *d_ctx_bytes, const uint64_t *d_ctx_off,
@@ -88,6 +93,32 @@ int cpz_challenges(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_
                    const uint8_t *y1, const uint8_t *y2, const uint8_t *r1, const uint8_t *r2,
                    const uint8_t *ctx_bytes, const uint64_t *ctx_off, const uint8_t *ctx_present,
                    uint8_t *c_out);
+
+/* Per-proof verification with caller-supplied challenges c_i (32-byte little-endian scalars):
+ * Verifier::verify_response (verifier/mod.rs:144-171) -- g^s == r1 y1^c and h^s == r2 y2^c,
+ * no transcript.  status_out[i] as for cpz_verify_each: the entry's decode-level checks first
+ * (2, 3 for s, 4, 5), then CPZ_STATUS_BAD_SCALAR if c_i is not canonical (c_i >= l: what
+ * scalar_from_bytes would reject, ristretto.rs:94-112), then 0 / 1.  n == 0 -> CPZ_EEMPTY. */
+int cpz_verify_response(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                        const uint8_t *y1, const uint8_t *y2, const uint8_t *r1, const uint8_t *r2,
+                        const uint8_t *s, const uint8_t *c, uint8_t *status_out);
+int cpz_verify_response_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
+                               const void *d_y1, const void *d_y2, const void *d_r1, const void *d_r2,
+                               const void *d_s, const void *d_c, void *d_status_out, void *stream);
+
+/* Batch prover from caller witnesses x_i and nonces k_i (32-byte little-endian scalars, taken
+ * mod l): Prover::prove_with_transcript (prover/mod.rs:86-110) with commit's nonce supplied
+ * (commit :115-121, respond :126-131) and the statement from the witness (gadgets.rs:217-221):
+ *   y1 = x g, y2 = x h, r1 = k g, r2 = k h, c = the transcript challenge (optional per-proof
+ *   contexts as in cpz_verify_each, appended first as the service does), s = k + c x.
+ * Outputs are n x 32-byte encodings.  n == 0 -> CPZ_EEMPTY. */
+int cpz_prove(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n, const uint8_t *x,
+              const uint8_t *k, const uint8_t *ctx_bytes, const uint64_t *ctx_off, const uint8_t *ctx_present,
+              uint8_t *y1, uint8_t *y2, uint8_t *r1, uint8_t *r2, uint8_t *s);
+int cpz_prove_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n, const void *d_x,
+                     const void *d_k, const void *d_ctx_bytes, const uint64_t *d_ctx_off,
+                     const uint8_t *d_ctx_present, void *d_y1, void *d_y2, void *d_r1, void *d_r2, void *d_s,
+                     void *stream);
 
 /* Synthetic input generator (Prover::prove_with_transcript, prover/mod.rs:86-131):
  * witness x_i and nonce k_i = from_bytes_mod_order_wide(ChaCha20(seed_x / seed_k, block
@@ -129,6 +160,12 @@ int cpz_verify_batch_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[3
                             const uint8_t *d_ctx_present, const uint8_t seed[32], uint64_t first_index,
                             uint8_t partial_out[32], int *batch_ok, void *d_status_out, int fallback,
                             void *stream);
+
+/* Bulk Ristretto255::element_from_bytes (ristretto.rs:120-138) on the device: ok_out[i] = 1 iff
+ * the 32-byte encoding points[i] decodes (RFC 9496), and, when reencoded_out is not NULL, the
+ * element_to_bytes (ristretto.rs:141-143) encoding of the decoded point (32 zero bytes where
+ * it does not decode).  Statement registration (service.rs:82-86) and parity checks use it. */
+int cpz_decode_points(cpz_ctx *ctx, size_t n, const uint8_t *points, uint8_t *ok_out, uint8_t *reencoded_out);
 
 /* Multi-scalar multiplication through the same Pippenger kernels: out = enc(sum_j [k_j] P_j)
  * for n encoded points and n scalars (little-endian, < 2^253).  Exposed for testing the MSM
@@ -200,7 +237,8 @@ int cpz_verify_batch_multi(cpz_ctx *const *ctxs, int nctx, const uint8_t g[32], 
 /* Per-kernel timing (HIP events recorded on the launch stream around every kernel).
  * Stages: 0 = k_challenge, 1 = k_verify_each, 2 = RLC decode/weights, 3 = RLC MSM,
  * 4 = fallback, 5 = the whole per-proof verify of one call (first to last k_verify_each,
- * whose launches overlap on several streams).  cpz_ctx_stage_times synchronises, writes the summed milliseconds and
+ * whose launches overlap on several streams), 6 = prover (commitments / statements, then
+ * challenges + responses).  cpz_ctx_stage_times synchronises, writes the summed milliseconds and
  * launch counts per stage since the last call, and resets them. */
 #define CPZ_NUM_STAGES 8
 int cpz_ctx_set_timing(cpz_ctx *ctx, int enable);

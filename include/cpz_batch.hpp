@@ -8,6 +8,10 @@
 //   add / add_with_context               batch.rs:139-168  (cap MAX_BATCH_SIZE = 1000)
 //   verify()                             batch.rs:171-183  -> one Result per entry
 //   clear                                batch.rs:321-323
+//   Proof::to_bytes / Proof::from_bytes  gadgets.rs:343-489 (from_bytes on the device parser)
+//   Verifier: verify / verify_with_transcript / verify_response     verifier/mod.rs:42-172
+//   Prover: prove_with_transcript (caller nonce) / statement        prover/mod.rs:86-131,
+//                                                                    gadgets.rs:217-221
 //
 // Errors are returned, never thrown across the ABI; `Result` carries the reference's
 // error kind (src/error.rs:5-17).  Points and scalars stay as their 32-byte encodings:
@@ -49,8 +53,8 @@ inline Result status_result(uint8_t st) {
     case CPZ_STATUS_BAD_POINT:
       return Result::err(ErrorKind::InvalidGroupElement, "Bytes do not represent a valid Ristretto point");
     case CPZ_STATUS_BAD_SCALAR: return Result::err(ErrorKind::InvalidScalar, "Bytes do not represent a valid scalar");
-    default:
-      return Result::err(ErrorKind::InvalidParams, "Commitment contains identity element or response scalar is zero");
+    case CPZ_STATUS_IDENTITY: return Result::err(ErrorKind::InvalidParams, "Commitment contains identity element");
+    default: return Result::err(ErrorKind::InvalidParams, "Response scalar is zero");  // CPZ_STATUS_ZERO_S
   }
 }
 
@@ -67,7 +71,47 @@ struct Statement {  // gadgets.rs:177-239
 
 struct Proof {  // gadgets.rs:245-311
   Bytes32 r1, r2, s;
+
+  // gadgets.rs:343-361: [version 1][u32be 32][r1][u32be 32][r2][u32be 32][s] = 109 bytes.
+  std::vector<uint8_t> to_bytes() const {
+    std::vector<uint8_t> out{1};
+    for (const Bytes32* f : {&r1, &r2, &s}) {
+      const uint8_t len[4] = {0, 0, 0, 32};
+      out.insert(out.end(), len, len + 4);
+      out.insert(out.end(), f->begin(), f->end());
+    }
+    return out;
+  }
 };
+
+// The reference's error for a CPZ_PARSE_* code (gadgets.rs:364-489).
+inline Result parse_result(uint8_t code, uint32_t aux) {
+  const std::string a = std::to_string(aux);
+  switch (code) {
+    case CPZ_PARSE_OK: return Result::ok();
+    case CPZ_PARSE_TOO_SMALL: return Result::err(ErrorKind::InvalidParams, "Proof too small: " + a + " bytes");
+    case CPZ_PARSE_BAD_VERSION: return Result::err(ErrorKind::InvalidParams, "Unsupported proof version: " + a);
+    case CPZ_PARSE_R1_LEN_MISSING: return Result::err(ErrorKind::InvalidParams, "Truncated proof: missing r1 length");
+    case CPZ_PARSE_R1_LEN_INVALID: return Result::err(ErrorKind::InvalidParams, "Invalid r1 length: " + a);
+    case CPZ_PARSE_R1_TRUNCATED: return Result::err(ErrorKind::InvalidParams, "Truncated proof: incomplete r1 data");
+    case CPZ_PARSE_R2_LEN_MISSING: return Result::err(ErrorKind::InvalidParams, "Truncated proof: missing r2 length");
+    case CPZ_PARSE_R2_LEN_INVALID: return Result::err(ErrorKind::InvalidParams, "Invalid r2 length: " + a);
+    case CPZ_PARSE_R2_TRUNCATED: return Result::err(ErrorKind::InvalidParams, "Truncated proof: incomplete r2 data");
+    case CPZ_PARSE_R1_SIZE:
+    case CPZ_PARSE_R2_SIZE: return Result::err(ErrorKind::InvalidGroupElement, "Expected 32 bytes, got " + a);
+    case CPZ_PARSE_R1_POINT:
+    case CPZ_PARSE_R2_POINT:
+      return Result::err(ErrorKind::InvalidGroupElement, "Bytes do not represent a valid Ristretto point");
+    case CPZ_PARSE_S_LEN_MISSING: return Result::err(ErrorKind::InvalidParams, "Truncated proof: missing s length");
+    case CPZ_PARSE_S_LEN_INVALID: return Result::err(ErrorKind::InvalidParams, "Invalid s length: " + a);
+    case CPZ_PARSE_S_TRUNCATED: return Result::err(ErrorKind::InvalidParams, "Truncated proof: incomplete s data");
+    case CPZ_PARSE_S_SIZE: return Result::err(ErrorKind::InvalidScalar, "Expected 32 bytes, got " + a);
+    case CPZ_PARSE_S_SCALAR: return Result::err(ErrorKind::InvalidScalar, "Bytes do not represent a valid scalar");
+    case CPZ_PARSE_TRAILING: return Result::err(ErrorKind::InvalidParams, "Proof has " + a + " trailing bytes");
+    case CPZ_PARSE_IDENTITY: return Result::err(ErrorKind::InvalidParams, "Commitment contains identity element");
+    default: return Result::err(ErrorKind::InvalidParams, "Response scalar is zero");  // CPZ_PARSE_ZERO_S
+  }
+}
 
 // One GPU context; shareable by many BatchVerifiers on one thread.
 class Device {
@@ -82,6 +126,81 @@ class Device {
  private:
   cpz_ctx* ctx_ = nullptr;
   int rc_ = CPZ_EINVAL;
+};
+
+// Proof::from_bytes (gadgets.rs:364-489) through the device parser: the reference's checks
+// in its order (point decodes and canonical-scalar checks included), first failure wins.
+inline Result proof_from_bytes(Device& dev, const uint8_t* blob, std::size_t len, Proof* out) {
+  const uint64_t off[2] = {0, len};
+  Proof p;
+  uint8_t code = 0;
+  uint32_t aux = 0;
+  const uint8_t pad = 0;
+  const int rc = cpz_parse_proofs(dev.get(), 1, len ? blob : &pad, off, p.r1.data(), p.r2.data(), p.s.data(), &code,
+                                  &aux);
+  if (rc != CPZ_OK) return Result::err(ErrorKind::Device, cpz_last_error());
+  Result r = parse_result(code, aux);
+  if (r.is_ok() && out) *out = p;
+  return r;
+}
+
+// Verifier (verifier/mod.rs:42-172) for one statement; each call is a 1-entry device call.
+class Verifier {
+ public:
+  Verifier(Device& dev, Parameters params, Statement st) : dev_(&dev), params_(params), st_(st) {}
+  // verifier/mod.rs:85-88 (fresh transcript) and :120-139 (transcript with an optional context)
+  Result verify(const Proof& pr) const { return verify_with_transcript(pr, std::nullopt); }
+  Result verify_with_transcript(const Proof& pr, const std::optional<std::vector<uint8_t>>& context) const {
+    uint8_t st = 0, present = context ? 1 : 0, pad = 0;
+    const uint64_t off[2] = {0, context ? context->size() : 0};
+    const uint8_t* cb = (context && !context->empty()) ? context->data() : &pad;
+    const int rc = cpz_verify_each(dev_->get(), params_.g.data(), params_.h.data(), 1, st_.y1.data(), st_.y2.data(),
+                                   pr.r1.data(), pr.r2.data(), pr.s.data(), context ? cb : nullptr,
+                                   context ? off : nullptr, context ? &present : nullptr, &st);
+    if (rc != CPZ_OK) return Result::err(ErrorKind::Device, cpz_last_error());
+    return status_result(st);
+  }
+  // verifier/mod.rs:144-171: the caller's challenge (32 canonical little-endian bytes)
+  Result verify_response(const Bytes32& challenge, const Proof& pr) const {
+    uint8_t st = 0;
+    const int rc = cpz_verify_response(dev_->get(), params_.g.data(), params_.h.data(), 1, st_.y1.data(),
+                                       st_.y2.data(), pr.r1.data(), pr.r2.data(), pr.s.data(), challenge.data(), &st);
+    if (rc != CPZ_OK) return Result::err(ErrorKind::Device, cpz_last_error());
+    return status_result(st);
+  }
+
+ private:
+  Device* dev_;
+  Parameters params_;
+  Statement st_;
+};
+
+// Prover (prover/mod.rs:25-132) for one witness x; the nonce k is the caller's (commit draws it
+// from an rng in the reference, :115-121).
+class Prover {
+ public:
+  Prover(Device& dev, Parameters params, Bytes32 x) : dev_(&dev), params_(params), x_(x) {}
+  // prover/mod.rs:86-110: proof (and the statement y = x g, x h) for nonce k.
+  Result prove_with_transcript(const Bytes32& k, const std::optional<std::vector<uint8_t>>& context, Proof* proof,
+                               Statement* statement = nullptr) const {
+    Statement st;
+    Proof pr;
+    uint8_t present = context ? 1 : 0, pad = 0;
+    const uint64_t off[2] = {0, context ? context->size() : 0};
+    const uint8_t* cb = (context && !context->empty()) ? context->data() : &pad;
+    const int rc = cpz_prove(dev_->get(), params_.g.data(), params_.h.data(), 1, x_.data(), k.data(),
+                             context ? cb : nullptr, context ? off : nullptr, context ? &present : nullptr,
+                             st.y1.data(), st.y2.data(), pr.r1.data(), pr.r2.data(), pr.s.data());
+    if (rc != CPZ_OK) return Result::err(ErrorKind::Device, cpz_last_error());
+    if (proof) *proof = pr;
+    if (statement) *statement = st;
+    return Result::ok();
+  }
+
+ private:
+  Device* dev_;
+  Parameters params_;
+  Bytes32 x_;
 };
 
 class BatchVerifier {

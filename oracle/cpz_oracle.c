@@ -596,7 +596,7 @@ static void chacha_block(uint8_t out[64], const uint8_t key[32], uint64_t ctr, u
 /* ------------------------------------------------------------------------------------ */
 /* Protocol                                                                              */
 /* ------------------------------------------------------------------------------------ */
-enum { ST_OK = 0, ST_EQ = 1, ST_POINT = 2, ST_SCALAR = 3, ST_IDZ = 4 };
+enum { ST_OK = 0, ST_EQ = 1, ST_POINT = 2, ST_SCALAR = 3, ST_IDENT = 4, ST_ZERO_S = 5 };
 
 typedef struct {
   ge y1, y2, r1, r2;
@@ -615,8 +615,8 @@ static int decode_entry(decoded *d, const uint8_t *y1, const uint8_t *y2, const 
   if (!r_decode(&d->y1, y1) || !r_decode(&d->y2, y2)) return ST_POINT;
   if (!r_decode(&d->r1, r1) || !r_decode(&d->r2, r2)) return ST_POINT;
   if (!sc_canonical(s)) return ST_SCALAR;
-  if (is_zero32(r1) || is_zero32(r2)) return ST_IDZ; /* identity encodes as 32 zero bytes */
-  if (is_zero32(s)) return ST_IDZ;
+  if (is_zero32(r1) || is_zero32(r2)) return ST_IDENT; /* gadgets.rs:474-478; identity = 32 zero bytes */
+  if (is_zero32(s)) return ST_ZERO_S;                     /* gadgets.rs:480-482 */
   memcpy(d->s, s, 32);
   return ST_OK;
 }

@@ -501,7 +501,7 @@ def rlc_weights(seed: bytes, index: int):
 # ----------------------------------------------------------------------------
 # Protocol: prover (input generator) and per-proof verification
 # ----------------------------------------------------------------------------
-ST_OK, ST_EQ_FAIL, ST_BAD_POINT, ST_BAD_SCALAR, ST_IDENTITY_OR_ZERO = 0, 1, 2, 3, 4
+ST_OK, ST_EQ_FAIL, ST_BAD_POINT, ST_BAD_SCALAR, ST_IDENTITY, ST_ZERO_S = 0, 1, 2, 3, 4, 5
 
 
 @dataclass
@@ -552,9 +552,9 @@ def decode_status(rec: ProofRecord):
     if s is None:
         return ST_BAD_SCALAR, None, None
     if pt_is_identity(r1) or pt_is_identity(r2):
-        return ST_IDENTITY_OR_ZERO, None, None
+        return ST_IDENTITY, None, None      # gadgets.rs:474-478
     if s == 0:
-        return ST_IDENTITY_OR_ZERO, None, None
+        return ST_ZERO_S, None, None        # gadgets.rs:480-482
     return ST_OK, (y1, y2, r1, r2), s
 
 
@@ -572,6 +572,25 @@ def verify_one(rec: ProofRecord, g_bytes: bytes = G_BYTES, h_bytes: bytes = H_BY
     lhs2 = pt_mul(h, s)
     rhs2 = pt_add(r2, pt_mul(y2, c))
     return ST_OK if (pt_eq(lhs1, rhs1) and pt_eq(lhs2, rhs2)) else ST_EQ_FAIL
+
+
+def verify_response(rec: ProofRecord, c_bytes: bytes, g_bytes: bytes = G_BYTES, h_bytes: bytes = H_BYTES) -> int:
+    """`Verifier::verify_response` (verifier/mod.rs:144-171) with a caller-supplied challenge,
+    preceded by decode_status (the Proof / Statement were decoded before the call).  The
+    challenge arrives as 32 bytes here: non-canonical bytes (scalar_from_bytes would fail,
+    ristretto.rs:94-112) give ST_BAD_SCALAR, after the entry's own decode-level checks."""
+    st, pts, s = decode_status(rec)
+    if st != ST_OK:
+        return st
+    c = scalar_from_canonical(c_bytes)
+    if c is None:
+        return ST_BAD_SCALAR
+    y1, y2, r1, r2 = pts
+    g = ristretto_decode(g_bytes)
+    h = ristretto_decode(h_bytes)
+    ok1 = pt_eq(pt_mul(g, s), pt_add(r1, pt_mul(y1, c)))
+    ok2 = pt_eq(pt_mul(h, s), pt_add(r2, pt_mul(y2, c)))
+    return ST_OK if (ok1 and ok2) else ST_EQ_FAIL
 
 
 def reference_batch_equation(recs: Sequence[ProofRecord], alphas: Sequence[int],

@@ -3,6 +3,7 @@
 // Proofs come from the GPU prover (cpz_prove_synthetic); contexts follow
 // examples/batch_verification.rs ("user-{i}-session").  Exit status 0 = all passed.
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -123,6 +124,62 @@ int main() {
     for (auto& x : r) CHECK(x.is_ok());
     b.clear();
     CHECK(b.is_empty());
+  }
+  {  // Proof::to_bytes / from_bytes (gadgets.rs:555-652): round trip, corrupted byte 6 of r1,
+     // identity commitment, zero s, truncation -- the reference's errors, in its order
+    const std::vector<uint8_t> w = base.pr[3].to_bytes();
+    CHECK(w.size() == 109);
+    Proof q;
+    CHECK(proof_from_bytes(dev, w.data(), w.size(), &q).is_ok() && q.s == base.pr[3].s && q.r1 == base.pr[3].r1);
+    std::vector<uint8_t> bad = w;
+    bad[6] ^= 0xff;
+    Result r = proof_from_bytes(dev, bad.data(), bad.size(), nullptr);
+    CHECK(r.is_err() && r.kind == ErrorKind::InvalidGroupElement);
+    Proof id = base.pr[3];
+    id.r2.fill(0);
+    std::vector<uint8_t> wi = id.to_bytes();
+    r = proof_from_bytes(dev, wi.data(), wi.size(), nullptr);
+    CHECK(r.is_err() && r.message == "Commitment contains identity element");
+    Proof zs = base.pr[3];
+    zs.s.fill(0);
+    std::vector<uint8_t> wz = zs.to_bytes();
+    r = proof_from_bytes(dev, wz.data(), wz.size(), nullptr);
+    CHECK(r.is_err() && r.message == "Response scalar is zero");
+    r = proof_from_bytes(dev, w.data(), 100, nullptr);
+    CHECK(r.is_err() && r.message == "Truncated proof: incomplete s data");
+    r = proof_from_bytes(dev, w.data(), 0, nullptr);
+    CHECK(r.is_err() && r.message == "Proof too small: 0 bytes");
+  }
+  {  // Verifier (verifier/mod.rs:174-229) and Prover (prover/mod.rs:154-197) with a caller nonce
+    Bytes32 x{}, k{};
+    for (int i = 0; i < 31; i++) { x[i] = (uint8_t)(3 * i + 1); k[i] = (uint8_t)(5 * i + 2); }
+    Prover pv(dev, params, x);
+    Proof pr;
+    Statement st;
+    const std::string c = "challenge-42";
+    const std::vector<uint8_t> ctxv(c.begin(), c.end());
+    CHECK(pv.prove_with_transcript(k, std::nullopt, &pr, &st).is_ok());
+    Verifier v(dev, params, st);
+    CHECK(v.verify(pr).is_ok());
+    CHECK(v.verify_with_transcript(pr, ctxv).is_err());
+    Proof pc;
+    CHECK(pv.prove_with_transcript(k, ctxv, &pc, nullptr).is_ok());
+    CHECK(v.verify_with_transcript(pc, ctxv).is_ok() && v.verify(pc).is_err());
+    // verify_response: s = k + c x for the caller's c; c = 0 makes s = k
+    Bytes32 zero{};
+    Proof pk = pr;
+    pk.s = k;
+    CHECK(v.verify_response(zero, pk).is_ok());
+    Bytes32 one{};
+    one[0] = 1;
+    CHECK(v.verify_response(one, pk).is_err());
+    Bytes32 big;
+    big.fill(0xff);  // non-canonical challenge -> InvalidScalar
+    Result rr = v.verify_response(big, pk);
+    CHECK(rr.is_err() && rr.kind == ErrorKind::InvalidScalar);
+    // same nonce, same witness -> same proof (deterministic given k)
+    Proof again;
+    CHECK(pv.prove_with_transcript(k, std::nullopt, &again, nullptr).is_ok() && again.s == pr.s && again.r1 == pr.r1);
   }
   if (failures) {
     std::fprintf(stderr, "%d failures\n", failures);

@@ -154,13 +154,13 @@ def main():
         ("s_high_bit", dict(s=(s_int | (1 << 255)).to_bytes(32, "little")), O.ST_BAD_SCALAR),
         ("s_eq_l", dict(s=L.to_bytes(32, "little")), O.ST_BAD_SCALAR),
         ("s_all_ff", dict(s=b"\xff" * 32), O.ST_BAD_SCALAR),
-        ("s_zero", dict(s=ident), O.ST_IDENTITY_OR_ZERO),
-        ("r1_identity", dict(r1=ident), O.ST_IDENTITY_OR_ZERO),
-        ("r2_identity", dict(r2=ident), O.ST_IDENTITY_OR_ZERO),
+        ("s_zero", dict(s=ident), O.ST_ZERO_S),
+        ("r1_identity", dict(r1=ident), O.ST_IDENTITY),
+        ("r2_identity", dict(r2=ident), O.ST_IDENTITY),
         ("identity_statement", dict(y1=ident, y2=ident), O.ST_EQ_FAIL),
         ("bad_point_and_bad_scalar", dict(r1=bytes.fromhex(RFC_BAD[5]), s=b"\xff" * 32), O.ST_BAD_POINT),
         ("bad_scalar_and_identity", dict(r1=ident, s=b"\xff" * 32), O.ST_BAD_SCALAR),
-        ("zero_s_and_identity", dict(r1=ident, s=ident), O.ST_IDENTITY_OR_ZERO),
+        ("zero_s_and_identity", dict(r1=ident, s=ident), O.ST_IDENTITY),
     ]
     for j, enc in enumerate(RFC_BAD):
         field = ("y1", "y2", "r1", "r2")[j % 4]
@@ -280,6 +280,52 @@ def main():
     for w, e in zip(wire, out["wire"]):  # the coarse oracle (error kind) agrees
         kind = O.proof_from_bytes(w)
         assert (kind[0] == "ok") == (e["code"] == 0)
+
+    # 8. verify_response (verifier/mod.rs:144-171) with caller-supplied challenges: the
+    #    transcript's challenge (with or without a context: the caller's c replaces the
+    #    transcript), c + 1, c + l (non-canonical), and decode-level failures first.
+    resp = []
+    for i in range(6):
+        rec = recs[i]
+        c = O.challenge(O.G_BYTES, O.H_BYTES, rec.y1, rec.y2, rec.r1, rec.r2, rec.ctx)
+        cases = [("transcript_c", O.scalar_bytes(c)), ("c_plus_1", O.scalar_bytes((c + 1) % L)),
+                 ("c_plus_l", (c + L).to_bytes(32, "little")), ("c_zero", bytes(32))]
+        for kind, cb in cases:
+            st = O.verify_response(rec, cb)
+            d = rec_json(rec, st, None, kind)
+            d["c"] = cb.hex()
+            resp.append(d)
+    # c = 0 verifies exactly when s is the nonce: g^k == r1 (a proof made with x = 0 or c = 0)
+    rec0c = O.prove(O.bench_scalar(b"x", 77), O.bench_scalar(b"k", 77), None)
+    k77 = O.bench_scalar(b"k", 77)
+    zero_c = O.ProofRecord(rec0c.y1, rec0c.y2, rec0c.r1, rec0c.r2, O.scalar_bytes(k77))
+    d = rec_json(zero_c, O.verify_response(zero_c, bytes(32)), None, "s_eq_k_with_c_zero")
+    d["c"] = bytes(32).hex()
+    assert d["status"] == O.ST_OK
+    resp.append(d)
+    for p in proofs[48:]:
+        if p["kind"] in ("s_zero", "r1_identity", "s_plus_l", "bad_r1_rfc2", "identity_statement"):
+            r = O.ProofRecord(*(bytes.fromhex(p[k]) for k in ("y1", "y2", "r1", "r2", "s")))
+            cb = (L + 5).to_bytes(32, "little")  # non-canonical c: decode-level statuses come first
+            d = rec_json(r, O.verify_response(r, cb), None, "resp_" + p["kind"])
+            d["c"] = cb.hex()
+            resp.append(d)
+    out["response"] = resp
+
+    # 9. Prover (Prover::prove_with_transcript / commit / respond, prover/mod.rs:86-131, and
+    #    the statement y = x g, x h, gadgets.rs:217-221) from caller witnesses and nonces.
+    prv = []
+    for i in range(10):
+        x = O.bench_scalar(b"px", i) if i != 3 else 0
+        k = O.bench_scalar(b"pk", i)
+        ctx = [None, b"", b"user-%d-session" % i, bytes(range(32))][i % 4]
+        rec = O.prove(x, k, ctx)
+        assert O.verify_one(rec) == (O.ST_OK if True else None) or x == 0
+        d = rec_json(rec, O.verify_one(rec))
+        d["x"] = O.scalar_bytes(x).hex()
+        d["k"] = O.scalar_bytes(k).hex()
+        prv.append(d)
+    out["prove"] = prv
 
     path = os.path.join(HERE, "golden.json")
     with open(path, "w") as f:

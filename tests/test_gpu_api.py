@@ -1,0 +1,192 @@
+"""GPU tests of the reference interface beyond BatchVerifier: Proof::from_bytes through the
+device parser (gadgets.rs:364-489), Verifier::verify_response with caller challenges
+(verifier/mod.rs:144-171), the prover from caller witnesses (prover/mod.rs:86-131,
+gadgets.rs:217-221), bulk element_from_bytes / element_to_bytes (ristretto.rs:120-143), the
+service's registration checks (service.rs:61-97), and call ordering across streams."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import chaum_pedersen as cp
+import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _rows(ps, k):
+    return np.frombuffer(b"".join(bytes.fromhex(p[k]) for p in ps), np.uint8).reshape(-1, 32)
+
+
+def test_from_bytes_golden_wire(gpu, golden):
+    """Every golden blob: Proof.from_bytes returns the proof or raises the reference's error
+    type with its exact message (the oracle's code / value for that blob)."""
+    for w in golden["wire"]:
+        b = bytes.fromhex(w["blob"])
+        want = cp.parse_error(w["code"], w["aux"])
+        if want is None:
+            p = cp.Proof.from_bytes(b, gpu)
+            assert (p.r1, p.r2, p.s) == (b[5:37], b[41:73], b[77:109])
+            assert p.to_bytes() == b
+        else:
+            with pytest.raises(cp.Error) as exc:
+                cp.Proof.from_bytes(b, gpu)
+            assert type(exc.value) is type(want) and str(exc.value) == str(want), w
+    many = cp.Proof.from_bytes_many([bytes.fromhex(w["blob"]) for w in golden["wire"]], gpu)
+    assert [isinstance(m, cp.Proof) for m in many] == [w["code"] == 0 for w in golden["wire"]]
+
+
+def test_verify_response_golden(gpu, golden):
+    rs = golden["response"]
+    st = gpu.verify_response(*(_rows(rs, k) for k in ("y1", "y2", "r1", "r2", "s", "c")))
+    assert [int(v) for v in st] == [r["status"] for r in rs], [(r["kind"], int(v)) for r, v in zip(rs, st)]
+    # the transcript's challenge as the caller's c gives verify_one's answer on the golden proofs
+    ps = [p for p in golden["proofs"] if "c" in p]
+    st = gpu.verify_response(*(_rows(ps, k) for k in ("y1", "y2", "r1", "r2", "s", "c")))
+    assert [int(v) for v in st] == [p["status"] for p in ps]
+
+
+def test_prove_golden_and_roundtrip(gpu, golden):
+    pv = golden["prove"]
+    ctxs = [None if p["ctx"] is None else bytes.fromhex(p["ctx"]) for p in pv]
+    out = gpu.prove(_rows(pv, "x"), _rows(pv, "k"), contexts=ctxs)
+    for i, p in enumerate(pv):
+        for k in ("y1", "y2", "r1", "r2", "s"):
+            assert out[k][i].tobytes().hex() == p[k], (i, k)
+    st = gpu.verify_each(out["y1"], out["y2"], out["r1"], out["r2"], out["s"], contexts=ctxs)
+    assert [int(v) for v in st] == [p["status"] for p in pv]
+
+
+def test_prove_device_matches_host_and_verifies(gpu):
+    """2^16 random witnesses / nonces (>= l included, taken mod l): the device-buffer prover
+    equals the host-buffer one byte for byte, every proof verifies, a sample equals the oracle."""
+    torch = pytest.importorskip("torch")
+    n = 1 << 16
+    rng = np.random.default_rng(3)
+    x = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    k = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    x[5] = 0xFF                      # >= l: taken mod l
+    host = gpu.prove(x, k)
+    dev = torch.device("cuda:0")
+    t = {q: torch.empty((n, 32), dtype=torch.uint8, device=dev) for q in ("y1", "y2", "r1", "r2", "s")}
+    gpu.prove_device(torch.from_numpy(x).to(dev), torch.from_numpy(k).to(dev), t["y1"], t["y2"], t["r1"], t["r2"],
+                     t["s"])
+    torch.cuda.synchronize()
+    for q in t:
+        assert np.array_equal(t[q].cpu().numpy(), host[q]), q
+    st = gpu.verify_each(host["y1"], host["y2"], host["r1"], host["r2"], host["s"])
+    assert not st.any()
+    for i in (0, 5, 1234, n - 1):
+        rec = O.prove(int.from_bytes(x[i].tobytes(), "little") % O.L, int.from_bytes(k[i].tobytes(), "little") % O.L)
+        assert (host["y1"][i].tobytes(), host["r2"][i].tobytes(), host["s"][i].tobytes()) == (rec.y1, rec.r2, rec.s)
+
+
+def test_verifier_and_prover_mirrors(gpu):
+    """verifier/mod.rs:174-229 and prover/mod.rs:154-197 through the Python mirrors."""
+    params = cp.Parameters()
+    pv = cp.Prover(params, O.bench_scalar(b"x", 5), gpu)
+    st = pv.statement()
+    rec = O.prove(O.bench_scalar(b"x", 5), 9)
+    assert (st.y1, st.y2) == (rec.y1, rec.y2)
+    v = cp.Verifier(params, st, gpu)
+    proof = pv.prove_with_transcript(None, cp.Transcript.new(), nonce=9)
+    assert (proof.r1, proof.r2, proof.s) == (rec.r1, rec.r2, rec.s)
+    v.verify(proof)
+    # proofs are randomised (security_tests.rs:166-209): two calls, two different proofs, both valid
+    p1, p2 = pv.prove(), pv.prove()
+    assert p1.s != p2.s and p1.r1 != p2.r1
+    v.verify(p1)
+    v.verify(p2)
+    # wrong statement (verifier/mod.rs tests): InvalidParams("Proof verification failed")
+    other = cp.Prover(params, 12345, gpu).statement()
+    with pytest.raises(cp.InvalidParams) as e:
+        cp.Verifier(params, other, gpu).verify(proof)
+    assert str(e.value) == "Proof verification failed"
+    # transcript context binds the proof (security_tests.rs:6-39)
+    t = cp.Transcript.new()
+    t.append_context(b"challenge-12345")
+    bound = pv.prove_with_transcript(None, t)
+    v.verify_with_transcript(bound, t)
+    with pytest.raises(cp.InvalidParams):
+        v.verify(bound)
+    # interactive: commit, caller challenge, respond, verify_response
+    (r1, r2), k = pv.commit()
+    c = 0xC0FFEE
+    s = pv.respond(k, c)
+    v.verify_response(c, cp.Proof(r1, r2, s))
+    with pytest.raises(cp.InvalidParams):
+        v.verify_response(c + 1, cp.Proof(r1, r2, s))
+    with pytest.raises(cp.InvalidScalar):
+        v.verify_response((O.L + 1).to_bytes(32, "little"), cp.Proof(r1, r2, s))
+
+
+def test_decode_points_rfc9496(gpu, golden):
+    """element_from_bytes / element_to_bytes: RFC 9496 A.1 multiples decode and re-encode to
+    themselves; every A.2 invalid encoding is rejected."""
+    good = [bytes.fromhex(e) for e in golden["rfc9496_multiples"]]
+    bad = [bytes.fromhex(e) for e in golden["rfc9496_bad"]]
+    ok, enc = gpu.decode_points(good + bad)
+    assert list(ok) == [1] * len(good) + [0] * len(bad)
+    assert [enc[i].tobytes() for i in range(len(good))] == good
+    assert not enc[len(good):].any()
+    # statements and commitments of the golden proofs: decode <=> the oracle decodes
+    pts = [bytes.fromhex(p[k]) for p in golden["proofs"] for k in ("y1", "r1")]
+    ok, enc = gpu.decode_points(pts)
+    for i, p in enumerate(pts):
+        dec = O.ristretto_decode(p)
+        assert bool(ok[i]) == (dec is not None)
+        if dec is not None:
+            assert enc[i].tobytes() == O.ristretto_encode(dec)
+
+
+def test_register_handler_checks(gpu):
+    """service.rs:61-97: sizes, element_from_bytes of y1 / y2, identity statements refused."""
+    from chaum_pedersen.service import InvalidArgument, MemoryState, register
+    st = MemoryState()
+    rec = O.prove(O.bench_scalar(b"x", 1), 3)
+    register(st, "alice", rec.y1, rec.y2, gpu)
+    assert st.get_user("alice") == (rec.y1, rec.y2)
+    cases = [("bob", b"", rec.y2, "Empty y1 or y2 values"),
+             ("bob", rec.y1, b"\x01" * 4097, "y1 or y2 values too large"),
+             ("bob", rec.y1[:31], rec.y2, "Invalid y1: Invalid group element: Expected 32 bytes, got 31"),
+             ("bob", rec.y1, bytes.fromhex("01" + "00" * 31),
+              "Invalid y2: Invalid group element: Bytes do not represent a valid Ristretto point"),
+             ("bob", bytes(32), rec.y2, "Statement contains identity elements"),
+             ("bad id!", rec.y1, rec.y2, "User ID contains invalid characters"),
+             ("alice", rec.y1, rec.y2, "Registration failed: Invalid group parameters: User 'alice' already registered")]
+    for uid, y1, y2, msg in cases:
+        with pytest.raises(InvalidArgument) as e:
+            register(st, uid, y1, y2, gpu)
+        assert str(e.value) == msg
+    assert st.get_user("bob") is None
+
+
+def test_calls_ordered_across_streams(gpu, golden):
+    """A device-path verify enqueued on a side stream, then -- without any synchronisation --
+    a host-path call and a call with other generators (which rebuilds the context's tables):
+    every call still sees its own inputs (each call is ordered after the previous one)."""
+    torch = pytest.importorskip("torch")
+    n = 1 << 18
+    dev = torch.device("cuda:0")
+    sx, sk = hashlib.sha256(b"cpz-bench-x").digest(), hashlib.sha256(b"cpz-bench-k").digest()
+    t = {q: torch.empty((n, 32), dtype=torch.uint8, device=dev) for q in ("y1", "y2", "r1", "r2", "s")}
+    gpu.prove_synthetic_device(n, sx, sk, t["y1"], t["y2"], t["r1"], t["r2"], t["s"])
+    torch.cuda.synchronize()
+    status = torch.full((n,), 0xFF, dtype=torch.uint8, device=dev)
+    side = torch.cuda.Stream(dev)
+    with torch.cuda.stream(side):
+        gpu.verify_each_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status)
+    # host path on the context's own stream, other data (golden proofs, some invalid)
+    ps = golden["proofs"]
+    st = gpu.verify_each(*(_rows(ps, k) for k in ("y1", "y2", "r1", "r2", "s")),
+                         contexts=[None if p["ctx"] is None else bytes.fromhex(p["ctx"]) for p in ps])
+    assert [int(v) for v in st] == [p["status"] for p in ps]
+    # other generators: the comb / prefix tables are rebuilt
+    cg = golden["custom_generators"]
+    params = cp.Parameters.with_generators(bytes.fromhex(cg["g"]), bytes.fromhex(cg["h"]))
+    cps = cg["proofs"]
+    st = gpu.verify_each(*(_rows(cps, k) for k in ("y1", "y2", "r1", "r2", "s")),
+                         contexts=[bytes.fromhex(p["ctx"]) for p in cps], params=params)
+    assert not st.any()
+    side.synchronize()
+    assert int((status != 0).sum().item()) == 0

@@ -156,11 +156,21 @@ def test_security_corrupted_bytes(gpu):
     st = cp.Statement(rec.y1, rec.y2)
     wire = cp.Proof(rec.r1, rec.r2, rec.s).to_bytes()
     assert len(wire) == 109
+    assert cp.Proof.from_bytes(wire, gpu).s == rec.s
     for pos in (1 + 5, len(wire) - 10):
         w = bytearray(wire)
         w[pos] ^= 0xFF
+        # as the reference test: either from_bytes rejects the blob (it decodes r1 / checks s)
+        # or the proof fails verification -- and which one happens is the oracle's answer
+        try:
+            proof = cp.Proof.from_bytes(bytes(w), gpu)
+        except cp.Error as e:
+            code, aux = O.proof_from_bytes_code(bytes(w))
+            assert code != 0 and str(e) == str(cp.parse_error(code, aux))
+            continue
+        assert O.proof_from_bytes_code(bytes(w))[0] == 0
         b = cp.BatchVerifier(gpu)
-        b.add(cp.Parameters(), st, cp.Proof.from_bytes(bytes(w)))
+        b.add(cp.Parameters(), st, proof)
         assert b.verify()[0].is_err()
 
 
