@@ -47,6 +47,12 @@ def load():
         lib.cpzo_sc_reduce_wide.argtypes = [_p, _p]
         lib.cpzo_sc_mul.argtypes = [_p, _p, _p]
         lib.cpzo_chacha_block.argtypes = [_p, _p, ctypes.c_uint64, ctypes.c_uint64]
+        lib.cpzo_verify_many_ctx.restype = None
+        lib.cpzo_verify_many_ctx.argtypes = [_p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p, _p, _p]
+        lib.cpzo_challenge_many.restype = None
+        lib.cpzo_challenge_many.argtypes = [_p, _p, ctypes.c_size_t] + [_p] * 4 + [_p, _p, _p, _p]
+        lib.cpzo_rlc_partial.restype = ctypes.c_long
+        lib.cpzo_rlc_partial.argtypes = [_p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p, _p, _p, _p, _p]
         _lib = lib
     return _lib
 
@@ -100,6 +106,92 @@ def verify_many(rows, lo=0, hi=None, g=DEFAULT_G, h=DEFAULT_H, threads=1) -> np.
     for t in ts:
         t.join()
     return out
+
+
+def _ctx_arrays(contexts, n):
+    """None -> (None, None, None); else (blob, absolute offsets[n + 1], present[n])."""
+    if contexts is None:
+        return None, None, None
+    present = np.array([0 if c is None else 1 for c in contexts], np.uint8)
+    lens = np.array([0 if c is None else len(c) for c in contexts], np.uint64)
+    off = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens, out=off[1:])
+    blob = np.frombuffer(b"".join(c for c in contexts if c is not None) + b"\0", np.uint8).copy()
+    return blob, off, present
+
+
+def _pp(a):
+    return None if a is None else a.ctypes.data
+
+
+def _parallel(n, threads, fn):
+    """fn(lo, hi) on `threads` threads over [0, n) (ctypes releases the GIL)."""
+    bounds = [(n * t) // threads for t in range(threads + 1)]
+    ts = [threading.Thread(target=fn, args=(bounds[t], bounds[t + 1])) for t in range(threads) if bounds[t + 1] > bounds[t]]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+
+
+def verify_many_ctx(rows, contexts=None, g=DEFAULT_G, h=DEFAULT_H, threads=1) -> np.ndarray:
+    """Per-proof statuses (decode + verify_one) for rows (dict of (n, 32) arrays) with an
+    optional context per entry (None / bytes), on `threads` threads."""
+    lib = load()
+    n = len(rows["y1"])
+    arr = [np.ascontiguousarray(rows[k], dtype=np.uint8) for k in ("y1", "y2", "r1", "r2", "s")]
+    blob, off, present = _ctx_arrays(contexts, n)
+    out = np.zeros(n, np.uint8)
+
+    def work(lo, hi):
+        lib.cpzo_verify_many_ctx(g, h, hi - lo, *[a[lo:].ctypes.data for a in arr], _pp(blob),
+                                 None if off is None else off[lo:].ctypes.data,
+                                 None if present is None else present[lo:].ctypes.data, out[lo:].ctypes.data)
+    _parallel(n, max(1, threads), work)
+    return out
+
+
+def challenge_many(rows, contexts=None, g=DEFAULT_G, h=DEFAULT_H, threads=1) -> np.ndarray:
+    """Transcript challenges (n, 32) for rows with optional contexts."""
+    lib = load()
+    n = len(rows["y1"])
+    arr = [np.ascontiguousarray(rows[k], dtype=np.uint8) for k in ("y1", "y2", "r1", "r2")]
+    blob, off, present = _ctx_arrays(contexts, n)
+    out = np.zeros((n, 32), np.uint8)
+
+    def work(lo, hi):
+        lib.cpzo_challenge_many(g, h, hi - lo, *[a[lo:].ctypes.data for a in arr], _pp(blob),
+                                None if off is None else off[lo:].ctypes.data,
+                                None if present is None else present[lo:].ctypes.data, out[lo:].ctypes.data)
+    _parallel(n, max(1, threads), work)
+    return out
+
+
+def rlc_partial(rows, gidx, seed, contexts=None, g=DEFAULT_G, h=DEFAULT_H, threads=1):
+    """(encoding, live count) of the corrected RLC partial over the given entries, whose
+    global batch indices are gidx (weights keyed by them).  Threads sum disjoint slices
+    (partials combined by cpzo_point_sum)."""
+    lib = load()
+    n = len(rows["y1"])
+    arr = [np.ascontiguousarray(rows[k], dtype=np.uint8) for k in ("y1", "y2", "r1", "r2", "s")]
+    gi = np.ascontiguousarray(np.asarray(gidx, dtype=np.uint64))
+    blob, off, present = _ctx_arrays(contexts, n)
+    parts, lives = {}, {}
+
+    def work(lo, hi):
+        out = ctypes.create_string_buffer(32)
+        live = lib.cpzo_rlc_partial(g, h, hi - lo, *[a[lo:].ctypes.data for a in arr], _pp(blob),
+                                    None if off is None else off[lo:].ctypes.data,
+                                    None if present is None else present[lo:].ctypes.data, gi[lo:].ctypes.data,
+                                    bytes(seed), out)
+        parts[lo], lives[lo] = out.raw, live
+    _parallel(n, max(1, threads), work)
+    if len(parts) == 1:
+        return parts[min(parts)], sum(lives.values())
+    out = ctypes.create_string_buffer(32)
+    blob_p = b"".join(parts[k] for k in sorted(parts))
+    assert lib.cpzo_point_sum(out, len(parts), blob_p) == 1
+    return out.raw, sum(lives.values())
 
 
 def reference_batch_verify(rows, lo, hi, g=DEFAULT_G, h=DEFAULT_H, seed=WEIGHT_SEED):

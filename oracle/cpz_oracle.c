@@ -739,3 +739,135 @@ void cpzo_sc_mul(uint8_t out[32], const uint8_t a[32], const uint8_t b[32]) { sc
 void cpzo_chacha_block(uint8_t out[64], const uint8_t key[32], uint64_t ctr, uint64_t stream) {
   chacha_block(out, key, ctr, stream);
 }
+
+/* ------------------------------------------------------------------------------------ */
+/* At-scale checkers (test infrastructure): per-entry statuses and challenges with         */
+/* optional contexts, and the corrected RLC partial of a subset of a batch.                */
+/* ------------------------------------------------------------------------------------ */
+static void entry_ctx(const uint8_t *ctx_bytes, const uint64_t *ctx_off, const uint8_t *ctx_present, size_t i,
+                      const uint8_t **p, uint64_t *len, int *has) {
+  *has = ctx_off != 0 && (ctx_present == 0 || ctx_present[i] != 0);
+  *p = *has ? ctx_bytes + ctx_off[i] : 0;
+  *len = *has ? ctx_off[i + 1] - ctx_off[i] : 0;
+}
+
+/* Per-proof statuses (decode + verify_one, batch.rs:185-231) for n SoA rows with contexts
+ * (ctx_off: n + 1 absolute offsets into ctx_bytes, or NULL: no contexts; ctx_present: NULL =
+ * every entry Some). */
+void cpzo_verify_many_ctx(const uint8_t g[32], const uint8_t h[32], size_t n, const uint8_t *y1, const uint8_t *y2,
+                          const uint8_t *r1, const uint8_t *r2, const uint8_t *s, const uint8_t *ctx_bytes,
+                          const uint64_t *ctx_off, const uint8_t *ctx_present, uint8_t *status) {
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t *cp;
+    uint64_t cl;
+    int has;
+    entry_ctx(ctx_bytes, ctx_off, ctx_present, i, &cp, &cl, &has);
+    status[i] = (uint8_t)cpzo_verify_one(g, h, y1 + 32 * i, y2 + 32 * i, r1 + 32 * i, r2 + 32 * i, s + 32 * i, cp, cl,
+                                         has);
+  }
+}
+
+/* Transcript challenges (transcript.rs:29-71) for n rows with contexts. */
+void cpzo_challenge_many(const uint8_t g[32], const uint8_t h[32], size_t n, const uint8_t *y1, const uint8_t *y2,
+                         const uint8_t *r1, const uint8_t *r2, const uint8_t *ctx_bytes, const uint64_t *ctx_off,
+                         const uint8_t *ctx_present, uint8_t *c_out) {
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t *cp;
+    uint64_t cl;
+    int has;
+    entry_ctx(ctx_bytes, ctx_off, ctx_present, i, &cp, &cl, &has);
+    protocol_challenge(c_out + 32 * i, g, h, y1 + 32 * i, y2 + 32 * i, r1 + 32 * i, r2 + 32 * i, cp, cl, has);
+  }
+}
+
+static void sc_add(uint8_t out[32], const uint8_t a[32], const uint8_t b[32]) {
+  uint8_t wide[64] = {0};
+  unsigned carry = 0;
+  for (int i = 0; i < 32; i++) {
+    unsigned v = (unsigned)a[i] + b[i] + carry;
+    wide[i] = (uint8_t)v;
+    carry = v >> 8;
+  }
+  wide[32] = (uint8_t)carry;
+  sc_reduce(out, wide, 64);
+}
+
+static void sc_neg(uint8_t out[32], const uint8_t a[32]) { /* l - a (mod l), a canonical */
+  static const uint8_t L_BYTES[32] = {0xed, 0xd3, 0xf5, 0x5c, 0x1a, 0x63, 0x12, 0x58, 0xd6, 0x9c, 0xf7,
+                                      0xa2, 0xde, 0xf9, 0xde, 0x14, 0, 0, 0, 0, 0, 0,
+                                      0, 0, 0, 0, 0, 0, 0, 0, 0, 0x10};
+  uint8_t d[64] = {0};
+  int borrow = 0;
+  for (int i = 0; i < 32; i++) {
+    int v = (int)L_BYTES[i] - a[i] - borrow;
+    borrow = v < 0;
+    d[i] = (uint8_t)(v + (borrow ? 256 : 0));
+  }
+  sc_reduce(out, d, 64); /* l - 0 = l -> 0 */
+}
+
+/* The 128-bit RLC weight from 8 little-endian int16 words (pyoracle.rlc_weights):
+ * sum_k w_k 2^(16k) mod l, each signed word reduced mod l and scaled separately. */
+static void rlc_weight_words(uint8_t out[32], const uint8_t blk16[16]) {
+  uint8_t acc[32] = {0};
+  for (int k = 0; k < 8; k++) {
+    const int16_t w = (int16_t)(blk16[2 * k] | (blk16[2 * k + 1] << 8));
+    uint8_t mag[32] = {0}, term[32], pow2[32] = {0};
+    const int m = w < 0 ? -(int)w : (int)w;
+    mag[0] = (uint8_t)m;
+    mag[1] = (uint8_t)(m >> 8);
+    pow2[(16 * k) / 8] = 1; /* 2^(16k): byte 2k */
+    sc_mul(term, mag, pow2);
+    if (w < 0) sc_neg(term, term);
+    sc_add(acc, acc, term);
+  }
+  memcpy(out, acc, 32);
+}
+
+/* The corrected RLC partial (rlc.hip; pyoracle.rlc_partial) of n entries whose GLOBAL batch
+ * indices are gidx[i]:  sum over entries whose decode-level status is 0 of
+ *   [a s] g - [a] r1 - [a c] y1 + [b s] h - [b] r2 - [b c] y2,
+ * (a, b) = the weights of ChaCha20(seed) block gidx[i].  Returns the encoding in out and the
+ * number of live (weighted) entries. */
+long cpzo_rlc_partial(const uint8_t g[32], const uint8_t h[32], size_t n, const uint8_t *y1, const uint8_t *y2,
+                      const uint8_t *r1, const uint8_t *r2, const uint8_t *s, const uint8_t *ctx_bytes,
+                      const uint64_t *ctx_off, const uint8_t *ctx_present, const uint64_t *gidx,
+                      const uint8_t seed[32], uint8_t out[32]) {
+  ge G, H;
+  if (!r_decode(&G, g) || !r_decode(&H, h)) return -1;
+  ge acc = g_identity();
+  uint8_t sg[32] = {0}, sh[32] = {0};
+  long live = 0;
+  for (size_t i = 0; i < n; i++) {
+    decoded d;
+    if (decode_entry(&d, y1 + 32 * i, y2 + 32 * i, r1 + 32 * i, r2 + 32 * i, s + 32 * i) != ST_OK) continue;
+    live++;
+    const uint8_t *cp;
+    uint64_t cl;
+    int has;
+    entry_ctx(ctx_bytes, ctx_off, ctx_present, i, &cp, &cl, &has);
+    uint8_t c[32], blk[64], a[32], b[32], t[32], na[32];
+    protocol_challenge(c, g, h, y1 + 32 * i, y2 + 32 * i, r1 + 32 * i, r2 + 32 * i, cp, cl, has);
+    chacha_block(blk, seed, gidx[i], 0);
+    rlc_weight_words(a, blk);
+    rlc_weight_words(b, blk + 16);
+    sc_mul(t, a, d.s);
+    sc_add(sg, sg, t);
+    sc_mul(t, b, d.s);
+    sc_add(sh, sh, t);
+    sc_neg(na, a);
+    acc = g_add(acc, g_mul_ct(d.r1, na));
+    sc_mul(t, a, c);
+    sc_neg(t, t);
+    acc = g_add(acc, g_mul_ct(d.y1, t));
+    sc_neg(na, b);
+    acc = g_add(acc, g_mul_ct(d.r2, na));
+    sc_mul(t, b, c);
+    sc_neg(t, t);
+    acc = g_add(acc, g_mul_ct(d.y2, t));
+  }
+  acc = g_add(acc, g_mul_ct(G, sg));
+  acc = g_add(acc, g_mul_ct(H, sh));
+  r_encode(out, acc);
+  return live;
+}

@@ -1,0 +1,164 @@
+"""Parity at the configs' full sizes against the C oracle (oracle/cpz_oracle.c, the at-scale
+checker; test infrastructure only):
+
+* C2 (configs[1]): 2^20 proofs, a quarter with 32-byte transcript contexts (the service's
+  challenge ids), a 2^16-entry sample carrying every forgery / malformation kind -- s + 1,
+  wrong y1, wrong context, undecodable point, non-canonical s, zero s, identity commitment.
+  Statuses AND challenges of the whole sample equal the oracle's (batch.rs:185-231,
+  transcript.rs:29-71, gadgets.rs:364-489); every entry outside it is valid.
+* C5 (configs[4]) and C4 (configs[3]): the RLC partial of a forged batch -- whole batch and
+  every shard, weights keyed by the global index -- equals, byte for byte, the oracle's
+  partial computed from the forged entries ALONE (valid entries contribute the identity, so
+  the CPU needs only those), for 2^24 proofs with 16,777 forged and 2^26 proofs as 8 shards.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import coracle as C
+import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+SX = hashlib.sha256(b"cpz-bench-x").digest()
+SK = hashlib.sha256(b"cpz-bench-k").digest()
+WSEED = hashlib.sha256(b"cpz-weights-v1").digest()
+KEYS = ("y1", "y2", "r1", "r2", "s")
+
+
+def _threads():
+    try:
+        return max(1, min(16, len(os.sched_getaffinity(0))))
+    except AttributeError:
+        return max(1, min(16, os.cpu_count() or 1))
+
+
+def _le(b):
+    return int.from_bytes(bytes(b), "little")
+
+
+def test_c2_sample_every_forgery_kind(gpu, golden):
+    n = 1 << 20
+    rng = np.random.default_rng(20)
+    ctxs = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() if i % 4 == 0 else None for i in range(n)]
+    rows = gpu.prove_synthetic(n, SX, SK, contexts=ctxs)
+    rows = {k: np.ascontiguousarray(rows[k]) for k in KEYS}
+    sample = np.sort(rng.choice(n, size=1 << 16, replace=False))
+    forged = sample[rng.random(sample.size) < 0.25]
+    kinds = ("s_plus_1", "wrong_y1", "wrong_context", "bad_point", "s_plus_l", "zero_s", "identity_r")
+    bad_pts = [bytes.fromhex(e) for e in golden["rfc9496_bad"]]
+    expect_kind = {}
+    y1_orig = rows["y1"].copy()
+    for j, i in enumerate(forged):
+        kind = kinds[j % len(kinds)]
+        expect_kind[int(i)] = kind
+        if kind == "s_plus_1":
+            rows["s"][i] = np.frombuffer(((_le(rows["s"][i]) + 1) % O.L).to_bytes(32, "little"), np.uint8)
+        elif kind == "wrong_y1":
+            rows["y1"][i] = y1_orig[(i + 1) % n]
+        elif kind == "wrong_context":
+            ctxs[i] = b"replayed-" + bytes(8) if ctxs[i] is None else bytes(32)
+        elif kind == "bad_point":
+            rows[("y1", "y2", "r1", "r2")[j % 4]][i] = np.frombuffer(bad_pts[j % len(bad_pts)], np.uint8)
+        elif kind == "s_plus_l":
+            rows["s"][i] = np.frombuffer((_le(rows["s"][i]) + O.L).to_bytes(32, "little"), np.uint8)
+        elif kind == "zero_s":
+            rows["s"][i] = 0
+        else:
+            rows["r2" if j % 2 else "r1"][i] = 0
+    st = gpu.verify_each(*(rows[k] for k in KEYS), contexts=ctxs)
+    c = gpu.challenges(*(rows[k] for k in KEYS[:4]), contexts=ctxs)
+    sub = {k: rows[k][sample] for k in KEYS}
+    sub_ctx = [ctxs[i] for i in sample]
+    t = _threads()
+    st_o = C.verify_many_ctx(sub, sub_ctx, threads=t)
+    c_o = C.challenge_many(sub, sub_ctx, threads=t)
+    mism = np.nonzero(st[sample] != st_o)[0]
+    assert mism.size == 0, [(int(sample[m]), expect_kind.get(int(sample[m])), int(st[sample[m]]), int(st_o[m]))
+                            for m in mism[:10]]
+    assert np.array_equal(c[sample], c_o)
+    outside = np.setdiff1d(np.arange(n), sample)
+    assert not st[outside].any()
+    # every kind occurred and produced its reference status
+    want = {"s_plus_1": {1}, "wrong_y1": {1}, "wrong_context": {1}, "bad_point": {2}, "s_plus_l": {3},
+            "zero_s": {5}, "identity_r": {4}}
+    seen = {}
+    for i, kind in expect_kind.items():
+        seen.setdefault(kind, set()).add(int(st[i]))
+    assert seen == want, seen
+    assert np.array_equal(np.nonzero(st)[0], np.sort(forged))
+
+
+def _synthetic_device(gpu, torch, n):
+    dev = torch.device("cuda:0")
+    t = {k: torch.empty((n, 32), dtype=torch.uint8, device=dev) for k in KEYS}
+    gpu.prove_synthetic_device(n, SX, SK, t["y1"], t["y2"], t["r1"], t["r2"], t["s"])
+    return t
+
+
+def _forge(t, torch, idx):
+    """Half s := s + 1, half y1 := another proof's y1 (device rows, in place); returns the
+    forged rows as host arrays (what the CPU checker needs)."""
+    n = t["s"].shape[0]
+    bump, swap = idx[0::2], idx[1::2]
+    sel = torch.from_numpy(bump.astype(np.int64)).to("cuda:0")
+    rows = t["s"].index_select(0, sel).cpu().numpy()
+    for r in range(rows.shape[0]):
+        rows[r] = np.frombuffer(((_le(rows[r]) + 1) % O.L).to_bytes(32, "little"), np.uint8)
+    t["s"].index_copy_(0, sel, torch.from_numpy(rows).to("cuda:0"))
+    dst = torch.from_numpy(swap.astype(np.int64)).to("cuda:0")
+    src = torch.from_numpy(((swap + 7) % n).astype(np.int64)).to("cuda:0")
+    t["y1"].index_copy_(0, dst, t["y1"].index_select(0, src).clone())
+    allsel = torch.from_numpy(idx.astype(np.int64)).to("cuda:0")
+    return {k: t[k].index_select(0, allsel).cpu().numpy() for k in KEYS}
+
+
+def _oracle_partial(host, gidx, lo=None, hi=None):
+    m = np.ones(len(gidx), bool) if lo is None else (gidx >= lo) & (gidx < hi)
+    if not m.any():
+        return bytes(32)
+    enc, live = C.rlc_partial({k: host[k][m] for k in KEYS}, gidx[m], WSEED, threads=_threads())
+    assert live == int(m.sum())
+    return enc
+
+
+def test_c5_partial_from_forged_entries_alone(gpu):
+    torch = pytest.importorskip("torch")
+    n, nf = 1 << 24, 16_777
+    t = _synthetic_device(gpu, torch, n)
+    idx = np.sort(np.random.default_rng(2024).choice(n, size=nf, replace=False))
+    host = _forge(t, torch, idx)
+    st = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    whole, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED)
+    assert not ok
+    assert whole == _oracle_partial(host, idx)
+    shards = 8
+    per = n // shards
+    for k in range(shards):
+        lo, hi = k * per, (k + 1) * per
+        p, _ = gpu.verify_batch_device(*(t[q][lo:hi] for q in KEYS), st[lo:hi], WSEED, first_index=lo)
+        assert p == _oracle_partial(host, idx, lo, hi), k
+
+
+def test_c4_shard_partials_from_forged_entries_alone(gpu):
+    torch = pytest.importorskip("torch")
+    n, shards = 1 << 26, 8
+    per = n // shards
+    t = _synthetic_device(gpu, torch, n)
+    rng = np.random.default_rng(26)
+    idx = np.sort(np.concatenate([rng.choice(np.arange(2 * per, 3 * per), 300, replace=False),
+                                  rng.choice(np.arange(5 * per, 6 * per), 200, replace=False),
+                                  np.array([n - 1])]))
+    host = _forge(t, torch, idx)
+    st = torch.empty(per, dtype=torch.uint8, device="cuda:0")
+    parts = []
+    for k in range(shards):
+        lo, hi = k * per, (k + 1) * per
+        p, ok = gpu.verify_batch_device(*(t[q][lo:hi] for q in KEYS), st, WSEED, first_index=lo)
+        assert p == _oracle_partial(host, idx, lo, hi), k
+        assert ok == (p == bytes(32))
+        parts.append(p)
+    total, ident = gpu.combine_partials(parts)
+    assert not ident and total == _oracle_partial(host, idx)
