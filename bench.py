@@ -3,15 +3,26 @@
 
 Workload (BASELINE.json configs[1]): 2^20 ristretto255 Chaum-Pedersen proofs, per-proof
 (non-batched) verification -- the reference's BatchVerifier::verify outcome per entry
-(batch.rs:171-231) -- with inputs resident in HBM.  One step = one pass of the verify
-path over the whole batch: k_challenge (Merlin/STROBE Fiat-Shamir challenges + response
-checks) followed by k_verify_each (4 ristretto decodes + 2 Straus double-scalar
-equations per proof).  Inputs are synthetic: valid proofs from the GPU prover
-(cpz_prove_synthetic_device, ChaCha20-derived witnesses, distinct per rank).
+(batch.rs:171-231) -- with inputs resident in HBM.  One step = one pass of the verify path
+over the whole batch: k_challenge (Merlin/STROBE Fiat-Shamir challenges + response checks)
+and k_verify_each (4 ristretto decodes + 2 half-size Straus equations per proof).  Inputs are
+synthetic: valid proofs from the GPU prover (ChaCha20-derived witnesses, distinct per rank).
 
-Multi-GPU (torchrun, one process per GPU): each rank verifies its own 2^20 proofs; there
-is no data-path collective (per-proof verification has no exchange step), so scaling
-is weak and value = all ranks' proofs / max-over-ranks time.
+--mode rlc makes the step the random-linear-combination batch check (configs[2]; with
+--n-total 67108864 on 8 ranks, configs[3]): each rank reduces its shard to a 32-byte partial
+(weights keyed by the global index), the partials are all-gathered (RCCL over xGMI with the
+"nccl" backend) and combined.
+
+Multi-GPU (torchrun, one process per GPU): contiguous shards, no data-path collective in
+'each' mode.  --n sets the proofs per GPU (weak scaling, the default); --n-total sets the
+proofs of the whole job, split over the ranks (strong scaling, configs[3]).  value = all
+ranks' proofs / max-over-ranks time.
+
+At N = 1 the same run also measures (reported beside value, never as value): the RLC batch
+check of the same proofs with per-kernel roofline fractions (configs[2]), the 2^24-proof
+batch with 0.1 % forged proofs through the batch check + fallback (configs[4]), the prover
+(proof generation, published ~144 us/proof, lib.rs:55), the host-buffer entry point (PCIe
+included), and the CPU baseline.
 
 Prints ONE JSON line on rank 0.
 """
@@ -29,6 +40,9 @@ sys.path.insert(0, os.path.join(ROOT, "chaum-pedersen-zkp_amd"))
 
 SEED_X = hashlib.sha256(b"cpz-bench-x").digest()
 SEED_K = hashlib.sha256(b"cpz-bench-k").digest()
+WEIGHT_SEED = hashlib.sha256(b"cpz-weights-v1").digest()
+L = 2**252 + 27742317777372353535851937790883648493
+METRIC = "verified proofs/sec (1/2/4/8 MI355X) + % int-VALU roofline vs host-CPU"
 
 
 def _load_json(rel):
@@ -37,6 +51,29 @@ def _load_json(rel):
         with open(p) as f:
             return json.load(f)
     return None
+
+
+def _profile(name):
+    """The newest committed PMC summary of that name (profiles/rNN_<name>.json)."""
+    cands = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith("_" + name + ".json"))
+    return (_load_json(os.path.join("profiles", cands[-1])) or {}) if cands else {}
+
+
+def cpu_threads(requested: int) -> dict:
+    """Threads for the CPU baseline: the CPUs this process may run on (sched_getaffinity),
+    capped by OMP_NUM_THREADS when the environment sets it (the GPU box's CPU share)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if requested:
+        t = requested
+    elif omp and omp.isdigit():
+        t = min(aff, int(omp))
+    else:
+        t = aff
+    return {"threads": max(1, t), "affinity_cpus": aff, "omp_num_threads": omp}
 
 
 def cpu_baseline(host_rows, seconds: float, threads: int):
@@ -50,14 +87,58 @@ def cpu_baseline(host_rows, seconds: float, threads: int):
     return coracle.time_verify(host_rows, seconds=seconds, threads=threads)
 
 
+def _bump_s(torch, t, idx):
+    """s := s + 1 (mod l) on the given rows (host round trip of those rows only)."""
+    import numpy as np
+    sel = torch.from_numpy(np.asarray(idx, dtype=np.int64)).to(t["s"].device)
+    rows = t["s"].index_select(0, sel).cpu().numpy()
+    for r in range(rows.shape[0]):
+        v = (int.from_bytes(rows[r].tobytes(), "little") + 1) % L
+        rows[r] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)
+    t["s"].index_copy_(0, sel, torch.from_numpy(rows).to(t["s"].device))
+
+
+def rlc_roofline(stages, n, steps, oc):
+    """Per-kernel fractions of the RLC step from the runtime's HIP-event stage times."""
+    r = oc.get("rlc", {})
+    peak = oc["peaks"]["v_mad_i64_i32_lane_ops_per_s"]
+    hbm = oc["peaks"]["hbm_bytes_per_s"]
+    ms = {k: (v[0] / steps) for k, v in stages.items()}
+    out = {"unit_mad": "Tmad/s", "peak_mad": peak / 1e12, "unit_hbm": "GB/s", "peak_hbm": hbm / 1e9,
+           "kernel_ms_per_step": ms}
+    prep = r.get("prepare_per_proof", {}).get("mads")
+    if prep and ms.get("rlc_prepare"):
+        a = prep * n / (ms["rlc_prepare"] * 1e-3) / 1e12
+        out["k_rlc_prepare"] = {"bound": "valu-int", "mads_per_proof": prep, "achieved": a, "frac": a / (peak / 1e12)}
+    ent = r.get("bucket_entries_per_proof")
+    bk = r.get("bucket_per_entry", {})
+    if ent and ms.get("rlc_bucket"):
+        t = ms["rlc_bucket"] * 1e-3
+        a = bk["mads"] * ent * n / t / 1e12
+        gbs = bk["bytes"] * ent * n / t / 1e9
+        pmc = _profile("rlc_bucket_pmc")
+        out["k_rlc_bucket"] = {"bound": "valu-int", "mads_per_entry": bk["mads"], "entries_per_proof": ent,
+                               "achieved": a, "frac": a / (peak / 1e12),
+                               "algorithmic_bytes_per_entry": bk["bytes"], "achieved_gbs": gbs,
+                               "hbm_frac": gbs / (hbm / 1e9),
+                               "traffic_bytes_per_2p20": pmc.get("hbm_bytes_per_2p20"),
+                               "traffic_source": pmc.get("source")}
+    tails = sum(ms.get(k, 0.0) for k in ("rlc_sort", "rlc_bucket_fix", "rlc_reduce", "rlc_final"))
+    out["sort_plus_tails_ms"] = tails
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1 << 20, help="proofs per GPU")
+    ap.add_argument("--n", type=int, default=1 << 20, help="proofs per GPU (weak scaling)")
+    ap.add_argument("--n-total", type=int, default=0,
+                    help="proofs of the whole job, split over the ranks (strong scaling; configs[3] = 67108864)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (rank 0, N=1)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = min(16, cpus))")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: the affinity CPUs, capped by OMP_NUM_THREADS if set)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("each", "rlc"), default="each",
                     help="each: per-proof verification (configs[1], the headline); rlc: random-linear-"
@@ -66,17 +147,17 @@ def main():
     ap.add_argument("--ctx-len", type=int, default=0,
                     help="per-proof transcript context of this many random bytes (0: none, the configs' default; "
                          "32: the reference service's challenge ids, service.rs:294-295)")
-    ap.add_argument("--rlc-extra", type=int, default=1,
-                    help="at N=1 in 'each' mode also time the RLC batch path on the same proofs (reported "
-                         "under 'rlc', not in value)")
-    ap.add_argument("--host-e2e", type=int, default=1,
-                    help="at N=1 in 'each' mode also time the host-buffer entry point (PCIe included; "
-                         "reported under 'host_e2e', not in value)")
+    ap.add_argument("--extras", type=int, default=1,
+                    help="at N=1 in 'each' mode also measure the RLC check, C5, the prover and the host path")
+    ap.add_argument("--rlc-extra", type=int, default=None, help="override --extras for the RLC extra")
+    ap.add_argument("--host-e2e", type=int, default=None, help="override --extras for the host-buffer extra")
+    ap.add_argument("--c5-n", type=int, default=1 << 24, help="configs[4] batch size (0.1 %% forged)")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N > 1 ('nccl' = RCCL over xGMI; 'gloo' only for rehearsals)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses cuda:0 (with --backend gloo); not a measurement")
     args = ap.parse_args()
+    extra = lambda v: args.extras if v is None else v
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -94,9 +175,17 @@ def main():
     dev = torch.device("cuda", local_rank)
 
     import chaum_pedersen as cp
+    from chaum_pedersen.shard import all_gather_partials, shard_range
 
     gpu = cp.Gpu(local_rank)
-    n = args.n
+    if args.n_total:
+        lo, hi = shard_range(args.n_total, world, rank)
+        scaling = "strong"
+    else:
+        lo, hi = rank * args.n, (rank + 1) * args.n
+        scaling = "weak"
+    n = hi - lo
+    total_proofs = args.n_total if args.n_total else world * args.n
     t = {k: torch.empty((n, 32), dtype=torch.uint8, device=dev) for k in ("y1", "y2", "r1", "r2", "s")}
     status = torch.empty(n, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -107,12 +196,9 @@ def main():
         cx["ctx_bytes"] = torch.randint(0, 256, (n * args.ctx_len,), dtype=torch.int32, device=dev,
                                         generator=gen).to(torch.uint8)
         cx["ctx_off"] = torch.arange(n + 1, dtype=torch.int64, device=dev) * args.ctx_len
-    gpu.prove_synthetic_device(n, SEED_X, SEED_K, t["y1"], t["y2"], t["r1"], t["r2"], t["s"],
-                               first_index=rank * n, stream=stream, **cx)
+    gpu.prove_synthetic_device(n, SEED_X, SEED_K, t["y1"], t["y2"], t["r1"], t["r2"], t["s"], first_index=lo,
+                               stream=stream, **cx)
     torch.cuda.synchronize(dev)
-
-    weight_seed = hashlib.sha256(b"cpz-weights-v1").digest()
-    from chaum_pedersen.shard import all_gather_partials
 
     def step_each():
         gpu.verify_each_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status, stream=stream, **cx)
@@ -120,8 +206,8 @@ def main():
     rlc_state = {"ok": True}
 
     def step_rlc():
-        partial, ok = gpu.verify_batch_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status, weight_seed,
-                                              first_index=rank * n, stream=stream, **cx)
+        partial, ok = gpu.verify_batch_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status, WEIGHT_SEED,
+                                              first_index=lo, stream=stream, **cx)
         if world > 1:
             parts = all_gather_partials(partial)
             total, ident = gpu.combine_partials(parts)
@@ -134,9 +220,10 @@ def main():
         step()
     torch.cuda.synchronize(dev)
     n_bad = int((status != 0).sum().item())
-    if n_bad:
+    if n_bad or not rlc_state["ok"]:
         raise SystemExit("bench: %d of %d valid synthetic proofs rejected -- refusing to report" % (n_bad, n))
 
+    status.fill_(0xFF)  # the timed steps must write every entry (checked below)
     gpu.set_timing(True)
     gpu.stage_times()  # reset
     if world > 1:
@@ -155,15 +242,20 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    # the timed steps must also have verified everything
     n_bad = int((status != 0).sum().item())
     if n_bad or not rlc_state["ok"]:
-        raise SystemExit("bench: %d proofs rejected in the timed region" % n_bad)
+        raise SystemExit("bench: %d proofs rejected (or not written) in the timed region" % n_bad)
 
+    oc = _load_json("bench/opcount.json") or {}
+    peak_mad = oc.get("peaks", {}).get("v_mad_i64_i32_lane_ops_per_s", 28.32e12)
+    solo = world == 1
+
+    # -- extras at N = 1 ------------------------------------------------------------------
     rlc_extra = None
-    if args.mode == "each" and world == 1 and args.rlc_extra:
+    if args.mode == "each" and solo and extra(args.rlc_extra):
         for _ in range(2):
             step_rlc()
+        status.fill_(0xFF)
         gpu.set_timing(True)
         gpu.stage_times()
         torch.cuda.synchronize(dev)
@@ -174,17 +266,91 @@ def main():
         r_el = time.perf_counter() - r0
         r_st = gpu.stage_times()
         gpu.set_timing(False)
-        if not rlc_state["ok"]:
+        if not rlc_state["ok"] or int((status != 0).sum().item()):
             raise SystemExit("bench: RLC batch check rejected a valid batch")
         rlc_extra = {"workload": "configs[2]: RLC batch check of the same 2^20 proofs (Pippenger, 16-bit windows)",
                      "proofs_per_s": n * args.steps / r_el, "ms_per_step": r_el * 1e3 / args.steps,
-                     "kernel_ms_per_step": {k: v[0] / args.steps for k, v in r_st.items()}}
+                     "roofline": rlc_roofline(r_st, n, args.steps, oc)}
+
+    c5 = None
+    if args.mode == "each" and solo and args.extras and args.c5_n:
+        n5, nf = args.c5_n, max(1, args.c5_n // 1000)
+        t5 = {k: torch.empty((n5, 32), dtype=torch.uint8, device=dev) for k in t}
+        gpu.prove_synthetic_device(n5, SEED_X, SEED_K, t5["y1"], t5["y2"], t5["r1"], t5["r2"], t5["s"], stream=stream)
+        idx = np.sort(np.random.default_rng(2024).choice(n5, size=nf, replace=False))
+        bump, swap = idx[0::2], idx[1::2]
+        _bump_s(torch, t5, bump)
+        dst = torch.from_numpy(swap.astype(np.int64)).to(dev)
+        src = torch.from_numpy(((swap + 7) % n5).astype(np.int64)).to(dev)
+        t5["y1"].index_copy_(0, dst, t5["y1"].index_select(0, src).clone())
+        st5 = torch.empty(n5, dtype=torch.uint8, device=dev)
+        gpu.verify_batch_device(*(t5[k] for k in ("y1", "y2", "r1", "r2", "s")), st5, WEIGHT_SEED, fallback=True,
+                                stream=stream)  # warm-up (allocations)
+        st5.fill_(0xFF)
+        gpu.set_timing(True)
+        gpu.stage_times()
+        torch.cuda.synchronize(dev)
+        c0 = time.perf_counter()
+        partial, ok = gpu.verify_batch_device(*(t5[k] for k in ("y1", "y2", "r1", "r2", "s")), st5, WEIGHT_SEED,
+                                              fallback=True, stream=stream)
+        torch.cuda.synchronize(dev)
+        c_el = time.perf_counter() - c0
+        c_st = gpu.stage_times()
+        got = st5.cpu().numpy()
+        exact = (not ok) and np.array_equal(np.nonzero(got)[0], idx) and set(got[idx].tolist()) == {1}
+        if not exact:
+            raise SystemExit("bench: C5 fallback did not return exactly the forged set")
+        st5.fill_(0xFF)
+        torch.cuda.synchronize(dev)
+        p0 = time.perf_counter()
+        gpu.verify_each_device(*(t5[k] for k in ("y1", "y2", "r1", "r2", "s")), st5, stream=stream)
+        torch.cuda.synchronize(dev)
+        p_el = time.perf_counter() - p0
+        gpu.set_timing(False)
+        pp = st5.cpu().numpy()
+        if not np.array_equal(pp, got):
+            raise SystemExit("bench: C5 per-proof statuses differ from the fallback's")
+        ms = {k: v[0] for k, v in c_st.items()}
+        c5 = {"workload": "configs[4]: %d proofs, %d forged (half s+1, half wrong y1), RLC batch check + fallback "
+                          "(density probe, then per-proof on prepared points) -> exact invalid set" % (n5, nf),
+              "proofs": n5, "forged": nf, "ms": c_el * 1e3, "proofs_per_s": n5 / c_el, "exact_set": True,
+              "phase_ms": {"challenge": ms.get("challenge", 0.0), "rlc_prepare": ms.get("rlc_prepare", 0.0),
+                           "rlc_msm": ms.get("rlc_msm", 0.0), "fallback_per_proof": ms.get("fallback", 0.0)},
+              "per_proof_only_ms": p_el * 1e3,
+              "note": "per_proof_only_ms: cpz_verify_each of the same batch (same statuses); the batch path "
+                      "pays its challenge + prepare + one MSM before the failure is known"}
+        del t5, st5
+        torch.cuda.empty_cache()
+
+    prove = None
+    if args.mode == "each" and solo and args.extras:
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(77)
+        xk = [torch.randint(0, 256, (n, 32), dtype=torch.int32, device=dev, generator=gen).to(torch.uint8)
+              for _ in range(2)]
+        outs = {k: torch.empty((n, 32), dtype=torch.uint8, device=dev) for k in t}
+        gpu.prove_device(xk[0], xk[1], *(outs[k] for k in ("y1", "y2", "r1", "r2", "s")), stream=stream)
+        torch.cuda.synchronize(dev)
+        psteps = max(1, min(args.steps, 5))
+        q0 = time.perf_counter()
+        for _ in range(psteps):
+            gpu.prove_device(xk[0], xk[1], *(outs[k] for k in ("y1", "y2", "r1", "r2", "s")), stream=stream)
+        torch.cuda.synchronize(dev)
+        q_el = time.perf_counter() - q0
+        status.fill_(0xFF)
+        gpu.verify_each_device(*(outs[k] for k in ("y1", "y2", "r1", "r2", "s")), status, stream=stream)
+        torch.cuda.synchronize(dev)
+        if int((status != 0).sum().item()):
+            raise SystemExit("bench: generated proofs do not verify")
+        rate = n * psteps / q_el
+        prove = {"workload": "cpz_prove_device: %d proofs from random caller witnesses / nonces (prover/mod.rs:86-131)"
+                             % n, "proofs_per_s": rate, "us_per_proof": 1e6 / rate,
+                 "published_us_per_proof": 144.0, "published_source": "src/lib.rs:55 (M-series Mac, one core)",
+                 "all_verified": True}
+        del outs, xk
 
     host_e2e = None
-    if args.mode == "each" and world == 1 and args.host_e2e:
-        # The drop-in boundary hands over HOST buffers (cpz_verify_each): time that path too,
-        # PCIe copies of 160 B/proof included (overlapped with the kernels chunk by chunk).
-        # Reported beside value, never as value.
+    if args.mode == "each" and solo and extra(args.host_e2e):
         hrows = {k: t[k].cpu().numpy() for k in t}
         hst = gpu.verify_each(hrows["y1"], hrows["y2"], hrows["r1"], hrows["r2"], hrows["s"])
         steps_h = max(1, min(args.steps, 5))
@@ -198,53 +364,72 @@ def main():
                     "proofs_per_s": n * steps_h / h_el, "ms_per_call": h_el * 1e3 / steps_h, "calls": steps_h}
         del hrows
 
-    total = world * n * args.steps
-    value = total / elapsed
+    value = total_proofs * args.steps / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
-    oc = _load_json("bench/opcount.json") or {}
-    mads = oc.get("verify_each", {}).get("mads_per_proof", 490660)
-    peak_mad = oc.get("peaks", {}).get("v_mad_u64_u32_lane_ops_per_s", 25.35e12)
+    mads = oc.get("verify_each", {}).get("mads_per_proof", 342380)
     v_ms, v_cnt = stages.get("verify_each", (0.0, 0))
     c_ms, c_cnt = stages.get("challenge", (0.0, 0))
-    v_avg_s = (v_ms / v_cnt) * 1e-3 if v_cnt else None
-    # The runtime cuts a batch into launches of half the occupancy grid (2^16 proofs on
-    # MI355X) on two streams, so two launches are always in flight and their durations
-    # overlap: achieved = algorithmic MADs of the step's verify work / the verify span
-    # (first launch start to last launch end, HIP events on the launch stream).
+    # The runtime cuts a batch into launches of half the occupancy grid (2^16 proofs) on two
+    # streams, so two launches are always in flight and their durations overlap: achieved =
+    # algorithmic MADs of the step's verify work / the verify span (first launch start to last
+    # launch end, HIP events on the launch stream).
     per_launch = (n * args.steps / v_cnt) if v_cnt else None
     sp_ms, sp_cnt = stages.get("verify_span", (0.0, 0))
     span_s = (sp_ms / args.steps) * 1e-3 if sp_cnt else None
-    achieved = (mads * n / span_s) / 1e12 if span_s else None
-    pmc = _load_json("profiles/r01_verify_each_pmc.json") or {}
-    roofline = {
-        "kernel": "k_verify_each",
-        "bound": "valu-int",
-        "achieved": achieved,
-        "peak": peak_mad / 1e12,
-        "unit": "Tmad/s",
-        "frac": (achieved / (peak_mad / 1e12)) if achieved else None,
-        "traffic": pmc.get("hbm_bytes_per_launch"),
-        "algorithmic_mads_per_proof": mads,
-        "kernel_ms": v_ms / v_cnt if v_cnt else None,
-        "proofs_per_launch": per_launch,
-        "launches_in_flight": 2,
-        "verify_span_ms_per_step": sp_ms / args.steps if sp_cnt else None,
-        "span_covers": "all k_verify_each launches of a step and the per-chunk challenge launches between them",
-        "challenge_kernel_ms": c_ms / c_cnt if c_cnt else None,
-        "hbm_frac": ((194 * n / span_s) / 8.0e12) if span_s else None,
-    }
+    pmc = _profile("verify_each_pmc")
+    if args.mode == "each":
+        achieved = (mads * n / span_s) / 1e12 if span_s else None
+        roofline = {
+            "kernel": "k_verify_each",
+            "bound": "valu-int",
+            "achieved": achieved,
+            "peak": peak_mad / 1e12,
+            "unit": "Tmad/s",
+            "frac": (achieved / (peak_mad / 1e12)) if achieved else None,
+            "traffic": pmc.get("hbm_bytes_per_launch"),
+            "traffic_per_proof": pmc.get("hbm_bytes_per_proof"),
+            "traffic_source": pmc.get("source"),
+            "peak_source": oc.get("peaks", {}).get("source"),
+            "frac_vs_2p4ghz_spec": (achieved / (oc["peaks"]["v_mad_spec_lane_ops_per_s_at_2p4ghz"] / 1e12))
+            if achieved and "v_mad_spec_lane_ops_per_s_at_2p4ghz" in oc.get("peaks", {}) else None,
+            "algorithmic_mads_per_proof": mads,
+            "kernel_ms": v_ms / v_cnt if v_cnt else None,
+            "proofs_per_launch": per_launch,
+            "launches_in_flight": 2,
+            "verify_span_ms_per_step": sp_ms / args.steps if sp_cnt else None,
+            "span_covers": "all k_verify_each launches of a step and the per-chunk challenge launches between them",
+            "challenge_kernel_ms": c_ms / c_cnt if c_cnt else None,
+            "hbm_frac": ((194 * n / span_s) / 8.0e12) if span_s else None,
+        }
+    else:
+        rr = rlc_roofline(stages, n, args.steps, oc)
+        pk = rr.get("k_rlc_prepare", {})
+        roofline = {"kernel": "k_rlc_prepare (the RLC step's largest kernel; k_rlc_bucket below)",
+                    "bound": "valu-int", "achieved": pk.get("achieved"), "peak": peak_mad / 1e12, "unit": "Tmad/s",
+                    "frac": pk.get("frac"), "traffic": None, "rlc": rr}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    if rank == 0 and solo and not args.no_cpu_baseline:
+        th = cpu_threads(args.cpu_threads)
         sample = 1 << 14
         rows = {k: t[k][:sample].cpu().numpy() for k in t}
-        cpu = cpu_baseline(rows, args.cpu_seconds, threads)
+        cpu = cpu_baseline(rows, args.cpu_seconds, th["threads"])
+        if cpu:
+            cpu["affinity_cpus"] = th["affinity_cpus"]
+            cpu["omp_num_threads"] = th["omp_num_threads"]
 
     if rank == 0:
+        if args.mode == "each":
+            workload = ("configs[1]: per-proof verification (challenge + 2 equations), %d proofs per GPU" % n
+                        if scaling == "weak" else
+                        "per-proof verification of %d proofs split over %d GPUs" % (total_proofs, world))
+        else:
+            workload = ("configs[2]/[3]: RLC batch check via Pippenger MSM, %d proofs %s, per-rank 32-B partial + "
+                        "all-gather + combine" % (total_proofs if scaling == "strong" else n,
+                                                  "split over the GPUs" if scaling == "strong" else "per GPU"))
         line = {
-            "metric": "verified proofs/sec (1/2/4/8 MI355X) + % int-VALU roofline vs host-CPU",
+            "metric": METRIC,
             "value": value,
             "unit": "proofs/s",
             "n_gpus": world,
@@ -252,24 +437,26 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "int32/int64 limbs (GF(2^255-19), radix 2^25.5)",
             "data": "synthetic (GPU prover, ChaCha20-derived witnesses; all proofs valid, checked)",
-            "config": {"workload": "configs[1]: 2^20 proofs per GPU, per-proof verification (challenge + 2 equations)",
+            "config": {"workload": workload,
+                       "proofs_total": total_proofs,
                        "proofs_per_gpu": n,
                        "contexts": ("%d random bytes per proof" % args.ctx_len) if args.ctx_len else "none",
                        "generators": "default (g, h)",
-                       "parallelism": "dp%d (independent shards, no collective)" % world},
+                       "parallelism": "dp%d (contiguous shards%s)" % (
+                           world, ", no collective" if args.mode == "each" else ", all-gather of 32-B partials")},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
-        if args.mode == "rlc":
-            line["config"]["workload"] = ("configs[2]/[3]: RLC batch check via Pippenger MSM, 2^20 proofs per GPU, "
-                                          "per-rank 32-B partial + all-gather + combine")
-            line["roofline"] = None
         if rlc_extra:
             line["rlc"] = rlc_extra
+        if c5:
+            line["c5"] = c5
+        if prove:
+            line["prove"] = prove
         if host_e2e:
             line["host_e2e"] = host_e2e
         print(json.dumps(line), flush=True)

@@ -34,7 +34,7 @@ EXPORTED = (
     "cpz_parse_proofs", "cpz_parse_proofs_device", "cpz_verify_each_multi", "cpz_verify_batch_multi",
     "cpz_verify_response", "cpz_verify_response_device", "cpz_prove", "cpz_prove_device", "cpz_decode_points",
 )
-NUM_STAGES = 8
+NUM_STAGES = 16
 
 
 class CpzError(RuntimeError):

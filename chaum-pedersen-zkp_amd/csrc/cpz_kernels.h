@@ -82,6 +82,9 @@ struct VerifyArgs {
   uint8_t* status;               // in: response-scalar status; out: final status
   const ge_niels* comb;          // fixed-base combs of g then h, kCombPerBase entries each
   char* scratch;                 // table slab: grid * kVerifyBlock threads x kCachedEntries ge_cached
+  const ge_niels* pre = nullptr; // RLC fallback: the prepared Niels points (-r1, -y1, -r2, -y2 of
+                                 // proof i at 4 i ..), reused instead of decoding; entries whose
+                                 // decode-level status is non-zero keep it
 };
 
 struct ProveArgs {

@@ -97,6 +97,7 @@ CPZ_HD fe FE_SQRT_M1() { return fe_const(34513072, 25610706, 9377949, 3500415, 1
 CPZ_HD fe FE_INVSQRT_A_MINUS_D() { return fe_const(6111466, 4156064, 39310137, 12243467, 41204824, 120896, 20826367, 26493656, 6093567, 31568420); }
 CPZ_HD fe FE_SQRT_AD_MINUS_ONE() { return fe_const(24849947, 33400850, 43495378, 6347714, 46036536, 32887293, 41837720, 18186727, 66238516, 14525638); }
 CPZ_HD fe FE_ONE_MINUS_D_SQ() { return fe_const(6275446, 16937061, 44170319, 29780721, 11667076, 7397348, 39186143, 1766194, 42675006, 672202); }
+CPZ_HD fe FE_INV2() { return fe_const(10, 0, 0, 0, 0, 0, 0, 0, 0, -16777216); }  // (p + 1) / 2
 CPZ_HD fe FE_D_MINUS_ONE_SQ() { return fe_const(15551776, 22456977, 53683765, 23429360, 55212328, 10178283, 40474537, 4729243, 61826754, 23438029); }
 
 CPZ_HD fe fe_add(const fe& a, const fe& b) {

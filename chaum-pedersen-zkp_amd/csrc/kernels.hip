@@ -329,6 +329,24 @@ __device__ __forceinline__ void verify_one_row(const VerifyArgs& a, int64_t i, c
                              comb_h, tab, dig, kVerifyBlock);
 }
 
+// The RLC fallback's per-proof pass (rlc_fallback): points, challenges and decode-level
+// statuses come from the RLC prepare of the same batch, so only the equations are checked.
+__global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_prepared(VerifyArgs a) {
+  const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
+  const int64_t gtid = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * kVerifyBlock;
+  const SlabTable tab{a.scratch, (uint32_t)gtid * (uint32_t)(kCachedEntries * sizeof(ge_cached)), 16u};
+  __shared__ uint32_t dig[16 * kVerifyBlock];
+  for (int64_t i = gtid; i < a.n; i += stride) {
+    if (a.status[i] != kStOk) continue;  // decode-level rejection: already final
+    uint32_t sw[8], cw[8];
+    load_words8(sw, a.s, i);
+    load_words8(cw, a.c, i);
+    a.status[i] = verify_proof<true>(nullptr, nullptr, nullptr, nullptr, sw, cw, kStOk, comb_g, comb_h, tab,
+                                     dig + threadIdx.x, kVerifyBlock, a.pre + 4 * i);
+  }
+}
+
 __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each(VerifyArgs a) {
   const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
   const int64_t gtid = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
@@ -493,7 +511,10 @@ int verify_each_blocks_per_cu() {
 
 hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_verify_each, dim3(grid), dim3(kVerifyBlock), 0, st, a);
+  if (a.pre)
+    hipLaunchKernelGGL(k_verify_prepared, dim3(grid), dim3(kVerifyBlock), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_verify_each, dim3(grid), dim3(kVerifyBlock), 0, st, a);
   return hipGetLastError();
 }
 

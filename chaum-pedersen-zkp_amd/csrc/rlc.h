@@ -63,8 +63,12 @@ struct RlcMsmArgs {
 hipError_t launch_rlc_prepare(const RlcPrepArgs& a, hipStream_t st);
 // Sort geometry for `npts` MSM points: sets a.groups / a.chunk.
 void rlc_sort_geometry(RlcMsmArgs& a, int64_t npts);
+// marks (optional, timing): kRlcMsmMarks events recorded on `st` at the phase boundaries
+// (start | sort: extra, hist, bscan, scan, coarse, fine | bucket | bucket fix | segment + window
+// | final).
+constexpr int kRlcMsmMarks = 6;
 hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0, int64_t b1, const ge_niels* tab,
-                          hipStream_t st);
+                          hipStream_t st, hipEvent_t* marks = nullptr);
 hipError_t launch_msm_load(int64_t n, const uint32_t* pts_enc, const uint32_t* scalars, ge_niels* pts,
                            int16_t* digits, int64_t dstride, int* bad, hipStream_t st);
 hipError_t launch_rlc_combine(const uint32_t* parts, int k, uint32_t* out, int* flags, hipStream_t st);

@@ -741,8 +741,10 @@ void rlc_sort_geometry(RlcMsmArgs& a, int64_t npts) {
 }
 
 hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0, int64_t b1, const ge_niels* tab,
-                          hipStream_t st) {
+                          hipStream_t st, hipEvent_t* marks) {
   hipError_t e;
+  auto mark = [&](int k) -> hipError_t { return marks ? hipEventRecord(marks[k], st) : hipSuccess; };
+  if ((e = mark(0)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_rlc_extra, dim3(1), dim3(256), 0, st, a, block_sums, b0, b1, tab);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const size_t lds = sizeof(uint32_t) * kRlcBuckets;  // 128 KB of the 160 KB LDS
@@ -764,18 +766,23 @@ hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0,
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_rlc_fine, dim3(kRlcCoarse, kRlcWindows), dim3(kRlcSortBlock), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = mark(1)) != hipSuccess) return e;
   const int64_t chunks = (a.istride + kRlcChunk - 1) / kRlcChunk;  // per window, upper bound
   hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((chunks + 255) / 256), kRlcWindows), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = mark(2)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_rlc_bucket_fix, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = mark(3)) != hipSuccess) return e;
   const int64_t ns = (int64_t)kRlcWindows * (kRlcBuckets / kRlcSegLen);
   hipLaunchKernelGGL(k_rlc_segment, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_rlc_window, dim3(kRlcWindows), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = mark(4)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_rlc_final, dim3(1), dim3(64), 0, st, a);
-  return hipGetLastError();
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return mark(5);
 }
 
 hipError_t launch_msm_load(int64_t n, const uint32_t* pts_enc, const uint32_t* scalars, ge_niels* pts,

@@ -320,6 +320,7 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
     v.r2 = va.r2 + 8 * a;
     v.s = va.s + 8 * a;
     v.c = va.c + 8 * a;
+    if (va.pre) v.pre = va.pre + 4 * a;
     v.status = va.status + a;
     const int k = (int)((rr ? rr->next++ : c) % nst);  // stream k owns scratch slab k
     v.scratch = static_cast<char*>(ctx->scratch.p) + (size_t)k * slab;
@@ -491,8 +492,18 @@ int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t part
   const int64_t b1 = (hi + cpz::kRlcPrepBlock - 1) / cpz::kRlcPrepBlock;
   {
     StageTimer t(ctx, 3, st);
+    // phase marks (stages 8-12) when timing: sort, bucket, bucket fix, segment + window, final
+    hipEvent_t marks[cpz::kRlcMsmMarks];
+    bool timed = ctx->timing;
+    int got = 0;
+    for (; got < cpz::kRlcMsmMarks && timed; got++) timed = (marks[got] = take_event(ctx)) != nullptr;
+    if (!timed)
+      for (int k = 0; k < got; k++)
+        if (marks[k]) ctx->free_events.push_back(marks[k]);
     CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_bsum.p), b0, b1,
-                                static_cast<const cpz::ge_niels*>(ctx->tab.p), st));
+                                static_cast<const cpz::ge_niels*>(ctx->tab.p), st, timed ? marks : nullptr));
+    if (timed)
+      for (int k = 0; k + 1 < cpz::kRlcMsmMarks; k++) ctx->marks.push_back({8 + k, marks[k], marks[k + 1]});
   }
   int flags[1];
   CPZ_HIP(hipMemcpyAsync(partial, ctx->rl_partial.p, 32, hipMemcpyDeviceToHost, st));
@@ -552,12 +563,21 @@ int rlc_prepare(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const vo
   return CPZ_OK;
 }
 
-// Batch-fail fallback: locate the invalid entries of [lo, hi) exactly.  Sub-ranges whose
-// partial is the identity are accepted (their decode-level statuses are final);
-// failing ones are split in kFanout parts, and a range is verified per proof
-// (k_verify_each) once it is small or most of its parts fail.
+// Batch-fail fallback (verify_individually, batch.rs:262-268, 314-318): locate the invalid
+// entries of [lo, hi) exactly.  Per-proof work here reuses the prepare's decoded points,
+// challenges and decode-level statuses (k_verify_prepared: the equations only).
+//   * Density probe (ranges >= kProbeMin): per-proof verification of kProbeChunks chunks of
+//     kRlcPrepBlock proofs spread over the range.  Two or more invalid entries in the probe
+//     (density >~ 1 / 2000: every 2^16-proof leaf of a bisection would fail too) -> the whole
+//     range per proof at once; C5's 0.1 % lands here.
+//   * Otherwise bisection: the range is cut in kFanout parts aligned to the weight blocks,
+//     each part's partial is one more MSM over the prepared points, identity parts are
+//     accepted, failing parts recurse; a range is verified per proof when it is <= kLeaf or
+//     when most of its parts fail.
 constexpr int64_t kLeaf = 1 << 16;
 constexpr int kFanout = 8;
+constexpr int64_t kProbeMin = 1 << 20;
+constexpr int kProbeChunks = 16;
 
 int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const void* y2, const void* r1, const void* r2,
                  const void* s, uint8_t* status, hipStream_t st, int depth) {
@@ -573,9 +593,43 @@ int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const voi
     va.status = status + a;  // decode-level status in, final status out
     va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
     va.scratch = nullptr;  // set per launch
+    va.pre = static_cast<const cpz::ge_niels*>(ctx->rl_pts.p) + 4 * a;
     return launch_verify_chunks(ctx, va, 4, st, nullptr, true);
   };
   if (hi - lo <= kLeaf || depth > 12) return per_proof(lo, hi);
+  if (depth == 0 && hi - lo >= kProbeMin) {
+    const int64_t blk = cpz::kRlcPrepBlock;
+    const int64_t span = (hi - lo) / kProbeChunks;
+    int64_t starts[kProbeChunks];
+    for (int k = 0; k < kProbeChunks; k++) {
+      starts[k] = lo + ((k * span + span / 2) / blk) * blk;
+      int rc = per_proof(starts[k], std::min(starts[k] + blk, hi));
+      if (rc) return rc;
+    }
+    std::vector<uint8_t> probe((size_t)(kProbeChunks * blk), 0);
+    for (int k = 0; k < kProbeChunks; k++) {
+      const int64_t m = std::min(starts[k] + blk, hi) - starts[k];
+      CPZ_HIP(hipMemcpyAsync(probe.data() + k * blk, status + starts[k], (size_t)m, hipMemcpyDeviceToHost, st));
+    }
+    CPZ_HIP(hipStreamSynchronize(st));
+    int bad = 0;
+    for (uint8_t v : probe) bad += (v == cpz::kStatusEqFail) ? 1 : 0;
+    if (bad >= 2) {
+      // dense: everything per proof (the probe chunks' statuses are final already; the
+      // ranges between them are verified now)
+      int64_t a = lo;
+      for (int k = 0; k < kProbeChunks; k++) {
+        if (starts[k] > a) {
+          int rc = per_proof(a, starts[k]);
+          if (rc) return rc;
+        }
+        a = std::min(starts[k] + blk, hi);
+      }
+      return a < hi ? per_proof(a, hi) : CPZ_OK;
+    }
+    // sparse: the probe chunks are verified; bisection re-verifies them harmlessly
+    // (k_verify_prepared leaves statuses that are already non-zero alone)
+  }
   int64_t cuts[kFanout + 1];
   for (int k = 0; k <= kFanout; k++) {
     int64_t c = lo + ((hi - lo) * k) / kFanout;
@@ -916,6 +970,7 @@ int cpz_ctx_stage_times(cpz_ctx* ctx, double ms_out[CPZ_NUM_STAGES], int launche
     ms_out[k] = 0.0;
     if (launches_out) launches_out[k] = 0;
   }
+  std::vector<hipEvent_t> done;  // consecutive RLC phase marks share events: return each once
   for (auto& m : ctx->marks) {
     CPZ_HIP(hipEventSynchronize(m.b));
     float ms = 0.f;
@@ -924,9 +979,12 @@ int cpz_ctx_stage_times(cpz_ctx* ctx, double ms_out[CPZ_NUM_STAGES], int launche
       ms_out[m.stage] += ms;
       if (launches_out) launches_out[m.stage] += 1;
     }
-    ctx->free_events.push_back(m.a);
-    ctx->free_events.push_back(m.b);
+    done.push_back(m.a);
+    done.push_back(m.b);
   }
+  std::sort(done.begin(), done.end());
+  done.erase(std::unique(done.begin(), done.end()), done.end());
+  ctx->free_events.insert(ctx->free_events.end(), done.begin(), done.end());
   ctx->marks.clear();
   return CPZ_OK;
 }
@@ -935,11 +993,17 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  for (auto& m : ctx->marks) {
-    (void)hipEventDestroy(m.a);
-    (void)hipEventDestroy(m.b);
+  {
+    std::vector<hipEvent_t> all(ctx->free_events);
+    for (auto& m : ctx->marks) {
+      all.push_back(m.a);
+      all.push_back(m.b);
+    }
+    std::sort(all.begin(), all.end());
+    all.erase(std::unique(all.begin(), all.end()), all.end());
+    for (auto e : all) (void)hipEventDestroy(e);
   }
-  for (auto e : ctx->free_events) (void)hipEventDestroy(e);
+  if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
   ctx->tab.release();
   ctx->comb.release();
   ctx->comb_q.release();

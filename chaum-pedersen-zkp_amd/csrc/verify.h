@@ -237,20 +237,51 @@ CPZ_HD bool challenge_masks_ctx32(uint32_t m[3][50], const uint32_t g[8], const 
 // [v s] B and [v s mod l] B differ by elements of E[4].)  [v s mod l] B comes from the
 // fixed-base comb of B (sdig: radix-2^16 digits).  Also reports whether Y and R decode
 // and whether R encodes the identity.
-template <class Comb, class Dig>
-CPZ_HD bool check_equation(const uint32_t y[8], const uint32_t r[8], const Dig& udig, const Dig& vdig, bool vneg,
-                           const Dig& sdig, const Comb& comb, const SlabTable& tab_y, const SlabTable& tab_r,
-                           bool& decoded, bool& r_identity) {
+// The affine point P from the affine Niels form of -P that the RLC prepare stores (rlc.hip):
+// -P = (-x, y), so q.ypx = y - x and q.ymx = y + x:  x = (q.ymx - q.ypx) / 2, y = (q.ypx +
+// q.ymx) / 2, T = x y (3 multiplications instead of a decode's inverse square root).
+CPZ_HD ge_p3 affine_from_neg_niels(const ge_niels& q) {
+  ge_p3 P;
+  P.X = fe_mul(fe_sub(q.ymx, q.ypx), FE_INV2());
+  P.Y = fe_mul(fe_add(q.ypx, q.ymx), FE_INV2());
+  P.Z = fe_one();
+  P.T = fe_mul(P.X, P.Y);
+  return P;
+}
+
+CPZ_HD ge_niels niels_load(const ge_niels* p) {
+  ge_niels r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint4* s = reinterpret_cast<const uint4*>(p);
+  uint4* d = reinterpret_cast<uint4*>(&r);
+#pragma unroll
+  for (int v = 0; v < (int)(sizeof(ge_niels) / 16); v++) d[v] = s[v];
+#else
+  r = *p;
+#endif
+  return r;
+}
+
+// kPre: the points were decoded already (pre_y / pre_r: Niels of -Y / -R from the RLC
+// prepare) and the entry's decode-level status is 0, so nothing is decoded here.
+template <bool kPre, class Comb, class Dig>
+CPZ_HD bool check_equation(const uint32_t y[8], const uint32_t r[8], const ge_niels* pre_y, const ge_niels* pre_r,
+                           const Dig& udig, const Dig& vdig, bool vneg, const Dig& sdig, const Comb& comb,
+                           const SlabTable& tab_y, const SlabTable& tab_r, bool& decoded, bool& r_identity) {
   // One copy of the decode + table code for both points (a rolled loop): the kernel's
   // instruction footprint, not its arithmetic, is what the 64 KB instruction cache sees.
   decoded = true;
 CPZ_EQ_LOOP
   for (int k = 0; k < 2; k++) {
     ge_p3 P;
-    decoded = ristretto_decode(P, k ? r : y) && decoded;
+    if constexpr (kPre) {
+      P = affine_from_neg_niels(niels_load(k ? pre_r : pre_y));
+    } else {
+      decoded = ristretto_decode(P, k ? r : y) && decoded;
+    }
     build_cached_table(k ? tab_r : tab_y, (k && vneg) ? P : ge_neg(P));
   }
-  r_identity = words8_zero(r);
+  r_identity = kPre ? false : words8_zero(r);
   return ristretto_is_identity(straus_half_comb(tab_y, tab_r, comb, udig, vdig, sdig));
 }
 
@@ -258,10 +289,13 @@ CPZ_EQ_LOOP
 // comb_g / comb_h: fixed-base combs of g and h; tab_v: 2 * kTableSlots entries of per-proof
 // scratch (the y table, then the r table); dig: 16 words of digit storage at stride dstride
 // (u: words 0-3, |v|: 4-7, v s mod l: 8-15).
-template <class Comb>
+// pre (kPre only): the entry's 4 prepared Niels points (-r1, -y1, -r2, -y2), st_s its
+// decode-level status, which must be 0.
+template <bool kPre = false, class Comb>
 CPZ_HD uint8_t verify_proof(const uint32_t y1[8], const uint32_t y2[8], const uint32_t r1[8], const uint32_t r2[8],
                             const uint32_t s[8], const uint32_t c[8], uint8_t st_s, const Comb& comb_g,
-                            const Comb& comb_h, const SlabTable& tab_v, uint32_t* dig, int dstride) {
+                            const Comb& comb_h, const SlabTable& tab_v, uint32_t* dig, int dstride,
+                            const ge_niels* pre = nullptr) {
   bool vneg;
   {
     uint32_t u[4], va[4], w[8];
@@ -286,8 +320,9 @@ CPZ_HD uint8_t verify_proof(const uint32_t y1[8], const uint32_t y2[8], const ui
 CPZ_EQ_LOOP
   for (int e = 0; e < 2; e++) {
     bool d, r_id;
-    eq = check_equation(e ? y2 : y1, e ? r2 : r1, udig, vdig, vneg, sdig, e ? comb_h : comb_g, tab_v,
-                        tab_v.shifted(kTableSlots), d, r_id) && eq;
+    eq = check_equation<kPre>(e ? y2 : y1, e ? r2 : r1, kPre ? pre + 1 + 2 * e : nullptr, kPre ? pre + 2 * e : nullptr,
+                              udig, vdig, vneg, sdig, e ? comb_h : comb_g, tab_v, tab_v.shifted(kTableSlots), d,
+                              r_id) && eq;
     dec = dec && d;
     id = id || r_id;
   }

@@ -238,9 +238,11 @@ int cpz_verify_batch_multi(cpz_ctx *const *ctxs, int nctx, const uint8_t g[32], 
  * Stages: 0 = k_challenge, 1 = k_verify_each, 2 = RLC decode/weights, 3 = RLC MSM,
  * 4 = fallback, 5 = the whole per-proof verify of one call (first to last k_verify_each,
  * whose launches overlap on several streams), 6 = prover (commitments / statements, then
- * challenges + responses).  cpz_ctx_stage_times synchronises, writes the summed milliseconds and
+ * challenges + responses); phases of the RLC MSM (inside stage 3): 8 = bucket sort, 9 =
+ * bucket accumulation (k_rlc_bucket), 10 = bucket fix-up, 11 = bucket reduction (segment +
+ * window), 12 = window combine + encode (k_rlc_final).  cpz_ctx_stage_times synchronises, writes the summed milliseconds and
  * launch counts per stage since the last call, and resets them. */
-#define CPZ_NUM_STAGES 8
+#define CPZ_NUM_STAGES 16
 int cpz_ctx_set_timing(cpz_ctx *ctx, int enable);
 int cpz_ctx_stage_times(cpz_ctx *ctx, double ms_out[CPZ_NUM_STAGES], int launches_out[CPZ_NUM_STAGES]);
 

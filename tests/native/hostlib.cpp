@@ -261,6 +261,60 @@ int cpzt_verify_opcount(unsigned long long* mul, unsigned long long* sq, const u
   return st;
 }
 
+// Field-op counts of the RLC path's per-unit work (rlc.hip), for bench.py's roofline:
+//   which = 0: k_rlc_prepare per proof -- 4 decodes + the Niels conversion of each (1 M);
+//   which = 1: k_rlc_bucket per sorted entry -- one p1p1 -> p3 conversion + one mixed
+//              (affine Niels) addition;
+//   which = 2: k_verify_prepared per proof (the fallback's per-proof pass) -- the equations
+//              with the points rebuilt from the prepared Niels forms instead of decoded.
+int cpzt_rlc_opcount(int which, unsigned long long* mul, unsigned long long* sq, const uint8_t* g, const uint8_t* h,
+                     const uint8_t* y1, const uint8_t* y2, const uint8_t* r1, const uint8_t* r2, const uint8_t* s,
+                     const uint8_t* c) {
+  uint32_t w[4][8];
+  words_from(w[0], r1);
+  words_from(w[1], y1);
+  words_from(w[2], r2);
+  words_from(w[3], y2);
+  ge_niels pre[4];
+  for (int q = 0; q < 4; q++) {
+    ge_p3 P;
+    if (!ristretto_decode(P, w[q])) return -1;
+    ge_niels n;
+    n.ypx = fe_add(P.Y, P.X);
+    n.ymx = fe_sub(P.Y, P.X);
+    n.xy2d = fe_mul(P.T, FE_D2());
+    pre[q] = ge_niels_cneg(n, true);
+  }
+  unsigned long long m0, s0;
+  cpzt_opcount(&m0, &s0);
+  if (which == 0) {
+    for (int q = 0; q < 4; q++) {
+      ge_p3 P;
+      (void)ristretto_decode(P, w[q]);
+      (void)fe_mul(P.T, FE_D2());
+    }
+  } else if (which == 1) {
+    ge_p1p1 r = p1p1_identity();
+    r = ge_add_niels(p1p1_to_p3(r), pre[0]);
+    cpzt_opcount(&m0, &s0);  // one steady-state step: conversion + addition
+    r = ge_add_niels(p1p1_to_p3(r), pre[1]);
+  } else {
+    GenTables gt;
+    if (!gt.build(g, h)) return -1;
+    cpzt_opcount(&m0, &s0);
+    uint32_t sw[8], cw[8], dig[16];
+    words_from(sw, s);
+    words_from(cw, c);
+    ge_cached tv[2 * kTableSlots];
+    const int st = verify_proof<true>(nullptr, nullptr, nullptr, nullptr, sw, cw, 0, gt.g, gt.h, host_table(tv), dig,
+                                      1, pre);
+    cpzt_opcount(mul, sq);
+    return st;
+  }
+  cpzt_opcount(mul, sq);
+  return 0;
+}
+
 // Full per-proof verification exactly as k_challenge + k_verify_each compute it.
 int cpzt_verify(const uint8_t* g, const uint8_t* h, const uint8_t* y1, const uint8_t* y2, const uint8_t* r1,
                 const uint8_t* r2, const uint8_t* s, const uint8_t* ctx, uint32_t ctx_len, int has_ctx) {

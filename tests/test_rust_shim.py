@@ -1,0 +1,106 @@
+"""The Rust side of the boundary (rust/): no Rust toolchain exists in this image, so the
+crates are checked mechanically -- every function and constant of include/cpz.h appears in
+the -sys crate's extern block with the same parameter list (C types mapped to their Rust
+FFI equivalents), the build script compiles exactly the HIP units the library is made of,
+and the reference-side patch contains no `unsafe` (the reference crate is
+#![forbid(unsafe_code)], src/lib.rs:64)."""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SYS = os.path.join(ROOT, "rust", "chaum-pedersen-gpu-sys")
+
+
+def _strip_c_comments(s):
+    return re.sub(r"/\*.*?\*/", "", s, flags=re.S)
+
+
+def _c_decls():
+    src = _strip_c_comments(open(os.path.join(ROOT, "include", "cpz.h")).read())
+    out = {}
+    for ret, name, args in re.findall(r"^\s*((?:const\s+)?\w+\s*\*?)\s*(cpz_\w+)\s*\((.*?)\);", src, flags=re.S | re.M):
+        args = " ".join(args.split())
+        out[name] = (" ".join(ret.split()), [] if args == "void" else [a.strip() for a in args.split(",")])
+    return out
+
+
+def _c_defines():
+    src = open(os.path.join(ROOT, "include", "cpz.h")).read()
+    return {k: int(v) for k, v in re.findall(r"#define (CPZ_\w+) \(?(-?\d+)\)?", src)}
+
+
+def _c_param_to_rust(p):
+    """(name, rust type) of one C parameter."""
+    m = re.match(r"^(const\s+)?(\w+)\s*(\*\s*const\s*\*|\*\*|\*)?\s*(\w+)(\[[^\]]*\])?$", p)
+    assert m, p
+    const, base, stars, name, arr = m.groups()
+    stars = (stars or "").replace(" ", "")
+    prim = {"uint8_t": "u8", "uint32_t": "u32", "uint64_t": "u64", "size_t": "usize", "int": "c_int",
+            "double": "f64", "void": "c_void", "cpz_ctx": "cpz_ctx"}[base]
+    if stars == "*const*":
+        return name, "*const *mut " + prim
+    if stars == "**":
+        return name, "*mut *mut " + prim
+    if stars == "*" or arr:
+        return name, ("*const " if const else "*mut ") + prim
+    return name, prim
+
+
+def _c_ret_to_rust(r):
+    return {"int": "c_int", "void": None, "const char *": "*const c_char"}[r]
+
+
+def _rust_decls():
+    src = open(os.path.join(SYS, "src", "lib.rs")).read()
+    block = src[src.index('extern "C" {'):]
+    out = {}
+    for name, args, ret in re.findall(r"pub fn (cpz_\w+)\((.*?)\)\s*(?:->\s*([^;]+))?;", block, flags=re.S):
+        args = " ".join(args.split())
+        params = [] if not args else [tuple(x.strip() for x in a.split(":", 1)) for a in args.split(",") if a.strip()]
+        out[name] = (" ".join(ret.split()) or None, params)
+    consts = {k: int(v) for k, v in re.findall(r"pub const (CPZ_\w+): \w+ = (-?\d+);", src)}
+    return out, consts
+
+
+def test_extern_block_matches_header():
+    c = _c_decls()
+    r, _ = _rust_decls()
+    assert set(c) == set(r), (sorted(set(c) - set(r)), sorted(set(r) - set(c)))
+    for name, (ret, params) in c.items():
+        rret, rparams = r[name]
+        assert rret == _c_ret_to_rust(ret), (name, ret, rret)
+        want = [_c_param_to_rust(p) for p in params]
+        assert [tuple(p) for p in rparams] == want, (name, rparams, want)
+
+
+def test_constants_match_header():
+    _, consts = _rust_decls()
+    defs = _c_defines()
+    assert set(defs) == set(consts), (sorted(set(defs) - set(consts)), sorted(set(consts) - set(defs)))
+    for k, v in defs.items():
+        assert consts[k] == v, k
+
+
+def test_build_script_compiles_the_library_units():
+    import build_native  # the in-tree recipe: the same translation units
+    b = open(os.path.join(SYS, "build.rs")).read()
+    units = re.search(r"const UNITS: \[&str; \d+\] = \[(.*?)\];", b).group(1)
+    units = [u.strip().strip('"') for u in units.split(",")]
+    csrc = os.path.join(ROOT, "chaum-pedersen-zkp_amd", "csrc")
+    assert sorted(units) == sorted(f for f in os.listdir(csrc) if f.endswith(".hip"))
+    assert "gfx950" in b and 'links = "cpz"' in open(os.path.join(SYS, "Cargo.toml")).read()
+    assert "kernels.hip" in open(build_native.__file__).read()
+
+
+def test_reference_patch_is_safe_code():
+    for rel in ("rust/reference-patch/batch_gpu.rs",):
+        src = open(os.path.join(ROOT, rel)).read()
+        code = "\n".join(l.split("//")[0] for l in src.splitlines())
+        assert "unsafe" not in code, rel
+    wrap = open(os.path.join(ROOT, "rust", "chaum-pedersen-gpu", "src", "lib.rs")).read()
+    # every unsafe block in the safe wrapper carries a SAFETY note
+    lines = wrap.splitlines()
+    for i, l in enumerate(lines):
+        if "unsafe {" in l and "impl" not in l:
+            ctx = "\n".join(lines[max(0, i - 3):i + 1])
+            assert "SAFETY" in ctx, (i, l)
