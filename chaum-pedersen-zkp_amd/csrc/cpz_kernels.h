@@ -85,6 +85,10 @@ struct VerifyArgs {
   const ge_niels* pre = nullptr; // RLC fallback: the prepared Niels points (-r1, -y1, -r2, -y2 of
                                  // proof i at 4 i ..), reused instead of decoding; entries whose
                                  // decode-level status is non-zero keep it
+  const uint32_t* fused = nullptr;  // non-null: no contexts and the fixed challenge schedule applies;
+                                    // the kernel computes c and the response status itself from these
+                                    // 100 words (prefix ^ k1, then k2: challenge_fixed's constants)
+                                    // instead of reading c / status from k_challenge
 };
 
 struct ProveArgs {

@@ -318,44 +318,77 @@ __global__ void __launch_bounds__(256) k_parse_proofs(ParseArgs a) {
 #ifndef CPZ_VERIFY_WAVES
 #define CPZ_VERIFY_WAVES 2  // waves per SIMD (256 VGPRs each)
 #endif
+// The proof's four point encodings are staged in LDS (one word column per thread): they are
+// read once per decode, and no row address has to stay live across the Straus loops.
 __device__ __forceinline__ void verify_one_row(const VerifyArgs& a, int64_t i, const CombTable& comb_g,
-                                               const CombTable& comb_h, const SlabTable& tab, uint32_t* dig) {
-  // Rows are read where they are consumed (decode just before each equation) so only one
-  // decoded point is live at a time.
+                                               const CombTable& comb_h, const SlabTable& tab, uint32_t* dig,
+                                               uint32_t* rows) {
+  const uint32_t* src[4] = {a.y1, a.y2, a.r1, a.r2};
   uint32_t sw[8], cw[8];
-  load_words8(sw, a.s, i);
-  load_words8(cw, a.c, i);
-  a.status[i] = verify_proof(a.y1 + 8 * i, a.y2 + 8 * i, a.r1 + 8 * i, a.r2 + 8 * i, sw, cw, a.status[i], comb_g,
-                             comb_h, tab, dig, kVerifyBlock);
+  uint8_t st_s;
+  if (a.fused) {
+    // the challenge and the response checks here, from the rows being staged (no k_challenge
+    // launch, no c round trip through HBM)
+    uint32_t w[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      load_words8(w[q], src[q], i);
+#pragma unroll
+      for (int k = 0; k < 8; k++) rows[(8 * q + k) * kVerifyBlock] = w[q][k];
+    }
+    load_words8(sw, a.s, i);
+    const sc c = challenge_fixed_pk(a.fused, a.fused + 50, w[0], w[1], w[2], w[3]);
+#pragma unroll
+    for (int k = 0; k < 8; k++) cw[k] = c.w[k];
+    st_s = response_status(sw);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      uint32_t w[8];
+      load_words8(w, src[q], i);
+#pragma unroll
+      for (int k = 0; k < 8; k++) rows[(8 * q + k) * kVerifyBlock] = w[k];
+    }
+    load_words8(sw, a.s, i);
+    load_words8(cw, a.c, i);
+    st_s = a.status[i];
+  }
+  const DigitRef y1{rows, kVerifyBlock}, y2{rows + 8 * kVerifyBlock, kVerifyBlock},
+      r1{rows + 16 * kVerifyBlock, kVerifyBlock}, r2{rows + 24 * kVerifyBlock, kVerifyBlock};
+  a.status[i] = verify_proof(y1, y2, r1, r2, sw, cw, st_s, comb_g, comb_h, tab, dig, kVerifyBlock);
 }
 
 // The RLC fallback's per-proof pass (rlc_fallback): points, challenges and decode-level
 // statuses come from the RLC prepare of the same batch, so only the equations are checked.
 __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_prepared(VerifyArgs a) {
   const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
-  const int64_t gtid = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
-  const int64_t stride = (int64_t)gridDim.x * kVerifyBlock;
-  const SlabTable tab{a.scratch, (uint32_t)gtid * (uint32_t)(kCachedEntries * sizeof(ge_cached)), 16u};
+  const int64_t i = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;  // one proof per thread
+  if (i >= a.n) return;
+  const SlabTable tab{a.scratch, (uint32_t)i * (uint32_t)(kCachedEntries * sizeof(ge_cached)), 16u};
   __shared__ uint32_t dig[16 * kVerifyBlock];
-  for (int64_t i = gtid; i < a.n; i += stride) {
-    if (a.status[i] != kStOk) continue;  // decode-level rejection: already final
+  {
+    if (a.status[i] != kStOk) return;  // decode-level rejection: already final
     uint32_t sw[8], cw[8];
     load_words8(sw, a.s, i);
     load_words8(cw, a.c, i);
-    a.status[i] = verify_proof<true>(nullptr, nullptr, nullptr, nullptr, sw, cw, kStOk, comb_g, comb_h, tab,
-                                     dig + threadIdx.x, kVerifyBlock, a.pre + 4 * i);
+    const DigitRef none{nullptr, 0};
+    a.status[i] = verify_proof<true>(none, none, none, none, sw, cw, kStOk, comb_g, comb_h, tab, dig + threadIdx.x,
+                                     kVerifyBlock, a.pre + 4 * i);
   }
 }
 
 __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each(VerifyArgs a) {
   const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
-  const int64_t gtid = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
-  const int64_t stride = (int64_t)gridDim.x * kVerifyBlock;
+  // one proof per thread: the runtime cuts a batch into launches of at most grid x block
+  // proofs (launch_verify_chunks), so there is no grid-stride loop state to keep live
+  const int64_t i = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
+  if (i >= a.n) return;
   // this thread's tables: kCachedEntries entries, contiguous (scalarmul.h, SlabTable)
-  const SlabTable tab{a.scratch, (uint32_t)gtid * (uint32_t)(kCachedEntries * sizeof(ge_cached)), 16u};
-  // digit words in LDS, one column per thread (scalarmul.h, DigitRef)
+  const SlabTable tab{a.scratch, (uint32_t)i * (uint32_t)(kCachedEntries * sizeof(ge_cached)), 16u};
+  // digit words and point encodings in LDS, one column per thread (scalarmul.h, DigitRef)
   __shared__ uint32_t dig[16 * kVerifyBlock];
-  for (int64_t i = gtid; i < a.n; i += stride) verify_one_row(a, i, comb_g, comb_h, tab, dig + threadIdx.x);
+  __shared__ uint32_t rows[32 * kVerifyBlock];
+  verify_one_row(a, i, comb_g, comb_h, tab, dig + threadIdx.x, rows + threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -90,6 +90,7 @@ struct cpz_ctx {
   DevBuf prefix;    // 2 StrobeSnap
   bool prefix_fixed = false;  // prefix[1] at the fixed position: k_challenge_noctx applies
   uint32_t chal_k1[50], chal_k2[50];  // its framing masks
+  DevBuf chal_fused;          // prefix[1] ^ k1, k2 (100 words): the challenge fused into k_verify_each
   bool ctx32_fixed = false;   // prefix[0] at the fixed position: 32-byte contexts' fast path
   uint32_t chal_c32[3][50];   // its framing masks (g and h folded in)
   DevBuf gh_words;  // 16 words
@@ -111,6 +112,10 @@ struct cpz_ctx {
   hipEvent_t aux_done[3] = {nullptr, nullptr, nullptr};
   // wire-format ingestion
   DevBuf pz_blob, pz_off, pz_rows, pz_code, pz_aux;
+  // batch-check density probe (verify_batch_impl): sampled rows, challenges, statuses
+  DevBuf probe;
+  hipStream_t probe_stream = nullptr;
+  hipEvent_t probe_done = nullptr;
   // RLC / Pippenger buffers (sized for the largest batch seen)
   DevBuf rl_pts, rl_dig, rl_bsum, rl_counts, rl_offsets, rl_bhist, rl_idx, rl_inter, rl_buckets, rl_heads, rl_segs,
       rl_segw, rl_win,
@@ -211,6 +216,16 @@ int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32]) {
   CPZ_HIP(hipMemcpyAsync(snap, ctx->prefix.p, sizeof(snap), hipMemcpyDeviceToHost, ctx->stream));
   CPZ_HIP(hipStreamSynchronize(ctx->stream));
   ctx->prefix_fixed = cpz::challenge_prefix_is_fixed(snap[1]) && cpz::challenge_masks(ctx->chal_k1, ctx->chal_k2);
+  if (ctx->prefix_fixed) {
+    uint32_t fw[100];
+    std::memcpy(fw, snap[1].state, 200);
+    for (int w = 0; w < 50; w++) {
+      fw[w] ^= ctx->chal_k1[w];
+      fw[50 + w] = ctx->chal_k2[w];
+    }
+    CPZ_HIP(ctx->chal_fused.ensure(sizeof(fw)));
+    CPZ_HIP(hipMemcpy(ctx->chal_fused.p, fw, sizeof(fw), hipMemcpyHostToDevice));
+  }
   {
     uint32_t gw[16];
     words_from_bytes(gw, g, h);
@@ -263,6 +278,9 @@ int verify_grid(cpz_ctx* ctx, size_t n) {
 // 4 / half 51.5 M, 3 / third 47.3 M, 4 / quarter 48.8 M.
 // Challenges per verify chunk on the chunk's stream (hidden under the other stream's verify
 // work; +0.5-1.1 % A/B on one box against one up-front challenge launch).
+#ifndef CPZ_VERIFY_FUSED
+#define CPZ_VERIFY_FUSED 1  // no-context challenges computed inside k_verify_each
+#endif
 #ifndef CPZ_CHALLENGE_PER_CHUNK
 #define CPZ_CHALLENGE_PER_CHUNK 1
 #endif
@@ -390,6 +408,14 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
   va.scratch = nullptr;  // set per launch
   StageTimer span(ctx, 5, st);  // all chunks, all streams (the launches overlap)
+#if CPZ_VERIFY_FUSED
+  if (ca.ctx_off == nullptr && ctx->prefix_fixed) {
+    // no contexts on the fixed schedule: k_verify_each computes c and the response status
+    // itself (c_buf is left unwritten; no caller reads it after a verify)
+    va.fused = static_cast<const uint32_t*>(ctx->chal_fused.p);
+    return launch_verify_chunks(ctx, va, 1, st, rr, join);
+  }
+#endif
 #if CPZ_CHALLENGE_PER_CHUNK
   return launch_verify_chunks(ctx, va, 1, st, rr, join, &ca);
 #else
@@ -580,7 +606,7 @@ constexpr int64_t kProbeMin = 1 << 20;
 constexpr int kProbeChunks = 16;
 
 int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const void* y2, const void* r1, const void* r2,
-                 const void* s, uint8_t* status, hipStream_t st, int depth) {
+                 const void* s, uint8_t* status, hipStream_t st, int depth, bool allow_probe = true) {
   auto per_proof = [&](int64_t a, int64_t b) -> int {
     cpz::VerifyArgs va;
     va.n = b - a;
@@ -597,7 +623,7 @@ int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const voi
     return launch_verify_chunks(ctx, va, 4, st, nullptr, true);
   };
   if (hi - lo <= kLeaf || depth > 12) return per_proof(lo, hi);
-  if (depth == 0 && hi - lo >= kProbeMin) {
+  if (depth == 0 && allow_probe && hi - lo >= kProbeMin) {
     const int64_t blk = cpz::kRlcPrepBlock;
     const int64_t span = (hi - lo) / kProbeChunks;
     int64_t starts[kProbeChunks];
@@ -657,12 +683,78 @@ int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const voi
   return CPZ_OK;
 }
 
+// The density probe of a fallback-enabled batch check, launched BEFORE the prepare on its own
+// stream so that it runs beside it: per-proof verification (challenge + k_verify_each) of
+// kProbeChunks chunks of kRlcPrepBlock proofs spread over the batch, gathered into a small
+// buffer.  Returns the number of chunk starts (0: no probe).
+int launch_probe(cpz_ctx* ctx, size_t n, const void* const rows[5], int64_t starts[kProbeChunks], hipStream_t st) {
+  const int64_t blk = cpz::kRlcPrepBlock;
+  const size_t m = (size_t)kProbeChunks * blk;
+  CPZ_HIP(ctx->probe.ensure(m * (5 * 32 + 32 + 1)));
+  if (!ctx->probe_stream) CPZ_HIP(hipStreamCreateWithFlags(&ctx->probe_stream, hipStreamNonBlocking));
+  if (!ctx->probe_done) CPZ_HIP(hipEventCreateWithFlags(&ctx->probe_done, hipEventDisableTiming));
+  if (!ctx->aux_start) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_start, hipEventDisableTiming));
+  CPZ_HIP(hipEventRecord(ctx->aux_start, st));  // after everything before this call on st
+  CPZ_HIP(hipStreamWaitEvent(ctx->probe_stream, ctx->aux_start, 0));
+  uint8_t* base = static_cast<uint8_t*>(ctx->probe.p);
+  const int64_t span = (int64_t)n / kProbeChunks;
+  for (int k = 0; k < kProbeChunks; k++) {
+    starts[k] = ((k * span + span / 2) / blk) * blk;
+    for (int q = 0; q < 5; q++)
+      CPZ_HIP(hipMemcpyAsync(base + (q * m + (size_t)k * blk) * 32, static_cast<const uint8_t*>(rows[q]) + starts[k] * 32,
+                             (size_t)blk * 32, hipMemcpyDeviceToDevice, ctx->probe_stream));
+  }
+  uint8_t* prow[5];
+  for (int q = 0; q < 5; q++) prow[q] = base + q * m * 32;
+  uint32_t* pc = reinterpret_cast<uint32_t*>(base + 5 * m * 32);
+  uint8_t* pst = base + 6 * m * 32;
+  int rc = enqueue_verify(ctx, m, prow[0], prow[1], prow[2], prow[3], prow[4], nullptr, nullptr, nullptr, pst,
+                          ctx->probe_stream, pc);
+  if (rc) return rc;
+  CPZ_HIP(hipEventRecord(ctx->probe_done, ctx->probe_stream));
+  return kProbeChunks;
+}
+
 int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
                       const void* s, const void* cb, const uint64_t* co, const uint8_t* cp, uint8_t* d_status,
                       const uint8_t seed[32], uint64_t first_index, uint8_t partial_out[32], int* batch_ok,
                       int fallback, uint8_t* host_status, hipStream_t st) {
+  // A fallback-enabled check of a large batch without contexts first samples its density,
+  // beside the prepare (the probe's ~2 ms of per-proof latency hides under it).  A dense
+  // batch (>= 2 invalid entries among the kProbeChunks x 256 sampled) cannot pass and
+  // bisection cannot prune it: the MSM is skipped and every entry is verified per proof on
+  // the prepared points; partial_out is then 32 x 0xff ("no partial": not an encoding).
+  int64_t starts[kProbeChunks];
+  const bool probe = fallback && co == nullptr && (int64_t)n >= kProbeMin;
+  if (probe) {
+    const void* rows[5] = {y1, y2, r1, r2, s};
+    int rc = launch_probe(ctx, n, rows, starts, st);
+    if (rc < 0) return rc;
+  }
   int rc = rlc_prepare(ctx, n, y1, y2, r1, r2, s, cb, co, cp, d_status, seed, first_index, st);
   if (rc) return rc;
+  if (probe) {
+    const size_t m = (size_t)kProbeChunks * cpz::kRlcPrepBlock;
+    std::vector<uint8_t> pst(m);
+    CPZ_HIP(hipStreamWaitEvent(st, ctx->probe_done, 0));  // the probe used scratch slab 0 too
+    CPZ_HIP(hipMemcpyAsync(pst.data(), static_cast<uint8_t*>(ctx->probe.p) + 6 * m * 32, m, hipMemcpyDeviceToHost,
+                           ctx->probe_stream));
+    CPZ_HIP(hipStreamSynchronize(ctx->probe_stream));
+    int bad = 0;
+    for (uint8_t v : pst) bad += (v == cpz::kStatusEqFail) ? 1 : 0;
+    if (bad >= 2) {
+      if (partial_out) std::memset(partial_out, 0xff, 32);
+      if (batch_ok) *batch_ok = 0;
+      rc = rlc_fallback(ctx, 0, (int64_t)n, y1, y2, r1, r2, s, d_status, st, 13, false);  // depth > 12: per proof
+      if (rc) return rc;
+      CPZ_HIP(hipStreamSynchronize(st));
+      if (host_status) {
+        CPZ_HIP(hipMemcpyAsync(host_status, d_status, n, hipMemcpyDeviceToHost, st));
+        CPZ_HIP(hipStreamSynchronize(st));
+      }
+      return CPZ_OK;
+    }
+  }
   uint8_t part[32];
   int ident = 0;
   rc = rlc_range(ctx, 0, (int64_t)n, st, part, &ident);
@@ -675,7 +767,7 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
   const bool all_live = any_bad == 0;
   if (batch_ok) *batch_ok = (ident && all_live) ? 1 : 0;
   if (!ident && fallback) {
-    rc = rlc_fallback(ctx, 0, (int64_t)n, y1, y2, r1, r2, s, d_status, st, 0);
+    rc = rlc_fallback(ctx, 0, (int64_t)n, y1, y2, r1, r2, s, d_status, st, 0, !probe);
     if (rc) return rc;
     CPZ_HIP(hipStreamSynchronize(st));  // statuses complete on return (documented)
   }
@@ -946,6 +1038,15 @@ int cpz_verify_batch_multi(cpz_ctx* const* ctxs, int nctx, const uint8_t g[32], 
                             &ok[k], status_out ? status_out + lo : nullptr);
   });
   if (rc) return rc;
+  static const uint8_t kNoPartial[32] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+                                         0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+                                         0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff};
+  for (int k = 0; k < nctx; k++)
+    if (std::memcmp(partials_out + 32 * k, kNoPartial, 32) == 0) {  // a dense shard skipped its MSM
+      std::memcpy(total_out, kNoPartial, 32);
+      *batch_ok = 0;
+      return CPZ_OK;
+    }
   int ident = 0;
   rc = cpz_combine_partials(ctxs[0], (size_t)nctx, partials_out, total_out, &ident);
   if (rc) return rc;
@@ -1018,6 +1119,12 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->ctxo.release();
   ctx->ctxp.release();
   if (ctx->copy_done) (void)hipEventDestroy(ctx->copy_done);
+  if (ctx->probe_done) (void)hipEventDestroy(ctx->probe_done);
+  if (ctx->probe_stream) {
+    (void)hipStreamSynchronize(ctx->probe_stream);
+    (void)hipStreamDestroy(ctx->probe_stream);
+  }
+  ctx->probe.release();
   if (ctx->aux_start) (void)hipEventDestroy(ctx->aux_start);
   for (auto& e : ctx->aux_done)
     if (e) (void)hipEventDestroy(e);

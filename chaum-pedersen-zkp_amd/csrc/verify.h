@@ -132,6 +132,24 @@ CPZ_HD sc challenge_fixed(const uint32_t prefix[50], const uint32_t k1[50], cons
   return sc_reduce_wide(st);  // challenge bytes 0..63 = state words 0..15
 }
 
+// challenge_fixed with the prefix and the first mask pre-combined (pk1 = prefix ^ k1): the
+// form k_verify_each uses when it computes the challenge itself.
+CPZ_HD sc challenge_fixed_pk(const uint32_t pk1[50], const uint32_t k2[50], const uint32_t y1[8], const uint32_t y2[8],
+                             const uint32_t r1[8], const uint32_t r2[8]) {
+  uint32_t st[50];
+#pragma unroll
+  for (int w = 0; w < 50; w++) st[w] = pk1[w];
+  xor_message<kTailY1>(st, y1);
+  xor_message<kTailY2>(st, y2);
+  xor_message<kTailR1>(st, r1);
+  keccak_words(st);
+#pragma unroll
+  for (int w = 0; w < 50; w++) st[w] ^= k2[w];
+  xor_message<kTailR2>(st, r2);
+  keccak_words(st);
+  return sc_reduce_wide(st);
+}
+
 // 32-byte-context tail: prefix = the state after Transcript::new, m = the three segments'
 // framing masks (challenge_masks_ctx32, g and h included), ctx = the context as 8 words.
 CPZ_HD sc challenge_fixed_ctx32(const uint32_t prefix[50], const uint32_t m[3][50], const uint32_t ctx[8],
@@ -265,7 +283,7 @@ CPZ_HD ge_niels niels_load(const ge_niels* p) {
 // kPre: the points were decoded already (pre_y / pre_r: Niels of -Y / -R from the RLC
 // prepare) and the entry's decode-level status is 0, so nothing is decoded here.
 template <bool kPre, class Comb, class Dig>
-CPZ_HD bool check_equation(const uint32_t y[8], const uint32_t r[8], const ge_niels* pre_y, const ge_niels* pre_r,
+CPZ_HD bool check_equation(const Dig& y, const Dig& r, const ge_niels* pre_y, const ge_niels* pre_r,
                            const Dig& udig, const Dig& vdig, bool vneg, const Dig& sdig, const Comb& comb,
                            const SlabTable& tab_y, const SlabTable& tab_r, bool& decoded, bool& r_identity) {
   // One copy of the decode + table code for both points (a rolled loop): the kernel's
@@ -277,11 +295,21 @@ CPZ_EQ_LOOP
     if constexpr (kPre) {
       P = affine_from_neg_niels(niels_load(k ? pre_r : pre_y));
     } else {
-      decoded = ristretto_decode(P, k ? r : y) && decoded;
+      uint32_t w[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) w[q] = k ? r[q] : y[q];
+      decoded = ristretto_decode(P, w) && decoded;
     }
     build_cached_table(k ? tab_r : tab_y, (k && vneg) ? P : ge_neg(P));
   }
-  r_identity = kPre ? false : words8_zero(r);
+  if constexpr (kPre) {
+    r_identity = false;
+  } else {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) acc |= r[q];
+    r_identity = acc == 0;
+  }
   return ristretto_is_identity(straus_half_comb(tab_y, tab_r, comb, udig, vdig, sdig));
 }
 
@@ -289,10 +317,12 @@ CPZ_EQ_LOOP
 // comb_g / comb_h: fixed-base combs of g and h; tab_v: 2 * kTableSlots entries of per-proof
 // scratch (the y table, then the r table); dig: 16 words of digit storage at stride dstride
 // (u: words 0-3, |v|: 4-7, v s mod l: 8-15).
-// pre (kPre only): the entry's 4 prepared Niels points (-r1, -y1, -r2, -y2), st_s its
-// decode-level status, which must be 0.
+// rows: the encodings y1, y2, r1, r2 (words at rows[4 q + ...], see DigitRef: the verify kernel
+// stages them in LDS so that no per-row address stays live in registers); pre (kPre only):
+// the entry's 4 prepared Niels points (-r1, -y1, -r2, -y2), st_s its decode-level status,
+// which must be 0.
 template <bool kPre = false, class Comb>
-CPZ_HD uint8_t verify_proof(const uint32_t y1[8], const uint32_t y2[8], const uint32_t r1[8], const uint32_t r2[8],
+CPZ_HD uint8_t verify_proof(const DigitRef& y1, const DigitRef& y2, const DigitRef& r1, const DigitRef& r2,
                             const uint32_t s[8], const uint32_t c[8], uint8_t st_s, const Comb& comb_g,
                             const Comb& comb_h, const SlabTable& tab_v, uint32_t* dig, int dstride,
                             const ge_niels* pre = nullptr) {

@@ -256,7 +256,8 @@ int cpzt_verify_opcount(unsigned long long* mul, unsigned long long* sq, const u
   uint32_t dig[16];
   unsigned long long m0, s0;
   cpzt_opcount(&m0, &s0);
-  const int st = verify_proof(a, b, cc, d, sw, cw, response_status(sw), gt.g, gt.h, host_table(tv), dig, 1);
+  const int st = verify_proof(host_digits(a), host_digits(b), host_digits(cc), host_digits(d), sw, cw,
+                              response_status(sw), gt.g, gt.h, host_table(tv), dig, 1);
   cpzt_opcount(mul, sq);
   return st;
 }
@@ -306,8 +307,8 @@ int cpzt_rlc_opcount(int which, unsigned long long* mul, unsigned long long* sq,
     words_from(sw, s);
     words_from(cw, c);
     ge_cached tv[2 * kTableSlots];
-    const int st = verify_proof<true>(nullptr, nullptr, nullptr, nullptr, sw, cw, 0, gt.g, gt.h, host_table(tv), dig,
-                                      1, pre);
+    const DigitRef none{nullptr, 0};
+    const int st = verify_proof<true>(none, none, none, none, sw, cw, 0, gt.g, gt.h, host_table(tv), dig, 1, pre);
     cpzt_opcount(mul, sq);
     return st;
   }
@@ -331,7 +332,8 @@ int cpzt_verify(const uint8_t* g, const uint8_t* h, const uint8_t* y1, const uin
   words_from(cw, cb);
   ge_cached tv[2 * kTableSlots];
   uint32_t dig[16];
-  return verify_proof(a, b, c, d, sw, cw, response_status(sw), gt.g, gt.h, host_table(tv), dig, 1);
+  return verify_proof(host_digits(a), host_digits(b), host_digits(c), host_digits(d), sw, cw, response_status(sw),
+                      gt.g, gt.h, host_table(tv), dig, 1);
 }
 
 // The fixed-schedule no-context challenge (k_challenge_noctx's arithmetic) from the prefix

@@ -162,3 +162,30 @@ def test_c4_shard_partials_from_forged_entries_alone(gpu):
         parts.append(p)
     total, ident = gpu.combine_partials(parts)
     assert not ident and total == _oracle_partial(host, idx)
+
+
+def test_fallback_probe_sparse_and_dense(gpu):
+    """Fallback-enabled batch checks of 2^21 proofs: three forgeries (the density probe sees
+    none -> MSM + bisection: exact set, and the partial equals the oracle's partial of the
+    three), then 1 % forged (the probe sees several -> MSM skipped: exact set, partial_out
+    0xff...ff, batch not ok)."""
+    torch = pytest.importorskip("torch")
+    n = 1 << 21
+    t = _synthetic_device(gpu, torch, n)
+    st = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    sparse = np.array([12345, 1_000_001, n - 2])
+    host = _forge(t, torch, sparse)
+    p, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED, fallback=True)
+    assert not ok and p == _oracle_partial(host, sparse)
+    got = st.cpu().numpy()
+    assert np.array_equal(np.nonzero(got)[0], sparse) and set(got[sparse].tolist()) == {1}
+    dense = np.sort(np.random.default_rng(7).choice(np.setdiff1d(np.arange(n), sparse), n // 100, replace=False))
+    _forge(t, torch, dense)
+    p, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED, fallback=True)
+    assert not ok and p == b"\xff" * 32
+    got = st.cpu().numpy()
+    want = np.sort(np.concatenate([sparse, dense]))
+    assert np.array_equal(np.nonzero(got)[0], want) and set(got[want].tolist()) == {1}
+    # without a fallback the partial is always computed
+    p, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED)
+    assert not ok and p != b"\xff" * 32 and p != bytes(32)

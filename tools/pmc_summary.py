@@ -37,7 +37,7 @@ def mean(v):
 
 
 out = {}
-for tag in ("prof_fetch", "prof_write", "prof_sq"):
+for tag in ("prof_fetch", "prof_write", "prof_sq", "prof_l2"):
     for k, d in counters(os.path.join(src, tag, "run_counter_collection.csv")).items():
         if not k.startswith("k_"):
             continue
@@ -54,6 +54,11 @@ if os.path.exists(stats):
 for k, d in out.items():
     if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
         d["hbm_bytes_per_launch"] = 2 * d["FETCH_SIZE"] * 1024 + d["WRITE_SIZE"] * 1024
+    if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d and d["TCC_HIT_sum"] + d["TCC_MISS_sum"] > 0:
+        d["l2_hit_rate"] = d["TCC_HIT_sum"] / (d["TCC_HIT_sum"] + d["TCC_MISS_sum"])
+    if "GRBM_GUI_ACTIVE" in d and d.get("avg_ns"):
+        # MI355X_MICROARCH.md DVFS: effective clock ~ GRBM_GUI_ACTIVE / 8 XCDs / wall time
+        d["effective_clock_ghz"] = d["GRBM_GUI_ACTIVE"] / 8.0 / d["avg_ns"]
 ve = out.get("k_verify_each", {})
 if ve:
     n = int(os.environ.get("PROOFS_PER_LAUNCH", 1 << 16))
@@ -64,6 +69,9 @@ if ve:
     ve["correction"] = ("gfx950: FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads "
                         "(MI355X_MICROARCH.md HBM) -> doubled; WRITE_SIZE as reported; units kB")
     ve["algorithmic_bytes_per_launch"] = 194 * n
+    if "hbm_bytes_per_launch" in ve:
+        ve["hbm_bytes_per_proof"] = ve["hbm_bytes_per_launch"] / n
+    ve["source"] = "profiles/%s_verify_each_pmc.json (tools/profile.sh + tools/pmc_summary.py)" % rnd
 # Verify span from the kernel trace: k_verify_each launches overlap (two streams), so the
 # per-step time is the union of their intervals; a "step" is 2^20 proofs = 2^20 / n launches.
 trace = os.path.join(src, "prof_trace", "run_kernel_trace.csv")
@@ -89,5 +97,16 @@ with open(os.path.join(prof, "%s_pmc.json" % rnd), "w") as f:
 if ve:
     with open(os.path.join(prof, "%s_verify_each_pmc.json" % rnd), "w") as f:
         json.dump(dict(ve, kernel="cpz::k_verify_each"), f, indent=1, sort_keys=True)
+# k_rlc_bucket: one launch per RLC step of 2^20 proofs (the bench's RLC extra)
+bk = out.get("k_rlc_bucket", {})
+if bk:
+    bk = dict(bk, kernel="cpz::k_rlc_bucket", workload="2^20 proofs per launch (bench.py RLC extra)",
+              source="profiles/%s_rlc_bucket_pmc.json (tools/profile.sh + tools/pmc_summary.py)" % rnd)
+    if "hbm_bytes_per_launch" in bk:
+        bk["hbm_bytes_per_2p20"] = bk["hbm_bytes_per_launch"]
+    bk["algorithmic_bytes_per_2p20"] = 48 * 132 * (1 << 20)
+    with open(os.path.join(prof, "%s_rlc_bucket_pmc.json" % rnd), "w") as f:
+        json.dump(bk, f, indent=1, sort_keys=True)
 print(json.dumps({k: {c: round(v, 1) if isinstance(v, float) else v for c, v in d.items()}
-                  for k, d in out.items() if k in ("k_verify_each", "k_challenge")}, indent=1))
+                  for k, d in out.items() if k in ("k_verify_each", "k_challenge", "k_rlc_bucket", "k_rlc_prepare")},
+                 indent=1))
