@@ -312,7 +312,7 @@ def main():
             raise SystemExit("bench: C5 per-proof statuses differ from the fallback's")
         ms = {k: v[0] for k, v in c_st.items()}
         c5 = {"workload": "configs[4]: %d proofs, %d forged (half s+1, half wrong y1), RLC batch check + fallback "
-                          "(density probe, then per-proof on prepared points) -> exact invalid set" % (n5, nf),
+                          "(density probe beside the challenges; a dense batch is verified per proof, nothing prepared) -> exact invalid set" % (n5, nf),
               "proofs": n5, "forged": nf, "ms": c_el * 1e3, "proofs_per_s": n5 / c_el, "exact_set": True,
               "phase_ms": {"challenge": ms.get("challenge", 0.0), "rlc_prepare": ms.get("rlc_prepare", 0.0),
                            "rlc_msm": ms.get("rlc_msm", 0.0), "fallback_per_proof": ms.get("fallback", 0.0)},

@@ -260,11 +260,28 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_hist(RlcMsmArgs a) {
   const int g = blockIdx.x, w = blockIdx.y;
   for (int b = threadIdx.x; b < kRlcBuckets; b += kRlcSortBlock) hist[b] = 0;
   __syncthreads();
-  const int64_t total = (a.p1 - a.p0) + 2;
+  const int64_t np = a.p1 - a.p0, total = np + 2;
   const int64_t t0 = (int64_t)g * a.chunk;
   const int64_t t1 = t0 + a.chunk < total ? t0 + a.chunk : total;
   const int16_t* dig = a.digits + (int64_t)w * a.dstride;
-  for (int64_t t = t0 + threadIdx.x; t < t1; t += kRlcSortBlock) {
+  // 8 digits per 16-byte load where the range is aligned (chunks are multiples of 64 points;
+  // p0 is a multiple of 4 * 256 on every RLC path), so each thread has 8 entries per load
+  // round trip instead of one
+  int64_t ts = t0;
+  if ((a.p0 & 7) == 0) {
+    const int64_t v1 = t0 + (((t1 < np ? t1 : np) - t0) & ~(int64_t)7);
+    for (int64_t t = t0 + 8 * threadIdx.x; t < v1; t += 8 * kRlcSortBlock) {
+      const uint4 q = *reinterpret_cast<const uint4*>(dig + a.p0 + t);
+      const uint32_t wv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int d = (int16_t)(wv[k >> 1] >> (16 * (k & 1)));
+        if (d != 0) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
+      }
+    }
+    ts = v1 > t0 ? v1 : t0;
+  }
+  for (int64_t t = ts + threadIdx.x; t < t1; t += kRlcSortBlock) {
     const int d = dig[msm_point(a, t)];
     if (d != 0) atomicAdd(&hist[(d < 0 ? -d : d) - 1], 1u);
   }
@@ -280,10 +297,17 @@ __global__ void __launch_bounds__(256) k_rlc_bscan(RlcMsmArgs a) {
   const int b = (int)(t % kRlcBuckets);
   uint32_t* h = a.bhist + (int64_t)w * a.groups * kRlcBuckets + b;
   uint32_t run = 0;
-  for (int g = 0; g < a.groups; g++) {
-    const uint32_t v = h[(int64_t)g * kRlcBuckets];
-    h[(int64_t)g * kRlcBuckets] = run;
-    run += v;
+  // 8 loads in flight, then their 8 stores (a load after a store to the same array would
+  // otherwise wait for it)
+  for (int g0 = 0; g0 < a.groups; g0 += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = g0 + k < a.groups ? h[(int64_t)(g0 + k) * kRlcBuckets] : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      if (g0 + k < a.groups) h[(int64_t)(g0 + k) * kRlcBuckets] = run;
+      run += v[k];
+    }
   }
   a.counts[t] = run;
 }
@@ -344,6 +368,7 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_coarse(RlcMsmArgs a) {
   __shared__ uint64_t buf[kRlcTile];
   __shared__ uint32_t gbase[kRlcCoarse], cnt[kRlcCoarse], start[kRlcCoarse];
   __shared__ uint32_t part[kRlcSortBlock];
+  __shared__ uint32_t wtot[kRlcCoarse / 64];
   const int g = blockIdx.x, w = blockIdx.y;
   const int tid = threadIdx.x;
   const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
@@ -389,13 +414,25 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_coarse(RlcMsmArgs a) {
       }
     }
     __syncthreads();
-    if (tid == 0) {  // exclusive scan of the 256 bin counts (tiny)
-      uint32_t run = 0;
-      for (int c = 0; c < kRlcCoarse; c++) {
-        start[c] = run;
-        run += cnt[c];
+    // exclusive scan of the 256 bin counts: a shuffle scan per wave, then the wave totals
+    // (a one-thread loop here was ~8 us of LDS latency per tile)
+    if (tid < kRlcCoarse) {
+      const uint32_t v = cnt[tid];
+      uint32_t x = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if ((tid & 63) >= d) x += y;
       }
-      part[0] = run;
+      start[tid] = x - v;
+      if ((tid & 63) == 63) wtot[tid >> 6] = x;
+    }
+    __syncthreads();
+    if (tid < kRlcCoarse) {
+      uint32_t add = 0;
+      for (int k = 0; k < (tid >> 6); k++) add += wtot[k];
+      start[tid] += add;
+      if (tid == kRlcCoarse - 1) part[0] = start[tid] + cnt[tid];
     }
     __syncthreads();
 #pragma unroll
@@ -417,6 +454,20 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_coarse(RlcMsmArgs a) {
   }
 }
 
+// Where sorted entry e of a window lives in idx: every group of 64 chunks (one wave of
+// k_rlc_bucket, kRlcChunk * 64 entries) is stored transposed, [entry in chunk][chunk], so
+// that the wave's 64 lanes, each walking its own chunk, read 64 consecutive ids per step
+// (two 128-byte lines, each used once) instead of 64 lines 256 bytes apart that the point
+// gathers evict before the lane comes back for the next id.
+static_assert(kRlcChunk == 64, "idx_slot assumes 64-entry chunks and 64-lane waves");
+#ifndef CPZ_RLC_IDX_T
+#define CPZ_RLC_IDX_T 0  // 1: transposed groups (bucket -1 %, fine +0.15 ms: not kept)
+#endif
+__device__ __forceinline__ uint32_t idx_slot(uint32_t e) {
+  if (!CPZ_RLC_IDX_T) return e;
+  return (e & ~(uint32_t)(kRlcChunk * 64 - 1)) | ((e % kRlcChunk) * 64) | ((e / kRlcChunk) % 64);
+}
+
 __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_fine(RlcMsmArgs a) {
   __shared__ uint32_t img[kRlcFineCap];
   __shared__ uint32_t cur[kRlcFinePerCoarse];
@@ -429,14 +480,24 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_fine(RlcMsmArgs a) {
   __syncthreads();
   const uint64_t* inter = a.inter + (int64_t)w * a.istride;
   uint32_t* idx = a.idx + (int64_t)w * a.istride;
-  for (uint32_t e = r0 + tid; e < r1; e += kRlcSortBlock) {
-    const uint64_t v = inter[e];
-    const uint32_t pos = atomicAdd(&cur[(uint32_t)(v >> 32)], 1u);
-    if (staged) img[pos] = (uint32_t)v; else idx[pos] = (uint32_t)v;
+  constexpr int U = 4;  // loads in flight per thread
+  for (uint32_t e0 = r0 + tid; e0 < r1; e0 += U * kRlcSortBlock) {
+    uint64_t v[U];
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      const uint32_t e = e0 + k * kRlcSortBlock;
+      v[k] = e < r1 ? inter[e] : ~0ull;  // entries have v >> 32 < 128: never ~0
+    }
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      if (v[k] == ~0ull) continue;
+      const uint32_t pos = atomicAdd(&cur[(uint32_t)(v[k] >> 32)], 1u);
+      if (staged) img[pos] = (uint32_t)v[k]; else idx[idx_slot(pos)] = (uint32_t)v[k];
+    }
   }
   if (!staged) return;
   __syncthreads();
-  for (uint32_t e = tid; e < r1 - r0; e += kRlcSortBlock) idx[r0 + e] = img[e];
+  for (uint32_t e = tid; e < r1 - r0; e += kRlcSortBlock) idx[idx_slot(r0 + e)] = img[e];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -461,7 +522,7 @@ __device__ __forceinline__ ge_p1p1 p1p1_identity_rlc() {
 
 // (141 VGPRs, 3 waves/SIMD; forcing 4 waves -- 128 VGPRs with spills -- measured 7 % slower)
 __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
-  const int w = blockIdx.y;
+  const int w = a.w0 + blockIdx.y;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
   const uint32_t total = off[kRlcBuckets];
@@ -482,11 +543,11 @@ __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
   uint32_t bend = off[b + 1];
   bool head = off[b] < e0;  // bucket b started in an earlier chunk
   ge_p1p1 r = p1p1_identity_rlc();
-  uint32_t id = idx[e0];
+  uint32_t id = idx[idx_slot(e0)];
   for (uint32_t e = e0; e < e1; e++) {
     const ge_niels p = load_niels(a.pts + (id & 0x7fffffffu));
     const bool neg = (id >> 31) != 0;
-    id = e + 1 < e1 ? idx[e + 1] : 0u;
+    id = e + 1 < e1 ? idx[idx_slot(e + 1)] : 0u;
     ge_p3 acc = p1p1_to_p3(r);
     if (e == bend) {  // bucket b complete: emit it (a store, no extra field work), restart
       if (head) store_p3(heads + t, acc); else store_p3(bw + b, acc);
@@ -500,118 +561,49 @@ __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
   if (head) store_p3(heads + t, v); else store_p3(bw + b, v);
 }
 
-// B[w][b] += heads of the chunks after the owner that bucket b spans; empty buckets
-// become the identity.
+// Buckets leave the fix-up in cached form (Y+X, Y-X, Z, 2dT, the same 160 bytes), so the
+// reduction kernels add them with 2 quad rounds and no conversion of their own.
+__device__ __forceinline__ void store_cached(ge_cached* dst, const ge_cached& v) {
+  store_p3(reinterpret_cast<ge_p3*>(dst), *reinterpret_cast<const ge_p3*>(&v));
+}
+
+__device__ __forceinline__ ge_cached load_cached(const ge_cached* src) {
+  const ge_p3 v = load_p3(reinterpret_cast<const ge_p3*>(src));
+  return *reinterpret_cast<const ge_cached*>(&v);
+}
+
+// B[w][b] += heads of the chunks after the owner that bucket b spans, then B[w][b] is
+// rewritten in cached form; empty buckets become the cached identity.
 __global__ void __launch_bounds__(256) k_rlc_bucket_fix(RlcMsmArgs a) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (int64_t)kRlcWindows * kRlcBuckets) return;
+  __builtin_amdgcn_s_setprio(3);  // issue ahead of bucket waves sharing the SIMD (pipelined tails)
+  const int64_t tl = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (tl >= (int64_t)(a.w1 - a.w0) * kRlcBuckets) return;
+  const int64_t t = tl + (int64_t)a.w0 * kRlcBuckets;
   const int w = (int)(t / kRlcBuckets);
   const int b = (int)(t % kRlcBuckets);
   const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
   const uint32_t s = off[b], e = off[b + 1];
-  ge_p3* dst = a.buckets + t;
+  ge_cached* dst = reinterpret_cast<ge_cached*>(a.buckets + t);
   if (s == e) {
-    store_p3(dst, ge_identity());
+    store_cached(dst, ge_cached_identity());
     return;
   }
   const uint32_t c0 = s / kRlcChunk, c1 = (e - 1) / kRlcChunk;
-  if (c1 == c0) return;  // entirely inside its owner's chunk
   const ge_p3* heads = a.heads + (int64_t)w * a.hstride;
-  ge_p3 v = load_p3(dst);
+  ge_p3 v = load_p3(a.buckets + t);
   for (uint32_t c = c0 + 1; c <= c1; c++) v = ge_add(v, load_p3(heads + c));
-  store_p3(dst, v);
+  store_cached(dst, p3_to_cached(v));
 }
 
-// One thread per (window, segment of kRlcSegLen buckets):
-//   S = sum_{b in seg} B_b,   W = sum_{b in seg} (b - lo + 1) B_b   (lo = first bucket value)
-__global__ void __launch_bounds__(256) k_rlc_segment(RlcMsmArgs a) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  constexpr int nseg = kRlcBuckets / kRlcSegLen;
-  if (t >= (int64_t)kRlcWindows * nseg) return;
-  const int w = (int)(t / nseg);
-  const int sg = (int)(t % nseg);
-  const ge_p3* B = a.buckets + (int64_t)w * kRlcBuckets + (int64_t)sg * kRlcSegLen;
-  ge_p3 run = ge_identity(), acc = ge_identity();
-  for (int k = kRlcSegLen - 1; k >= 0; k--) {
-    run = ge_add(run, load_p3(B + k));
-    acc = ge_add(acc, run);
-  }
-  store_p3(a.seg_s + t, run);
-  store_p3(a.seg_w + t, acc);
-}
-
-// One block (256 threads) per window.  Segment t covers bucket values L t + 1 .. L t + L
-// (L = kRlcSegLen):  T_w = sum_t W_t + L * sum_t t S_t.  Thread u owns the P = nseg / 256
-// segments P u .. P u + P - 1:  A_u = sum_j S_{Pu+j},  M_u = sum_j j S_{Pu+j},
-//   sum_t t S_t = P sum_u u A_u + sum_u M_u,   sum_u u A_u = sum_{k>=1} suffix_k(A).
-__global__ void __launch_bounds__(256) k_rlc_window(RlcMsmArgs a) {
-  __shared__ ge_p3 lds[256];
-  const int w = blockIdx.x;
-  const int u = threadIdx.x;
-  constexpr int nseg = kRlcBuckets / kRlcSegLen;
-  constexpr int P = nseg / 256;
-  static_assert(P * 256 == nseg && (P & (P - 1)) == 0 && (kRlcSegLen & (kRlcSegLen - 1)) == 0,
-                "window kernel assumes power-of-two segment counts");
-  const ge_p3* S = a.seg_s + (int64_t)w * nseg;
-  const ge_p3* Wt = a.seg_w + (int64_t)w * nseg;
-  ge_p3 A = ge_identity(), M = ge_identity(), Wsum = ge_identity();
-  {
-    ge_p3 run = ge_identity();
-    for (int j = P - 1; j >= 1; j--) {   // M = sum_j j S_j = sum_{j>=1} suffix_j
-      run = ge_add(run, load_p3(S + P * u + j));
-      M = ge_add(M, run);
-    }
-    A = ge_add(run, load_p3(S + P * u));
-    for (int j = 0; j < P; j++) Wsum = ge_add(Wsum, load_p3(Wt + P * u + j));
-  }
-  // suffix scan of A over u (inclusive): suf_u = sum_{v >= u} A_v
-  lds[u] = A;
-  __syncthreads();
-  ge_p3 suf = A;
-  for (int off = 1; off < 256; off <<= 1) {
-    ge_p3 other = ge_identity();
-    const bool has = u + off < 256;
-    if (has) other = lds[u + off];
-    __syncthreads();
-    if (has) suf = ge_add(suf, other);
-    lds[u] = suf;
-    __syncthreads();
-  }
-  // total = sum W + L * (P * sum_{u>=1} suf_u + sum M)
-  ge_p3 x = (u >= 1) ? suf : ge_identity();
-  // tree-sum the three quantities x, M, Wsum side by side (8 levels, not 3 x 8)
-  __shared__ ge_p3 lds_m[256], lds_w[256];
-  __syncthreads();
-  lds[u] = x;
-  lds_m[u] = M;
-  lds_w[u] = Wsum;
-  __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (u < off) {
-      lds[u] = ge_add(lds[u], lds[u + off]);
-      lds_m[u] = ge_add(lds_m[u], lds_m[u + off]);
-      lds_w[u] = ge_add(lds_w[u], lds_w[u + off]);
-    }
-    __syncthreads();
-  }
-  if (u == 0) {
-    ge_p3 r = lds[0];
-#pragma unroll 1
-    for (int k = 1; k < P; k <<= 1) r = p1p1_to_p3(p3_dbl(r));  // * P
-    r = ge_add(r, lds_m[0]);
-#pragma unroll 1
-    for (int k = 1; k < kRlcSegLen; k <<= 1) r = p1p1_to_p3(p3_dbl(r));  // * L
-    r = ge_add(r, lds_w[0]);
-    store_p3(a.win + w, r);
-  }
-}
-
-// Single block: P = sum_w 2^(16 w) T_w (tree), encode.
-// Quad-cooperative doubling for the latency-bound combine below: the four lanes of a quad
-// hold the same projective point; lane q squares [X, Y, Z, X+Y][q] (lane 2 folds the 2 of
-// 2Z^2 into its column sums), the four squares are broadcast inside the quad with DPP
-// quad_perm moves (full-rate VALU, no LDS), and lanes 0-2 do the three products of the
-// p1p1 -> p2 conversion.  One wave then issues 1 S + 1 M per doubling instead of 4 S + 3 M.
+// ---------------------------------------------------------------------------------------
+// Quad-cooperative point arithmetic for the reduction kernels below, which are chains of
+// dependent additions run by few waves (latency-bound: one wave issues ~1 VALU instruction
+// per 4-8 cycles whatever the chip's width).  The four lanes of a quad hold the same
+// points; each lane computes one of the four independent products of a round on operands
+// it selects by its lane index, and the four products are broadcast inside the quad with
+// DPP quad_perm moves (full-rate VALU, no LDS).  A cached addition (8 products) is then two
+// product latencies instead of eight.  Quads must be whole (all four lanes active).
+// ---------------------------------------------------------------------------------------
 template <int K>
 __device__ __forceinline__ fe fe_quad_bcast(const fe& a) {
   fe r;
@@ -620,69 +612,214 @@ __device__ __forceinline__ fe fe_quad_bcast(const fe& a) {
   return r;
 }
 
-__device__ __forceinline__ ge_p2 p2_dbl_quad(const ge_p2& p, int q) {
-  const fe xpy = fe_add(p.X, p.Y);
-  fe op = fe_select(p.X, p.Y, q == 1);
-  op = fe_select(op, p.Z, q == 2);
-  op = fe_select(op, xpy, q == 3);
-  int64_t h[10];
-  fe_sq_wide(h, op, 1);
-#pragma unroll
-  for (int i = 0; i < 10; i++) h[i] = q == 2 ? 2 * h[i] - carry_bias(i) : h[i];  // 2 Z^2, bias once
-  const fe sq = fe_carry_biased(h);
-  const fe XX = fe_quad_bcast<0>(sq), YY = fe_quad_bcast<1>(sq), ZZ2 = fe_quad_bcast<2>(sq),
-           XpY2 = fe_quad_bcast<3>(sq);
-  const fe Y1 = fe_add(YY, XX), Z1 = fe_sub(YY, XX);
-  const fe X1 = fe_sub(XpY2, Y1), T1 = fe_sub(ZZ2, Z1);
-  // lane 0: X1 T1, lane 1: Y1 Z1, lane 2: Z1 T1 (lane 3 repeats lane 0)
-  fe ma = fe_select(X1, Y1, q == 1);
-  ma = fe_select(ma, Z1, q == 2);
-  const fe mb = fe_select(T1, Z1, q == 1);
-  const fe m = fe_mul(ma, mb);
-  ge_p2 r;
-  r.X = fe_quad_bcast<0>(m);
-  r.Y = fe_quad_bcast<1>(m);
-  r.Z = fe_quad_bcast<2>(m);
+__device__ __forceinline__ fe fe_sel4(int q, const fe& a0, const fe& a1, const fe& a2, const fe& a3) {
+  fe r = fe_select(a0, a1, q == 1);
+  r = fe_select(r, a2, q == 2);
+  return fe_select(r, a3, q == 3);
+}
+
+// lane q multiplies its own pair (a, b); every lane of the quad receives the four products
+__device__ __forceinline__ void quad_mul(fe& m0, fe& m1, fe& m2, fe& m3, const fe& a, const fe& b) {
+  const fe m = fe_mul(a, b);
+  m0 = fe_quad_bcast<0>(m);
+  m1 = fe_quad_bcast<1>(m);
+  m2 = fe_quad_bcast<2>(m);
+  m3 = fe_quad_bcast<3>(m);
+}
+
+// P + Q (Q cached) -> extended: ge_add_cached + p1p1_to_p3 as two quad rounds
+__device__ __forceinline__ ge_p3 ge_add_quad(const ge_p3& p, const ge_cached& c, int q) {
+  fe PP, MM, TT2d, ZZ;
+  quad_mul(PP, MM, TT2d, ZZ, fe_sel4(q, fe_add(p.Y, p.X), fe_sub(p.Y, p.X), p.T, p.Z),
+           fe_sel4(q, c.YpX, c.YmX, c.T2d, c.Z));
+  const fe ZZ2 = fe_add(ZZ, ZZ);
+  const fe X = fe_sub(PP, MM), Y = fe_add(PP, MM), Z = fe_add(ZZ2, TT2d), T = fe_sub(ZZ2, TT2d);
+  ge_p3 r;  // p1p1_to_p3: X T, Z Y, Z T, X Y
+  quad_mul(r.X, r.Y, r.Z, r.T, fe_sel4(q, X, Z, Z, X), fe_sel4(q, T, Y, T, Y));
   return r;
 }
 
-// Single block: P = sum_w 2^(16 w) T_w by a tree, encode.  Quad g (lanes 4g..4g+3) owns
-// window g; at level `span` the active quads double their upper partner 16 span times
-// (240 doublings deep in all) with p2_dbl_quad and add it to their own.
-__global__ void __launch_bounds__(64) k_rlc_final(RlcMsmArgs a) {
-  __shared__ ge_p3 lds[kRlcWindows];
-  const int w = threadIdx.x >> 2, q = threadIdx.x & 3;
-  if (q == 0) lds[w] = load_p3(a.win + w);
-  __syncthreads();
-  for (int span = 1; span < kRlcWindows; span <<= 1) {
-    const bool active = (w % (2 * span)) == 0;
-    ge_p3 lo = ge_identity();
-    if (active) {
-      lo = lds[w];
-      const ge_p3 hi = lds[w + span];
-      ge_p2 t;
-      t.X = hi.X;
-      t.Y = hi.Y;
-      t.Z = hi.Z;
+// cached form of an extended point: its one product (2d T) done by every lane of the quad
+__device__ __forceinline__ ge_p3 ge_add_quad(const ge_p3& p, const ge_p3& o, int q) {
+  return ge_add_quad(p, p3_to_cached(o), q);
+}
+
+// (X : Y : Z) -> extended (XZ : YZ : Z^2 : XY), one quad round
+__device__ __forceinline__ ge_p3 p2_to_p3_quad(const ge_p2& t, int q) {
+  ge_p3 d;
+  quad_mul(d.X, d.Y, d.Z, d.T, fe_sel4(q, t.X, t.Y, t.Z, t.X), fe_sel4(q, t.Z, t.Z, t.Z, t.Y));
+  return d;
+}
+
+// 2^k P with the chain kept distributed: lane q holds v_q = [X, Y, Z, X+Y][q] of the
+// current point and squares it (lane 2: 2 Z^2); the four squares are broadcast, each lane
+// forms its own product operands (lane 0: X1 T1, 1: Y1 Z1, 2: Z1 T1), so after the product
+// lane q holds coordinate q of the double and lane 3 rebuilds X+Y from lanes 0 and 1.  Per
+// doubling that is 6 broadcasts and 4 selects per limb instead of the 7 and 9 of p2_dbl_quad
+// (the final's 240-doubling chain issues ~500 instructions per doubling from one wave).
+__device__ __forceinline__ ge_p3 p3_dbl_n_quad(const ge_p3& p, int k, int q) {
+  if (k == 0) return p;
+  fe v = fe_sel4(q, p.X, p.Y, p.Z, fe_add(p.X, p.Y));
 #pragma unroll 1
-      for (int k = 0; k < 16 * span; k++) t = p2_dbl_quad(t, q);
-      ge_p3 d;  // (X : Y : Z) -> extended (XZ : YZ : Z^2 : XY)
-      d.X = fe_mul(t.X, t.Z);
-      d.Y = fe_mul(t.Y, t.Z);
-      d.Z = fe_sq(t.Z);
-      d.T = fe_mul(t.X, t.Y);
-      lo = ge_add(lo, d);
-    }
+  for (int i = 0; i < k; i++) {
+    int64_t h[10];
+    fe_sq_wide(h, v, 1);
+#pragma unroll
+    for (int l = 0; l < 10; l++) h[l] = q == 2 ? 2 * h[l] - carry_bias(l) : h[l];  // 2 Z^2, bias once
+    const fe sq = fe_carry_biased(h);
+    const fe XX = fe_quad_bcast<0>(sq), YY = fe_quad_bcast<1>(sq), ZZ2 = fe_quad_bcast<2>(sq),
+             XpY2 = fe_quad_bcast<3>(sq);
+    const fe Y1 = fe_add(YY, XX), Z1 = fe_sub(YY, XX);
+    const fe X1 = fe_sub(XpY2, Y1), T1 = fe_sub(ZZ2, Z1);
+    const fe m = fe_mul(fe_select(fe_select(X1, Y1, q == 1), Z1, q == 2), fe_select(T1, Z1, q == 1));
+    v = fe_select(m, fe_add(fe_quad_bcast<0>(m), fe_quad_bcast<1>(m)), q == 3);
+  }
+  ge_p2 t;
+  t.X = fe_quad_bcast<0>(v);
+  t.Y = fe_quad_bcast<1>(v);
+  t.Z = fe_quad_bcast<2>(v);
+  return p2_to_p3_quad(t, q);
+}
+
+// One quad per (window, segment of kRlcSegLen buckets), buckets in cached form:
+//   S = sum_{b in seg} B_b,   W = sum_{b in seg} (b - lo + 1) B_b   (lo = first bucket value)
+// written in cached form for k_rlc_window.
+// (2 waves/SIMD: the 2048 waves of a launch are resident at once)
+__global__ void __launch_bounds__(256, 2) k_rlc_segment(RlcMsmArgs a) {
+  __builtin_amdgcn_s_setprio(3);
+  const int64_t tl = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 2;
+  const int q = threadIdx.x & 3;
+  constexpr int nseg = kRlcBuckets / kRlcSegLen;
+  if (tl >= (int64_t)(a.w1 - a.w0) * nseg) return;  // whole quads
+  const int64_t t = tl + (int64_t)a.w0 * nseg;
+  const int w = (int)(t / nseg);
+  const int sg = (int)(t % nseg);
+  const ge_cached* B =
+      reinterpret_cast<const ge_cached*>(a.buckets + (int64_t)w * kRlcBuckets + (int64_t)sg * kRlcSegLen);
+  ge_p3 run = ge_identity(), acc = ge_identity();
+  ge_cached nb = load_cached(B + kRlcSegLen - 1);
+#pragma unroll 1
+  for (int k = kRlcSegLen - 1; k >= 0; k--) {
+    const ge_cached cb = nb;
+    if (k > 0) nb = load_cached(B + k - 1);
+    run = ge_add_quad(run, cb, q);
+    acc = ge_add_quad(acc, run, q);
+  }
+  if (q == 0) {
+    store_cached(reinterpret_cast<ge_cached*>(a.seg_s) + t, p3_to_cached(run));
+    store_cached(reinterpret_cast<ge_cached*>(a.seg_w) + t, p3_to_cached(acc));
+  }
+}
+
+// One block of 512 threads (128 quads) per window.  Segment t covers bucket values L t + 1
+// .. L t + L (L = kRlcSegLen):  T_w = sum_t W_t + L * sum_t t S_t.  Quad u owns the
+// P = nseg / 128 segments P u .. P u + P - 1:  A_u = sum_j S_{Pu+j},  M_u = sum_j j S_{Pu+j},
+//   sum_t t S_t = P sum_u u A_u + sum_u M_u,   sum_u u A_u = sum_{k>=1} suffix_k(A).
+constexpr int kRlcWinQuads = 128;  // 512 threads: 256 VGPRs without spills (1024 spill)
+__global__ void __launch_bounds__(4 * kRlcWinQuads) k_rlc_window(RlcMsmArgs a) {
+  __shared__ ge_p3 lds[kRlcWinQuads], lds_m[kRlcWinQuads], lds_w[kRlcWinQuads];
+  __builtin_amdgcn_s_setprio(3);
+  const int w = a.w0 + blockIdx.x;
+  const int u = threadIdx.x >> 2, q = threadIdx.x & 3;
+  constexpr int nseg = kRlcBuckets / kRlcSegLen;
+  constexpr int P = nseg / kRlcWinQuads;
+  static_assert(P * kRlcWinQuads == nseg && (P & (P - 1)) == 0 && (kRlcSegLen & (kRlcSegLen - 1)) == 0,
+                "window kernel assumes power-of-two segment counts");
+  const ge_cached* S = reinterpret_cast<const ge_cached*>(a.seg_s) + (int64_t)w * nseg + P * u;
+  const ge_cached* Wt = reinterpret_cast<const ge_cached*>(a.seg_w) + (int64_t)w * nseg + P * u;
+  ge_p3 run = ge_identity(), M = ge_identity(), Wsum = ge_identity();
+#pragma unroll 1
+  for (int j = P - 1; j >= 1; j--) {  // M = sum_j j S_j = sum_{j>=1} suffix_j
+    run = ge_add_quad(run, load_cached(S + j), q);
+    M = ge_add_quad(M, run, q);
+    Wsum = ge_add_quad(Wsum, load_cached(Wt + j), q);
+  }
+  const ge_p3 A = ge_add_quad(run, load_cached(S), q);
+  Wsum = ge_add_quad(Wsum, load_cached(Wt), q);
+  // suffix scan of A over u (inclusive): suf_u = sum_{v >= u} A_v
+  if (q == 0) lds[u] = A;
+  __syncthreads();
+  ge_p3 suf = A;
+#pragma unroll 1
+  for (int off = 1; off < kRlcWinQuads; off <<= 1) {
+    const ge_p3 other = u + off < kRlcWinQuads ? lds[u + off] : ge_identity();
     __syncthreads();
-    if (active && q == 0) lds[w] = lo;
+    suf = ge_add_quad(suf, other, q);
+    if (q == 0) lds[u] = suf;
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    const ge_p3 P = lds[0];
-    uint32_t enc[8];
-    ristretto_encode(enc, P);
-    for (int k = 0; k < 8; k++) a.partial_out[k] = enc[k];
-    a.identity_out[0] = ristretto_is_identity(P) ? 1 : 0;
+  // total = sum W + L * (P * sum_{u>=1} suf_u + sum M): the three sums side by side
+  if (q == 0) {
+    lds[u] = u >= 1 ? suf : ge_identity();
+    lds_m[u] = M;
+    lds_w[u] = Wsum;
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int off = kRlcWinQuads / 2; off > 0; off >>= 1) {
+    ge_p3 x, m, ws;
+    if (u < off) {
+      x = ge_add_quad(lds[u], lds[u + off], q);
+      m = ge_add_quad(lds_m[u], lds_m[u + off], q);
+      ws = ge_add_quad(lds_w[u], lds_w[u + off], q);
+    }
+    __syncthreads();
+    if (u < off && q == 0) {
+      lds[u] = x;
+      lds_m[u] = m;
+      lds_w[u] = ws;
+    }
+    __syncthreads();
+  }
+  if (u == 0) {
+    constexpr int lgP = __builtin_ctz(P), lgL = __builtin_ctz(kRlcSegLen);
+    ge_p3 r = p3_dbl_n_quad(lds[0], lgP, q);                   // * P
+    r = p3_dbl_n_quad(ge_add_quad(r, lds_m[0], q), lgL, q);    // * L
+    r = ge_add_quad(r, lds_w[0], q);
+    if (q == 0) store_p3(a.win + w, r);
+  }
+}
+
+// P_g = sum_{w in [w0, w1)} 2^(16 (w - w0)) T_w by a tree: quad j of wave 0 owns window
+// w0 + j; at level `span` the active quads double their upper partner 16 span times and add
+// it to their own (16 (nw - 1) doublings deep).  Unless this is the top group, quad 0 of
+// wave 1 meanwhile shifts the groups above, acc, by 2^(16 nw); the sum is the new acc, or,
+// for the bottom group, the batch's partial P = sum_w 2^(16 w) T_w, encoded with its
+// identity flag.  (One group: the whole tree, 240 doublings deep.)
+__global__ void __launch_bounds__(128) k_rlc_final(RlcMsmArgs a, int first, int last) {
+  __shared__ ge_p3 lds[kRlcWindows + 1];
+  __builtin_amdgcn_s_setprio(3);
+  const int nw = a.w1 - a.w0;
+  const int j = threadIdx.x >> 2, q = threadIdx.x & 3;
+  if (threadIdx.x < 64) {
+    if (q == 0 && j < nw) lds[j] = load_p3(a.win + a.w0 + j);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int span = 1; span < nw; span <<= 1) {  // one wave: LDS traffic stays in program order
+      const bool active = j < nw && (j % (2 * span)) == 0;
+      if (active) {
+        const ge_p3 lo = ge_add_quad(lds[j], p3_dbl_n_quad(lds[j + span], 16 * span, q), q);
+        if (q == 0) lds[j] = lo;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  } else if (threadIdx.x < 68 && !first) {
+    const ge_p3 sh = p3_dbl_n_quad(load_p3(a.acc), 16 * nw, q);
+    if (q == 0) lds[kRlcWindows] = sh;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    ge_p3 P = lds[0];
+    if (!first) P = ge_add_quad(P, lds[kRlcWindows], q);
+    if (!last) {
+      if (q == 0) store_p3(a.acc, P);
+    } else if (q == 0) {
+      uint32_t enc[8];
+      ristretto_encode(enc, P);
+      for (int k = 0; k < 8; k++) a.partial_out[k] = enc[k];
+      a.identity_out[0] = ristretto_is_identity(P) ? 1 : 0;
+    }
   }
 }
 
@@ -737,13 +874,15 @@ void rlc_sort_geometry(RlcMsmArgs& a, int64_t npts) {
   if (g > kRlcSortGroups) g = kRlcSortGroups;
   if (g < 1) g = 1;
   a.groups = (int)g;
-  a.chunk = (npts + g - 1) / g;
+  a.chunk = ((npts + g - 1) / g + 63) & ~(int64_t)63;  // whole 16-byte digit loads (k_rlc_hist)
 }
 
 hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0, int64_t b1, const ge_niels* tab,
-                          hipStream_t st, hipEvent_t* marks) {
+                          hipStream_t st, hipEvent_t* marks, const RlcPipe* pipe) {
   hipError_t e;
-  auto mark = [&](int k) -> hipError_t { return marks ? hipEventRecord(marks[k], st) : hipSuccess; };
+  auto mark = [&](int k, hipStream_t s = nullptr) -> hipError_t {
+    return marks ? hipEventRecord(marks[k], s ? s : st) : hipSuccess;
+  };
   if ((e = mark(0)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_rlc_extra, dim3(1), dim3(256), 0, st, a, block_sums, b0, b1, tab);
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -768,20 +907,49 @@ hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0,
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = mark(1)) != hipSuccess) return e;
   const int64_t chunks = (a.istride + kRlcChunk - 1) / kRlcChunk;  // per window, upper bound
-  hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((chunks + 255) / 256), kRlcWindows), dim3(256), 0, st, a);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
+  auto tails = [&](const RlcMsmArgs& g, int first, int last, hipStream_t s) -> hipError_t {
+    const int nw = g.w1 - g.w0;
+    const int64_t nbg = (int64_t)nw * kRlcBuckets;
+    hipLaunchKernelGGL(k_rlc_bucket_fix, dim3((unsigned)((nbg + 255) / 256)), dim3(256), 0, s, g);
+    hipError_t r = hipGetLastError();
+    if (r != hipSuccess) return r;
+    if (last && (r = mark(3, s)) != hipSuccess) return r;
+    const int64_t ns = (int64_t)nw * (kRlcBuckets / kRlcSegLen);
+    hipLaunchKernelGGL(k_rlc_segment, dim3((unsigned)((4 * ns + 255) / 256)), dim3(256), 0, s, g);  // a quad each
+    if ((r = hipGetLastError()) != hipSuccess) return r;
+    hipLaunchKernelGGL(k_rlc_window, dim3(nw), dim3(4 * kRlcWinQuads), 0, s, g);
+    if ((r = hipGetLastError()) != hipSuccess) return r;
+    if (last && (r = mark(4, s)) != hipSuccess) return r;
+    hipLaunchKernelGGL(k_rlc_final, dim3(1), dim3(128), 0, s, g, first, last);
+    return hipGetLastError();
+  };
+  const int groups = pipe && pipe->side && pipe->groups > 1 ? pipe->groups : 1;
+  const int per = kRlcWindows / groups;
+  if (groups == 1) {
+    hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((chunks + 255) / 256), kRlcWindows), dim3(256), 0, st, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = mark(2)) != hipSuccess) return e;
+    if ((e = tails(a, 1, 1, st)) != hipSuccess) return e;
+    return mark(5);
+  }
+  for (int g = groups - 1; g >= 0; g--) {  // top windows first
+    RlcMsmArgs ga = a;
+    ga.w0 = g * per;
+    ga.w1 = ga.w0 + per;
+    hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((chunks + 255) / 256), per), dim3(256), 0, st, ga);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipEventRecord(pipe->ev[g], st)) != hipSuccess) return e;
+  }
   if ((e = mark(2)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rlc_bucket_fix, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, a);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  if ((e = mark(3)) != hipSuccess) return e;
-  const int64_t ns = (int64_t)kRlcWindows * (kRlcBuckets / kRlcSegLen);
-  hipLaunchKernelGGL(k_rlc_segment, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, st, a);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rlc_window, dim3(kRlcWindows), dim3(256), 0, st, a);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  if ((e = mark(4)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rlc_final, dim3(1), dim3(64), 0, st, a);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
+  for (int g = groups - 1; g >= 0; g--) {
+    RlcMsmArgs ga = a;
+    ga.w0 = g * per;
+    ga.w1 = ga.w0 + per;
+    if ((e = hipStreamWaitEvent(pipe->side, pipe->ev[g], 0)) != hipSuccess) return e;
+    if ((e = tails(ga, g == groups - 1, g == 0, pipe->side)) != hipSuccess) return e;
+  }
+  if ((e = hipEventRecord(pipe->done, pipe->side)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(st, pipe->done, 0)) != hipSuccess) return e;
   return mark(5);
 }
 

@@ -118,9 +118,11 @@ struct cpz_ctx {
   hipEvent_t probe_done = nullptr;
   // RLC / Pippenger buffers (sized for the largest batch seen)
   DevBuf rl_pts, rl_dig, rl_bsum, rl_counts, rl_offsets, rl_bhist, rl_idx, rl_inter, rl_buckets, rl_heads, rl_segs,
-      rl_segw, rl_win,
+      rl_segw, rl_win, rl_acc,
       rl_partial, rl_flags, rl_parts;
   int64_t rl_cap = 0;  // proofs
+  // pipelined MSM tails (cpz::RlcPipe): a high-priority side stream and its events
+  cpz::RlcPipe rl_pipe;
   // Completion of the last call's work on whatever stream it used: the *_device entry points
   // return without synchronising, and their kernels read context buffers (comb, tab, prefix,
   // c, scratch, RLC buffers) that the next call may rewrite on another stream.
@@ -279,7 +281,7 @@ int verify_grid(cpz_ctx* ctx, size_t n) {
 // Challenges per verify chunk on the chunk's stream (hidden under the other stream's verify
 // work; +0.5-1.1 % A/B on one box against one up-front challenge launch).
 #ifndef CPZ_VERIFY_FUSED
-#define CPZ_VERIFY_FUSED 1  // no-context challenges computed inside k_verify_each
+#define CPZ_VERIFY_FUSED 0  // 1: no-context challenges computed inside k_verify_each (measured +0.1 %, not kept)
 #endif
 #ifndef CPZ_CHALLENGE_PER_CHUNK
 #define CPZ_CHALLENGE_PER_CHUNK 1
@@ -460,24 +462,52 @@ int stage_inputs(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], int count
 }
 
 // ---- RLC batch path --------------------------------------------------------------------
+#ifndef CPZ_RLC_GROUPS
+#define CPZ_RLC_GROUPS 1  // window groups of the pipelined MSM tails (cpz::RlcPipe); 1 = one stream
+#endif
+
+// The side stream (highest priority) and events of the pipelined tails, created once.
+int rlc_pipe(cpz_ctx* ctx, const cpz::RlcPipe** out) {
+  *out = nullptr;
+  if (CPZ_RLC_GROUPS <= 1) return CPZ_OK;
+  cpz::RlcPipe& p = ctx->rl_pipe;
+  if (!p.side) {
+    int least = 0, greatest = 0;
+    CPZ_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    CPZ_HIP(hipStreamCreateWithPriority(&p.side, hipStreamNonBlocking, greatest));
+    for (int g = 0; g < CPZ_RLC_GROUPS; g++) CPZ_HIP(hipEventCreateWithFlags(&p.ev[g], hipEventDisableTiming));
+    CPZ_HIP(hipEventCreateWithFlags(&p.done, hipEventDisableTiming));
+    p.groups = CPZ_RLC_GROUPS;
+  }
+  *out = &p;
+  return CPZ_OK;
+}
+
+// digits row stride: 4 points per proof + g, h, rounded to 8 so that every window row starts
+// 16-byte aligned (k_rlc_hist reads 8 digits per load)
+int64_t rlc_dstride(int64_t cap) { return (4 * cap + 2 + 7) & ~(int64_t)7; }
+// sorted-entry row stride: whole 4096-entry groups (k_rlc_fine stores them transposed)
+int64_t rlc_istride(int64_t cap) { return (4 * cap + 2 + 4095) & ~(int64_t)4095; }
+
 int rlc_reserve(cpz_ctx* ctx, int64_t n) {
   if (n <= ctx->rl_cap) return CPZ_OK;
   const int64_t npts = 4 * n + 2;
   const int64_t nblk = (n + cpz::kRlcPrepBlock - 1) / cpz::kRlcPrepBlock;
   CPZ_HIP(ctx->rl_pts.ensure((size_t)npts * sizeof(cpz::ge_niels)));
-  CPZ_HIP(ctx->rl_dig.ensure((size_t)npts * cpz::kRlcWindows * sizeof(int16_t)));
+  CPZ_HIP(ctx->rl_dig.ensure((size_t)rlc_dstride(n) * cpz::kRlcWindows * sizeof(int16_t)));
   CPZ_HIP(ctx->rl_bsum.ensure((size_t)nblk * 2 * sizeof(cpz::sc)));
   CPZ_HIP(ctx->rl_counts.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcBuckets));
   CPZ_HIP(ctx->rl_offsets.ensure(sizeof(uint32_t) * cpz::kRlcWindows * (cpz::kRlcBuckets + 1)));
   CPZ_HIP(ctx->rl_bhist.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcSortGroups * cpz::kRlcBuckets));
-  CPZ_HIP(ctx->rl_idx.ensure((size_t)npts * cpz::kRlcWindows * sizeof(uint32_t)));
-  CPZ_HIP(ctx->rl_inter.ensure((size_t)npts * cpz::kRlcWindows * sizeof(uint64_t)));
+  CPZ_HIP(ctx->rl_idx.ensure((size_t)rlc_istride(n) * cpz::kRlcWindows * sizeof(uint32_t)));
+  CPZ_HIP(ctx->rl_inter.ensure((size_t)rlc_istride(n) * cpz::kRlcWindows * sizeof(uint64_t)));
   CPZ_HIP(ctx->rl_buckets.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * cpz::kRlcBuckets));
-  CPZ_HIP(ctx->rl_heads.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * (size_t)((npts + cpz::kRlcChunk - 1) / cpz::kRlcChunk)));
+  CPZ_HIP(ctx->rl_heads.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * (size_t)(rlc_istride(n) / cpz::kRlcChunk)));
   const size_t nseg = (size_t)cpz::kRlcWindows * (cpz::kRlcBuckets / cpz::kRlcSegLen);
   CPZ_HIP(ctx->rl_segs.ensure(sizeof(cpz::ge_p3) * nseg));
   CPZ_HIP(ctx->rl_segw.ensure(sizeof(cpz::ge_p3) * nseg));
   CPZ_HIP(ctx->rl_win.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows));
+  CPZ_HIP(ctx->rl_acc.ensure(sizeof(cpz::ge_p3)));
   CPZ_HIP(ctx->rl_partial.ensure(64));
   CPZ_HIP(ctx->rl_flags.ensure(4 * sizeof(int)));
   ctx->rl_cap = n;
@@ -491,20 +521,21 @@ cpz::RlcMsmArgs rlc_msm_args(cpz_ctx* ctx, int64_t lo, int64_t hi) {
   m.e0 = 4 * ctx->rl_cap;
   m.pts = static_cast<cpz::ge_niels*>(ctx->rl_pts.p);
   m.digits = static_cast<int16_t*>(ctx->rl_dig.p);
-  m.dstride = 4 * ctx->rl_cap + 2;
+  m.dstride = rlc_dstride(ctx->rl_cap);
   m.counts = static_cast<uint32_t*>(ctx->rl_counts.p);
   m.offsets = static_cast<uint32_t*>(ctx->rl_offsets.p);
   m.bhist = static_cast<uint32_t*>(ctx->rl_bhist.p);
   cpz::rlc_sort_geometry(m, (m.p1 - m.p0) + 2);
   m.idx = static_cast<uint32_t*>(ctx->rl_idx.p);
   m.inter = static_cast<uint64_t*>(ctx->rl_inter.p);
-  m.istride = 4 * ctx->rl_cap + 2;
+  m.istride = rlc_istride(ctx->rl_cap);
   m.buckets = static_cast<cpz::ge_p3*>(ctx->rl_buckets.p);
   m.heads = static_cast<cpz::ge_p3*>(ctx->rl_heads.p);
   m.hstride = (m.istride + cpz::kRlcChunk - 1) / cpz::kRlcChunk;
   m.seg_s = static_cast<cpz::ge_p3*>(ctx->rl_segs.p);
   m.seg_w = static_cast<cpz::ge_p3*>(ctx->rl_segw.p);
   m.win = static_cast<cpz::ge_p3*>(ctx->rl_win.p);
+  m.acc = static_cast<cpz::ge_p3*>(ctx->rl_acc.p);
   m.partial_out = static_cast<uint32_t*>(ctx->rl_partial.p);
   m.identity_out = static_cast<int*>(ctx->rl_flags.p);
   return m;
@@ -526,8 +557,10 @@ int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t part
     if (!timed)
       for (int k = 0; k < got; k++)
         if (marks[k]) ctx->free_events.push_back(marks[k]);
+    const cpz::RlcPipe* pipe;
+    if (int rc = rlc_pipe(ctx, &pipe)) return rc;
     CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_bsum.p), b0, b1,
-                                static_cast<const cpz::ge_niels*>(ctx->tab.p), st, timed ? marks : nullptr));
+                                static_cast<const cpz::ge_niels*>(ctx->tab.p), st, timed ? marks : nullptr, pipe));
     if (timed)
       for (int k = 0; k + 1 < cpz::kRlcMsmMarks; k++) ctx->marks.push_back({8 + k, marks[k], marks[k + 1]});
   }
@@ -539,12 +572,10 @@ int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t part
   return CPZ_OK;
 }
 
-// Prepare (challenge + decode + weights + points/digits) for the whole batch.
-int rlc_prepare(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
-                const void* s, const void* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
-                uint8_t* status, const uint8_t seed[32], uint64_t first_index, hipStream_t st) {
-  int rc = rlc_reserve(ctx, (int64_t)n);
-  if (rc) return rc;
+// Challenges of the whole batch into ctx->c, response statuses into `status`.
+int batch_challenges(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
+                     const void* s, const void* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
+                     uint8_t* status, hipStream_t st) {
   CPZ_HIP(ctx->c.ensure(n * 32));
   cpz::ChallengeArgs ca;
   set_challenge_schedules(ctx, ca);
@@ -561,24 +592,30 @@ int rlc_prepare(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const vo
   ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->prefix.p);
   ca.c_out = static_cast<uint32_t*>(ctx->c.p);
   ca.status_out = status;
-  {
-    StageTimer t(ctx, 0, st);
-    CPZ_HIP(cpz::launch_challenge(ca, st));
-  }
+  StageTimer t(ctx, 0, st);
+  CPZ_HIP(cpz::launch_challenge(ca, st));
+  return CPZ_OK;
+}
+
+// Decode + weights + points/digits of the whole batch (after batch_challenges).
+int rlc_prepare_points(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
+                       const void* s, uint8_t* status, const uint8_t seed[32], uint64_t first_index, hipStream_t st) {
+  int rc = rlc_reserve(ctx, (int64_t)n);
+  if (rc) return rc;
   cpz::RlcPrepArgs pa;
   pa.n = (int64_t)n;
   pa.first_index = first_index;
   std::memcpy(pa.seed, seed, 32);
-  pa.y1 = ca.y1;
-  pa.y2 = ca.y2;
-  pa.r1 = ca.r1;
-  pa.r2 = ca.r2;
-  pa.s = ca.s;
-  pa.c = ca.c_out;
+  pa.y1 = static_cast<const uint32_t*>(y1);
+  pa.y2 = static_cast<const uint32_t*>(y2);
+  pa.r1 = static_cast<const uint32_t*>(r1);
+  pa.r2 = static_cast<const uint32_t*>(r2);
+  pa.s = static_cast<const uint32_t*>(s);
+  pa.c = static_cast<const uint32_t*>(ctx->c.p);
   pa.status = status;
   pa.pts = static_cast<cpz::ge_niels*>(ctx->rl_pts.p);
   pa.digits = static_cast<int16_t*>(ctx->rl_dig.p);
-  pa.dstride = 4 * ctx->rl_cap + 2;
+  pa.dstride = rlc_dstride(ctx->rl_cap);
   pa.block_sums = static_cast<cpz::sc*>(ctx->rl_bsum.p);
   pa.any_bad = static_cast<int*>(ctx->rl_flags.p) + 3;
   CPZ_HIP(hipMemsetAsync(pa.any_bad, 0, sizeof(int), st));
@@ -587,6 +624,15 @@ int rlc_prepare(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const vo
     CPZ_HIP(cpz::launch_rlc_prepare(pa, st));
   }
   return CPZ_OK;
+}
+
+// Prepare (challenge + decode + weights + points/digits) for the whole batch.
+int rlc_prepare(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
+                const void* s, const void* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
+                uint8_t* status, const uint8_t seed[32], uint64_t first_index, hipStream_t st) {
+  int rc = batch_challenges(ctx, n, y1, y2, r1, r2, s, ctx_bytes, ctx_off, ctx_present, status, st);
+  if (rc) return rc;
+  return rlc_prepare_points(ctx, n, y1, y2, r1, r2, s, status, seed, first_index, st);
 }
 
 // Batch-fail fallback (verify_individually, batch.rs:262-268, 314-318): locate the invalid
@@ -720,10 +766,11 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
                       const uint8_t seed[32], uint64_t first_index, uint8_t partial_out[32], int* batch_ok,
                       int fallback, uint8_t* host_status, hipStream_t st) {
   // A fallback-enabled check of a large batch without contexts first samples its density,
-  // beside the prepare (the probe's ~2 ms of per-proof latency hides under it).  A dense
-  // batch (>= 2 invalid entries among the kProbeChunks x 256 sampled) cannot pass and
-  // bisection cannot prune it: the MSM is skipped and every entry is verified per proof on
-  // the prepared points; partial_out is then 32 x 0xff ("no partial": not an encoding).
+  // beside the batch's challenges (the probe's ~0.5 ms of per-proof latency hides under
+  // them).  A dense batch (>= 2 invalid entries among the kProbeChunks x 256 sampled)
+  // cannot pass and bisection cannot prune it: nothing is prepared, every entry is verified
+  // per proof (k_verify_each on the challenges just computed), and partial_out is 32 x 0xff
+  // ("no partial": not an encoding) -- the cost of the per-proof path plus the probe.
   int64_t starts[kProbeChunks];
   const bool probe = fallback && co == nullptr && (int64_t)n >= kProbeMin;
   if (probe) {
@@ -731,7 +778,7 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
     int rc = launch_probe(ctx, n, rows, starts, st);
     if (rc < 0) return rc;
   }
-  int rc = rlc_prepare(ctx, n, y1, y2, r1, r2, s, cb, co, cp, d_status, seed, first_index, st);
+  int rc = batch_challenges(ctx, n, y1, y2, r1, r2, s, cb, co, cp, d_status, st);
   if (rc) return rc;
   if (probe) {
     const size_t m = (size_t)kProbeChunks * cpz::kRlcPrepBlock;
@@ -745,8 +792,21 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
     if (bad >= 2) {
       if (partial_out) std::memset(partial_out, 0xff, 32);
       if (batch_ok) *batch_ok = 0;
-      rc = rlc_fallback(ctx, 0, (int64_t)n, y1, y2, r1, r2, s, d_status, st, 13, false);  // depth > 12: per proof
-      if (rc) return rc;
+      cpz::VerifyArgs va;
+      va.n = (int64_t)n;
+      va.y1 = static_cast<const uint32_t*>(y1);
+      va.y2 = static_cast<const uint32_t*>(y2);
+      va.r1 = static_cast<const uint32_t*>(r1);
+      va.r2 = static_cast<const uint32_t*>(r2);
+      va.s = static_cast<const uint32_t*>(s);
+      va.c = static_cast<const uint32_t*>(ctx->c.p);
+      va.status = d_status;  // response statuses from batch_challenges -> final statuses
+      va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
+      va.scratch = nullptr;  // set per launch
+      {
+        StageTimer span(ctx, 4, st);  // wall time of the fallback; launches timed as verify_each
+        if ((rc = launch_verify_chunks(ctx, va, 1, st, nullptr, true))) return rc;
+      }
       CPZ_HIP(hipStreamSynchronize(st));
       if (host_status) {
         CPZ_HIP(hipMemcpyAsync(host_status, d_status, n, hipMemcpyDeviceToHost, st));
@@ -755,6 +815,7 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
       return CPZ_OK;
     }
   }
+  if ((rc = rlc_prepare_points(ctx, n, y1, y2, r1, r2, s, d_status, seed, first_index, st))) return rc;
   uint8_t part[32];
   int ident = 0;
   rc = rlc_range(ctx, 0, (int64_t)n, st, part, &ident);
@@ -899,8 +960,10 @@ int cpz_msm(cpz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalar
                                static_cast<int*>(ctx->rl_flags.p) + 2, ctx->stream));
   (void)zero;
   // extra points get zero scalars (empty block range)
+  const cpz::RlcPipe* pipe;
+  if ((rc = rlc_pipe(ctx, &pipe))) return rc;
   CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_bsum.p), 0, 0,
-                              static_cast<const cpz::ge_niels*>(ctx->tab.p), ctx->stream));
+                              static_cast<const cpz::ge_niels*>(ctx->tab.p), ctx->stream, nullptr, pipe));
   int flags[3];
   CPZ_HIP(hipMemcpyAsync(out, ctx->rl_partial.p, 32, hipMemcpyDeviceToHost, ctx->stream));
   CPZ_HIP(hipMemcpyAsync(flags, ctx->rl_flags.p, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
@@ -1137,9 +1200,16 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->copy_stream);
     (void)hipStreamDestroy(ctx->copy_stream);
   }
+  if (ctx->rl_pipe.side) {
+    (void)hipStreamSynchronize(ctx->rl_pipe.side);
+    (void)hipStreamDestroy(ctx->rl_pipe.side);
+  }
+  for (auto& e : ctx->rl_pipe.ev)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->rl_pipe.done) (void)hipEventDestroy(ctx->rl_pipe.done);
   for (DevBuf* b : {&ctx->pz_blob, &ctx->pz_off, &ctx->pz_rows, &ctx->pz_code, &ctx->pz_aux}) b->release();
   for (DevBuf* b : {&ctx->rl_pts, &ctx->rl_dig, &ctx->rl_bsum, &ctx->rl_counts, &ctx->rl_offsets, &ctx->rl_bhist,
-                    &ctx->rl_idx, &ctx->rl_inter, &ctx->rl_buckets, &ctx->rl_heads, &ctx->rl_segs, &ctx->rl_segw, &ctx->rl_win, &ctx->rl_partial,
+                    &ctx->rl_idx, &ctx->rl_inter, &ctx->rl_buckets, &ctx->rl_heads, &ctx->rl_segs, &ctx->rl_segw, &ctx->rl_win, &ctx->rl_acc, &ctx->rl_partial,
                     &ctx->rl_flags, &ctx->rl_parts})
     b->release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -148,11 +148,11 @@ int cpz_prove_synthetic_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t 
  *                search (sub-range RLC partials, per-proof verification at the leaves)
  *                locates the invalid entries (verify_individually, batch.rs:314-318).
  *                With a fallback, a batch of >= 2^20 entries without contexts is first
- *                sampled (4096 entries verified per proof, beside the prepare): if two or
- *                more sampled entries are invalid the batch cannot pass and bisection could
- *                not prune it, so the MSM is skipped, every entry is verified per proof on
- *                the prepared points, batch_ok = 0 and partial_out is 32 bytes of 0xff
- *                (not an encoding: "no partial computed").
+ *                sampled (4096 entries verified per proof, beside the batch's challenges):
+ *                if two or more sampled entries are invalid the batch cannot pass and
+ *                bisection could not prune it, so nothing is prepared, every entry is
+ *                verified per proof, batch_ok = 0 and partial_out is 32 bytes of 0xff (not
+ *                an encoding: "no partial computed").
  * The _device form takes device-resident inputs and always needs d_status_out (decode-level
  * statuses, or exact ones when fallback != 0); it synchronises `stream`. */
 int cpz_verify_batch(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
