@@ -364,7 +364,7 @@ __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_prepa
   const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
   const int64_t i = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;  // one proof per thread
   if (i >= a.n) return;
-  const SlabTable tab{a.scratch, (uint32_t)i * (uint32_t)(kCachedEntries * sizeof(ge_cached)), 16u};
+  const SlabTable tab{a.scratch, (uint32_t)i * (uint32_t)(kCachedEntries * sizeof(ge_cached))};
   __shared__ uint32_t dig[16 * kVerifyBlock];
   {
     if (a.status[i] != kStOk) return;  // decode-level rejection: already final
@@ -384,7 +384,7 @@ __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each(
   const int64_t i = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
   if (i >= a.n) return;
   // this thread's tables: kCachedEntries entries, contiguous (scalarmul.h, SlabTable)
-  const SlabTable tab{a.scratch, (uint32_t)i * (uint32_t)(kCachedEntries * sizeof(ge_cached)), 16u};
+  const SlabTable tab{a.scratch, (uint32_t)i * (uint32_t)(kCachedEntries * sizeof(ge_cached))};
   // digit words and point encodings in LDS, one column per thread (scalarmul.h, DigitRef)
   __shared__ uint32_t dig[16 * kVerifyBlock];
   __shared__ uint32_t rows[32 * kVerifyBlock];

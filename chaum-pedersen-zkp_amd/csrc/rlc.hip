@@ -133,18 +133,43 @@ __global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_prepare(RlcPrepArgs a)
   __shared__ sc red_a[kRlcPrepBlock];
   __shared__ sc red_b[kRlcPrepBlock];
   const int64_t i = (int64_t)blockIdx.x * kRlcPrepBlock + threadIdx.x;
-  sc as, bs;
+  sc zero;
 #pragma unroll
-  for (int k = 0; k < 8; k++) { as.w[k] = 0; bs.w[k] = 0; }
+  for (int k = 0; k < 8; k++) zero.w[k] = 0;
+  red_a[threadIdx.x] = zero;
+  red_b[threadIdx.x] = zero;
   if (i < a.n) {
-    // weights (replacing random_scalar, batch.rs:240): one ChaCha20 block per proof
-    uint32_t blk[16];
-    chacha20_block(blk, a.seed, a.first_index + (uint64_t)i, 0);
-    const sc wa = rlc_weight(blk), wb = rlc_weight(blk + 4);
-    sc c;
-    rlc_load8(c.w, a.c, i);
+    // All scalar work first -- weights (replacing random_scalar, batch.rs:240: one ChaCha20
+    // block per proof), the four points' digits and the block-sum terms a s, b s (parked in
+    // LDS) -- so that nothing but the flags is live across the four decodes (56 VGPRs were
+    // spilled when the weights, c and s stayed in registers through them).
+    {
+      uint32_t blk[16];
+      chacha20_block(blk, a.seed, a.first_index + (uint64_t)i, 0);
+      const sc wa = rlc_weight(blk), wb = rlc_weight(blk + 4);
+      sc c, sv;
+      rlc_load8(c.w, a.c, i);
+      rlc_load8(sv.w, a.s, i);
+      // q = 0: -r1 (a), 1: -y1 (a c), 2: -r2 (b), 3: -y2 (b c); the r-points' digits are the
+      // weight words themselves (windows 8..15 empty)
+#pragma unroll 1
+      for (int q = 0; q < 4; q++) {
+        int16_t d[kRlcWindows];
+        if (q & 1) {
+          recode16(d, sc_mul(q == 1 ? wa : wb, c).w);
+        } else {
+          const uint32_t* u = q == 0 ? blk : blk + 4;
+#pragma unroll
+          for (int wv = 0; wv < kRlcWindows; wv++)
+            d[wv] = wv < 8 ? (int16_t)(u[wv >> 1] >> (16 * (wv & 1))) : (int16_t)0;
+        }
+#pragma unroll
+        for (int wv = 0; wv < kRlcWindows; wv++) a.digits[(int64_t)wv * a.dstride + 4 * i + q] = d[wv];
+      }
+      red_a[threadIdx.x] = sc_mul(wa, sv);
+      red_b[threadIdx.x] = sc_mul(wb, sv);
+    }
     bool ok = true, ident = false;
-    // q = 0: -r1 (a), 1: -y1 (a c), 2: -r2 (b), 3: -y2 (b c)
 #pragma unroll 1
     for (int q = 0; q < 4; q++) {
       const uint32_t* src = q == 0 ? a.r1 : (q == 1 ? a.y1 : (q == 2 ? a.r2 : a.y2));
@@ -153,19 +178,7 @@ __global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_prepare(RlcPrepArgs a)
       if (!(q & 1)) ident = words8_zero(w) || ident;
       ge_p3 P;
       ok = ristretto_decode(P, w) && ok;
-      const int64_t j = 4 * i + q;
-      store_niels(a.pts + j, niels_from_p3_affine(P, true));
-      int16_t d[kRlcWindows];
-      if (q & 1) {
-        recode16(d, sc_mul(q == 1 ? wa : wb, c).w);
-      } else {
-        const uint32_t* u = q == 0 ? blk : blk + 4;
-#pragma unroll
-        for (int wv = 0; wv < kRlcWindows; wv++)
-          d[wv] = wv < 8 ? (int16_t)(u[wv >> 1] >> (16 * (wv & 1))) : (int16_t)0;
-      }
-#pragma unroll
-      for (int wv = 0; wv < kRlcWindows; wv++) a.digits[(int64_t)wv * a.dstride + j] = d[wv];
+      store_niels(a.pts + 4 * i + q, niels_from_p3_affine(P, true));
     }
     const uint8_t st_s = a.status[i];
     uint8_t st;
@@ -175,21 +188,16 @@ __global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_prepare(RlcPrepArgs a)
     else if (st_s == kStZeroS) st = kStZeroS;
     else st = kStOk;
     a.status[i] = st;
-    if (st == kStOk) {
-      sc s;
-      rlc_load8(s.w, a.s, i);
-      as = sc_mul(wa, s);
-      bs = sc_mul(wb, s);
-    } else {
+    if (st != kStOk) {  // zero weight: no digits, no block-sum terms
       atomicOr(a.any_bad, 1);
+      red_a[threadIdx.x] = zero;
+      red_b[threadIdx.x] = zero;
       for (int q = 0; q < 4; q++)
 #pragma unroll
         for (int wv = 0; wv < kRlcWindows; wv++) a.digits[(int64_t)wv * a.dstride + 4 * i + q] = 0;
     }
   }
   // block sums of a_i s_i, b_i s_i (mod l)
-  red_a[threadIdx.x] = as;
-  red_b[threadIdx.x] = bs;
   __syncthreads();
   for (int off = kRlcPrepBlock / 2; off > 0; off >>= 1) {
     if (threadIdx.x < off) {

@@ -48,9 +48,9 @@ struct CombTable {
 };
 
 // Per-proof table of cached points (tab[0] = identity, tab[k] = k P), addressed as a base
-// pointer plus 32-bit byte offsets: 16-byte vector v of entry e at col + (e * kCachedVecs + v)
-// * stride.  The verify kernel keeps each thread's entries contiguous (stride 16, col = the
-// thread's slab slot).  Measured against two interleaved layouts in which one wave-wide load
+// pointer plus a 32-bit byte offset per entry: entry e at col + 160 e, its 16-byte vectors
+// contiguous.  The verify kernel keeps each thread's entries contiguous (col = the thread's
+// slab slot).  Measured against two interleaved layouts in which one wave-wide load
 // of a vector reads 1 KiB of consecutive slots (lane-interleaved over the whole slab, and
 // wave-interleaved: 64 lanes per 184 KB region): 48.0 M and 48.2 M against 51.8 M proofs/s for
 // the contiguous form (same gpurun call, two passes each) -- a lane's 9 entries in one 1.4 KB
@@ -58,22 +58,27 @@ struct CombTable {
 constexpr int kCachedVecs = (int)(sizeof(ge_cached) / 16);
 
 struct SlabTable {
-  char* base;       // slab (wave-uniform)
-  uint32_t col;     // this thread's column (t * 16) + the table's first entry
-  uint32_t stride;  // bytes between consecutive vectors of one thread
-  CPZ_HDM uint32_t off(int e, int v) const { return col + ((uint32_t)e * (uint32_t)kCachedVecs + (uint32_t)v) * stride; }
-    // the table that starts e0 entries further on
-  CPZ_HDM SlabTable shifted(int e0) const { return SlabTable{base, off(e0, 0), stride}; }
+  char* base;    // slab (wave-uniform)
+  uint32_t col;  // byte offset of this thread's table (entry 0)
+  static constexpr uint32_t kEntryBytes = kCachedVecs * 16;
+  // entry e: one 32-bit offset per lookup; the 16-byte vectors of the entry are then
+  // addressed as immediate offsets from it (computing base + 32-bit offset + 16 v in 32 bits
+  // per vector made the compiler hoist one address register per (entry, vector) out of the
+  // loops and spill)
+  CPZ_HDM const char* entry(int e) const { return base + (col + (uint32_t)e * kEntryBytes); }
+  // the table that starts e0 entries further on
+  CPZ_HDM SlabTable shifted(int e0) const { return SlabTable{base, col + (uint32_t)e0 * kEntryBytes}; }
   CPZ_HDM ge_cached load(int e) const {
     ge_cached r;
     uint32_t* d = reinterpret_cast<uint32_t*>(&r);
+    const char* p = entry(e);
 #pragma unroll
     for (int v = 0; v < kCachedVecs; v++) {
 #if defined(__HIP_DEVICE_COMPILE__)
-      const uint4 x = *reinterpret_cast<const uint4*>(base + off(e, v));
+      const uint4 x = *reinterpret_cast<const uint4*>(p + 16 * v);
       d[4 * v] = x.x; d[4 * v + 1] = x.y; d[4 * v + 2] = x.z; d[4 * v + 3] = x.w;
 #else
-      const uint32_t* s = reinterpret_cast<const uint32_t*>(base + off(e, v));
+      const uint32_t* s = reinterpret_cast<const uint32_t*>(p + 16 * v);
       for (int k = 0; k < 4; k++) d[4 * v + k] = s[k];
 #endif
     }
@@ -81,12 +86,13 @@ struct SlabTable {
   }
   CPZ_HDM void store(int e, const ge_cached& c) const {
     const uint32_t* s = reinterpret_cast<const uint32_t*>(&c);
+    char* p = const_cast<char*>(entry(e));
 #pragma unroll
     for (int v = 0; v < kCachedVecs; v++) {
 #if defined(__HIP_DEVICE_COMPILE__)
-      *reinterpret_cast<uint4*>(base + off(e, v)) = make_uint4(s[4 * v], s[4 * v + 1], s[4 * v + 2], s[4 * v + 3]);
+      *reinterpret_cast<uint4*>(p + 16 * v) = make_uint4(s[4 * v], s[4 * v + 1], s[4 * v + 2], s[4 * v + 3]);
 #else
-      uint32_t* d = reinterpret_cast<uint32_t*>(base + off(e, v));
+      uint32_t* d = reinterpret_cast<uint32_t*>(p + 16 * v);
       for (int k = 0; k < 4; k++) d[k] = s[4 * v + k];
 #endif
     }
@@ -104,7 +110,7 @@ struct DigitRef {
 CPZ_HD DigitRef host_digits(const uint32_t* a) { return DigitRef{a, 1}; }
 
 // A host array of cached points as a table (unit tests).
-CPZ_HD SlabTable host_table(ge_cached* p) { return SlabTable{reinterpret_cast<char*>(p), 0u, 16u}; }
+CPZ_HD SlabTable host_table(ge_cached* p) { return SlabTable{reinterpret_cast<char*>(p), 0u}; }
 
 CPZ_HD ge_niels niels_lookup(const ge_niels* tab, int digit) {
   const int mag = digit < 0 ? -digit : digit;

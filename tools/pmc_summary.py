@@ -66,8 +66,9 @@ if ve:
         ve["valu_instructions_per_proof"] = ve["SQ_INSTS_VALU"] * 64 / n
     ve["workload"] = ("%d proofs per launch (bench.py default 2^20 per step = 16 launches), rocprofv3 --pmc, "
                       "one counter group per pass" % n)
-    ve["correction"] = ("gfx950: FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads "
-                        "(MI355X_MICROARCH.md HBM) -> doubled; WRITE_SIZE as reported; units kB")
+    ve["correction"] = ("gfx950: FETCH_SIZE reports 64 B per 128-B L2 line miss, for coalesced streams and "
+                        "random 128/160-B gathers alike (MI355X_MICROARCH.md HBM; profiles/r02_gather_calibration.json) "
+                        "-> doubled; WRITE_SIZE as reported; units kB")
     ve["algorithmic_bytes_per_launch"] = 194 * n
     if "hbm_bytes_per_launch" in ve:
         ve["hbm_bytes_per_proof"] = ve["hbm_bytes_per_launch"] / n
@@ -91,6 +92,22 @@ if ve and os.path.exists(trace):
     steps = len(iv) * n / float(1 << 20)
     ve["trace_launches"] = len(iv)
     ve["trace_span_ns_per_2p20"] = union / steps if steps else None
+# The bench line printed by the kernel-trace pass itself: its HIP-event kernel time for
+# k_verify_each must agree with rocprof's average for the same launches.
+bench_line = None
+log = os.path.join(src, "prof_trace.log")
+if os.path.exists(log):
+    for line in open(log):
+        if line.startswith('{"metric"'):
+            bench_line = json.loads(line)
+if bench_line:
+    with open(os.path.join(prof, "%s_bench_under_profiler.json" % rnd), "w") as f:
+        json.dump(bench_line, f, indent=1, sort_keys=True)
+    ev = (bench_line.get("roofline") or {}).get("kernel_ms")
+    if ve and ev and ve.get("avg_ns"):
+        ve["bench_event_kernel_ms_same_run"] = ev
+        ve["rocprof_avg_kernel_ms"] = ve["avg_ns"] / 1e6
+        ve["event_vs_rocprof"] = ev / (ve["avg_ns"] / 1e6)
 summary = {"round": rnd, "source": "tools/profile.sh + tools/pmc_summary.py", "kernels": out}
 with open(os.path.join(prof, "%s_pmc.json" % rnd), "w") as f:
     json.dump(summary, f, indent=1, sort_keys=True)
