@@ -60,6 +60,11 @@ struct RlcMsmArgs {
   uint32_t* partial_out;         // 8 words
   int* identity_out;             // 1
   int w0 = 0, w1 = kRlcWindows;  // windows of this launch (bucket / fix / segment / window / final)
+  // A batch verified as several MSMs over consecutive proof spans: the final of each span
+  // adds its P into *total (the first span stores it), and only the last span encodes --
+  // the sum -- into partial_out / identity_out.  total == nullptr: a single MSM.
+  ge_p3* total = nullptr;
+  int total_first = 1, total_last = 1;
 };
 
 // Pipelined tails: the windows are cut into `groups` groups (a power of two <= 16); the

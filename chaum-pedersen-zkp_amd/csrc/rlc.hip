@@ -820,6 +820,13 @@ __global__ void __launch_bounds__(128) k_rlc_final(RlcMsmArgs a, int first, int 
   if (threadIdx.x < 4) {
     ge_p3 P = lds[0];
     if (!first) P = ge_add_quad(P, lds[kRlcWindows], q);
+    if (last && a.total) {  // one span of a multi-span batch
+      if (!a.total_first) P = ge_add_quad(load_p3(a.total), P, q);
+      if (!a.total_last) {
+        if (q == 0) store_p3(a.total, P);
+        return;
+      }
+    }
     if (!last) {
       if (q == 0) store_p3(a.acc, P);
     } else if (q == 0) {

@@ -118,7 +118,7 @@ struct cpz_ctx {
   hipEvent_t probe_done = nullptr;
   // RLC / Pippenger buffers (sized for the largest batch seen)
   DevBuf rl_pts, rl_dig, rl_bsum, rl_counts, rl_offsets, rl_bhist, rl_idx, rl_inter, rl_buckets, rl_heads, rl_segs,
-      rl_segw, rl_win, rl_acc,
+      rl_segw, rl_win, rl_acc, rl_total,
       rl_partial, rl_flags, rl_parts;
   int64_t rl_cap = 0;  // proofs
   // pipelined MSM tails (cpz::RlcPipe): a high-priority side stream and its events
@@ -543,11 +543,29 @@ cpz::RlcMsmArgs rlc_msm_args(cpz_ctx* ctx, int64_t lo, int64_t hi) {
 
 // MSM over proofs [lo, hi) (lo a multiple of kRlcPrepBlock) of the prepared batch.
 // Synchronises; returns the partial encoding and identity flag.
+#ifndef CPZ_RLC_SPAN
+#define CPZ_RLC_SPAN (1 << 20)  // proofs per MSM: the points of a span (512 MiB) stay gather-friendly
+#endif
+
+// P over proofs [lo, hi): one MSM per span of CPZ_RLC_SPAN proofs (aligned to the weight
+// blocks), each span's P added on the device (RlcMsmArgs::total).  Random 128-byte gathers
+// run at ~7 TB/s over a 512 MiB array but ~1.8 TB/s over 4 GiB (translation misses,
+// tools/ubench/gather_bytes.hip), so a 2^26-proof MSM over one 32 GiB points array spent
+// 2.8x the per-entry bucket time of a 2^20 one.
 int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t partial[32], int* identity) {
-  cpz::RlcMsmArgs m = rlc_msm_args(ctx, lo, hi);
-  const int64_t b0 = lo / cpz::kRlcPrepBlock;
-  const int64_t b1 = (hi + cpz::kRlcPrepBlock - 1) / cpz::kRlcPrepBlock;
-  {
+  static_assert(CPZ_RLC_SPAN % cpz::kRlcPrepBlock == 0, "spans are whole weight blocks");
+  const int64_t nspan = (hi - lo + CPZ_RLC_SPAN - 1) / CPZ_RLC_SPAN;
+  if (nspan > 1) CPZ_HIP(ctx->rl_total.ensure(sizeof(cpz::ge_p3)));
+  for (int64_t j = 0; j < nspan; j++) {
+    const int64_t slo = lo + j * CPZ_RLC_SPAN, shi = std::min<int64_t>(hi, slo + CPZ_RLC_SPAN);
+    cpz::RlcMsmArgs m = rlc_msm_args(ctx, slo, shi);
+    if (nspan > 1) {
+      m.total = static_cast<cpz::ge_p3*>(ctx->rl_total.p);
+      m.total_first = j == 0;
+      m.total_last = j == nspan - 1;
+    }
+    const int64_t b0 = slo / cpz::kRlcPrepBlock;
+    const int64_t b1 = (shi + cpz::kRlcPrepBlock - 1) / cpz::kRlcPrepBlock;
     StageTimer t(ctx, 3, st);
     // phase marks (stages 8-12) when timing: sort, bucket, bucket fix, segment + window, final
     hipEvent_t marks[cpz::kRlcMsmMarks];
@@ -1209,7 +1227,7 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   if (ctx->rl_pipe.done) (void)hipEventDestroy(ctx->rl_pipe.done);
   for (DevBuf* b : {&ctx->pz_blob, &ctx->pz_off, &ctx->pz_rows, &ctx->pz_code, &ctx->pz_aux}) b->release();
   for (DevBuf* b : {&ctx->rl_pts, &ctx->rl_dig, &ctx->rl_bsum, &ctx->rl_counts, &ctx->rl_offsets, &ctx->rl_bhist,
-                    &ctx->rl_idx, &ctx->rl_inter, &ctx->rl_buckets, &ctx->rl_heads, &ctx->rl_segs, &ctx->rl_segw, &ctx->rl_win, &ctx->rl_acc, &ctx->rl_partial,
+                    &ctx->rl_idx, &ctx->rl_inter, &ctx->rl_buckets, &ctx->rl_heads, &ctx->rl_segs, &ctx->rl_segw, &ctx->rl_win, &ctx->rl_acc, &ctx->rl_total, &ctx->rl_partial,
                     &ctx->rl_flags, &ctx->rl_parts})
     b->release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
