@@ -13,8 +13,11 @@ constexpr int kRlcBuckets = 1 << 15;     // |digit| in [1, 2^15]
 constexpr int kRlcSegLen = 16;           // buckets per reduction segment
 constexpr int kRlcPrepBlock = 256;       // proofs per prepare block (= block_sums granule)
 constexpr int kRlcSortBlock = 1024;
+#ifndef CPZ_RLC_SORT_CHUNK
+#define CPZ_RLC_SORT_CHUNK (1 << 16)
+#endif
 constexpr int kRlcSortGroups = 64;      // max blocks per window in the counting sort
-constexpr int64_t kRlcSortChunk = 1 << 16;  // target points per sort block
+constexpr int64_t kRlcSortChunk = CPZ_RLC_SORT_CHUNK;  // target points per sort block
 constexpr int kNielsEntriesRlc = kTableB;
 constexpr int kRlcChunk = 64;            // sorted entries per bucket-accumulation thread
 

@@ -544,7 +544,7 @@ cpz::RlcMsmArgs rlc_msm_args(cpz_ctx* ctx, int64_t lo, int64_t hi) {
 // MSM over proofs [lo, hi) (lo a multiple of kRlcPrepBlock) of the prepared batch.
 // Synchronises; returns the partial encoding and identity flag.
 #ifndef CPZ_RLC_SPAN
-#define CPZ_RLC_SPAN (1 << 20)  // proofs per MSM: the points of a span (512 MiB) stay gather-friendly
+#define CPZ_RLC_SPAN (1 << 21)  // proofs per MSM: the points of a span (1 GiB) stay gather-friendly
 #endif
 
 // P over proofs [lo, hi): one MSM per span of CPZ_RLC_SPAN proofs (aligned to the weight
