@@ -190,3 +190,20 @@ def test_calls_ordered_across_streams(gpu, golden):
     assert not st.any()
     side.synchronize()
     assert int((status != 0).sum().item()) == 0
+
+
+def test_security_tests_mirror(gpu):
+    """tests/security_tests.rs:136-163, 212-237 through the GPU path: an identity statement
+    (x = 0) is allowed and its proof verifies; malformed blobs are rejected by
+    Proof.from_bytes; a serialised proof is between 32 bytes and 1 KB."""
+    x = np.zeros((1, 32), np.uint8)
+    k = np.frombuffer(O.bench_scalar(b"k", 77).to_bytes(32, "little"), np.uint8).reshape(1, 32)
+    out = gpu.prove(x, k)
+    assert out["y1"][0].tobytes() == bytes(32) and out["y2"][0].tobytes() == bytes(32)
+    st = gpu.verify_each(out["y1"], out["y2"], out["r1"], out["r2"], out["s"])
+    assert list(st) == [0]
+    for blob in (b"", b"\x00", b"\xff" * 10, b"\x01" * 1000):
+        with pytest.raises(cp.Error):
+            cp.Proof.from_bytes(blob, gpu)
+    p = cp.Proof(out["r1"][0].tobytes(), out["r2"][0].tobytes(), out["s"][0].tobytes())
+    assert 32 < len(p.to_bytes()) < 1024 and cp.Proof.from_bytes(p.to_bytes(), gpu).to_bytes() == p.to_bytes()

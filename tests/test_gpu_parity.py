@@ -287,6 +287,19 @@ def test_ctx32_fast_path_and_mixed_contexts(gpu):
     for i in list(range(63)) + [63, 64, 65, 66, 1234, n - 1]:
         exp = O.challenge(O.G_BYTES, O.H_BYTES, *(bytes(a[i]) for a in rows[:4]), mixed[i])
         assert int.from_bytes(bytes(c[i]), "little") == exp, i
+    # a 4-byte context first: every later 32-byte context sits 4-byte but not 16-byte aligned
+    # in the blob, which still takes the register fast path (dword loads, no 16-byte access)
+    shifted = list(ctxs)
+    shifted[0] = b"\x01\x02\x03\x04"
+    r0 = _prove_oracle(900, shifted[0])
+    rows = [a.copy() for a in args]
+    for a, k in zip(rows, ("y1", "y2", "r1", "r2", "s")):
+        a[0] = np.frombuffer(getattr(r0, k), np.uint8)
+    assert not gpu.verify_each(*rows, contexts=shifted).any()
+    c = gpu.challenges(*rows[:4], contexts=shifted)
+    for i in (0, 1, 2, 3, 777, n - 1):
+        exp = O.challenge(O.G_BYTES, O.H_BYTES, *(bytes(a[i]) for a in rows[:4]), shifted[i])
+        assert int.from_bytes(bytes(c[i]), "little") == exp, i
 
 
 def test_host_pipeline_chunk_boundaries(gpu):
