@@ -317,8 +317,9 @@ def main():
               "phase_ms": {"challenge": ms.get("challenge", 0.0), "rlc_prepare": ms.get("rlc_prepare", 0.0),
                            "rlc_msm": ms.get("rlc_msm", 0.0), "fallback_per_proof": ms.get("fallback", 0.0)},
               "per_proof_only_ms": p_el * 1e3,
-              "note": "per_proof_only_ms: cpz_verify_each of the same batch (same statuses); the batch path "
-                      "pays its challenge + prepare + one MSM before the failure is known"}
+              "note": "per_proof_only_ms: cpz_verify_each of the same batch (same statuses); at this density "
+                      "the probe (4096 sampled proofs, run beside the challenges) finds the batch cannot pass, so "
+                      "nothing is prepared and no MSM runs"}
         del t5, st5
         torch.cuda.empty_cache()
 

@@ -528,6 +528,77 @@ __device__ __forceinline__ ge_p1p1 p1p1_identity_rlc() {
   return r;
 }
 
+#ifndef CPZ_RLC_BUCKET_LDS
+#define CPZ_RLC_BUCKET_LDS 0
+#endif
+#if CPZ_RLC_BUCKET_LDS
+// LDS-staged variant: the next entry's Niels point is brought into an LDS slot of the wave
+// by asynchronous direct-to-LDS loads (gfx950 global_load_lds_dwordx4) while the current
+// entry is added, instead of being prefetched into 30 VGPRs -- so the kernel fits 4 waves
+// per SIMD.  Each wave owns 8 x 64 x 16 B = 8 KB of LDS (32 KB per block).
+__device__ __forceinline__ void stage_point(uint4 (*slot)[64], const ge_niels* src) {
+  const uint4* g = reinterpret_cast<const uint4*>(src);
+#pragma unroll
+  for (int v = 0; v < 8; v++) __builtin_amdgcn_global_load_lds(g + v, &slot[v][0], 16, 0, 0);
+}
+
+__global__ void __launch_bounds__(256, 4) k_rlc_bucket(RlcMsmArgs a) {
+  __shared__ uint4 stage[4][8][64];
+  const int w = a.w0 + blockIdx.y;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
+  const uint32_t total = off[kRlcBuckets];
+  const int64_t e0l = t * kRlcChunk;
+  if (e0l >= (int64_t)total) return;
+  const uint32_t e0 = (uint32_t)e0l;
+  const uint32_t e1 = e0 + kRlcChunk < total ? e0 + kRlcChunk : total;
+  const uint32_t* idx = a.idx + (int64_t)w * a.istride;
+  ge_p3* bw = a.buckets + (int64_t)w * kRlcBuckets;
+  ge_p3* heads = a.heads + (int64_t)w * a.hstride;
+  int lo = 0, hi = kRlcBuckets - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= e0) lo = mid; else hi = mid - 1;
+  }
+  int b = lo;
+  uint32_t bend = off[b + 1];
+  bool head = off[b] < e0;
+  ge_p1p1 r = p1p1_identity_rlc();
+  uint32_t id = idx[idx_slot(e0)];
+  stage_point(stage[wv], a.pts + (id & 0x7fffffffu));
+  for (uint32_t e = e0; e < e1; e++) {
+    const bool neg = (id >> 31) != 0;
+    const uint32_t nid = e + 1 < e1 ? idx[idx_slot(e + 1)] : 0u;
+    ge_p3 acc = p1p1_to_p3(r);
+    // vmcnt counts loads and stores in issue order: the bucket-boundary loads go before the
+    // wait and the partial's store after the next point's staging, so the wait below never
+    // waits for a store issued in the same iteration
+    const bool emit = e == bend;
+    const int bo = b;
+    const bool ho = head;
+    if (emit) {
+      head = false;
+      do { b++; bend = off[b + 1]; } while (bend <= e);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this entry's point is in LDS
+    ge_niels p;
+    uint4* pv = reinterpret_cast<uint4*>(&p);
+#pragma unroll
+    for (int v = 0; v < 8; v++) pv[v] = stage[wv][v][lane];
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): read before the slot is refilled
+    if (e + 1 < e1) stage_point(stage[wv], a.pts + (nid & 0x7fffffffu));
+    id = nid;
+    if (emit) {
+      if (ho) store_p3(heads + t, acc); else store_p3(bw + bo, acc);
+      acc = ge_identity();
+    }
+    r = ge_add_niels(acc, ge_niels_cneg(p, neg));
+  }
+  const ge_p3 v = p1p1_to_p3(r);
+  if (head) store_p3(heads + t, v); else store_p3(bw + b, v);
+}
+#else
 // (141 VGPRs, 3 waves/SIMD; forcing 4 waves -- 128 VGPRs with spills -- measured 7 % slower)
 __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
   const int w = a.w0 + blockIdx.y;
@@ -568,6 +639,7 @@ __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
   const ge_p3 v = p1p1_to_p3(r);
   if (head) store_p3(heads + t, v); else store_p3(bw + b, v);
 }
+#endif
 
 // Buckets leave the fix-up in cached form (Y+X, Y-X, Z, 2dT, the same 160 bytes), so the
 // reduction kernels add them with 2 quad rounds and no conversion of their own.
