@@ -167,12 +167,12 @@ def main():
     import torch
     import torch.distributed as dist
 
-    if world > 1:
-        dist.init_process_group(args.backend, init_method="env://")
     if args.same_device:
         local_rank = 0
-    torch.cuda.set_device(local_rank)
+    torch.cuda.set_device(local_rank)  # before the process group, so RCCL binds each rank to its own GPU
     dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group(args.backend, init_method="env://")
 
     import chaum_pedersen as cp
     from chaum_pedersen.shard import all_gather_partials, shard_range
