@@ -89,7 +89,10 @@ def build_hosttest(force: bool = False) -> str:
         return HOSTTEST
     cxx = shutil.which("g++") or "g++"
     tmp = HOSTTEST + ".tmp"
-    _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-DCPZ_BOUNDS_CHECK", "-DCPZ_COUNT_OPS", "-I", CSRC, src, "-o", tmp])
+    # CPZ_HOST_DEFINES: extra -D flags to check a tuning variant of the device library on the CPU
+    extra = ["-D" + d for d in os.environ.get("CPZ_HOST_DEFINES", "").split()]
+    _run([cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-DCPZ_BOUNDS_CHECK", "-DCPZ_COUNT_OPS"] + extra +
+         ["-I", CSRC, src, "-o", tmp])
     os.replace(tmp, HOSTTEST)
     return HOSTTEST
 

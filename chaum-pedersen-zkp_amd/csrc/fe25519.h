@@ -12,9 +12,9 @@
 //
 // Limb bounds (checked by tests/test_device_arith.py through the host build of this
 // header, CPZ_BOUNDS_CHECK): a "tight" element (output of mul/sq/carry) has
-// |limb| <= 2^25 (+ a few units on limbs 1 and 5); add/sub of two tight elements is
-// "loose" (|limb| < 2^26.6) and is still a valid mul/sq operand: the worst column sum
-// is 267 * 2^26.6 * 2^26.6 < 2^63.
+// |limb| <= 2^25 (+ 2^7 from the high-word carry, a few units more on limb 1); add/sub
+// of two tight elements is "loose" (|limb| < 2^26.6) and is still a valid mul/sq operand:
+// the worst column sum is 267 * 2^26.6 * 2^26.6 < 2^63.
 //
 // Everything is __host__ __device__ so the exact same code can be unit-tested on the
 // CPU against the oracle; the product path only ever runs it on the GPU.
@@ -156,6 +156,15 @@ CPZ_HD int64_t acc_pin(int64_t x) {
   return x;
 }
 
+// A constant the compiler must not see through (kept in an SGPR): (int64)x * opaque_sgpr(2^k)
+// stays one v_mad_i64_i32 instead of becoming a 64-bit shift and add.
+CPZ_HD int32_t opaque_sgpr(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+s"(x));
+#endif
+  return x;
+}
+
 CPZ_HD int32_t unbias_limb(int64_t H, int k) {
   const uint32_t mask = (k & 1) ? 0x1ffffffu : 0x3ffffffu;
   return (int32_t)(((uint32_t)H & mask) - (uint32_t)carry_bias(k));
@@ -165,8 +174,37 @@ CPZ_HD int32_t unbias_limb(int64_t H, int k) {
 // column is carried once and the small wrap-around carry into limb 0 once more, so no
 // reduced limb has to be widened back to 64 bits (the two-chain ref10 order needs that
 // twice and is ~15 % more VALU work here).
+//
+// High-word carry (CPZ_CARRY_HI=1, default): with H = hi 2^32 + lo, column k's high word
+// moves into column k+1 as ONE v_mad_i64_i32 (hi * 2^(32-w) + H[k+1], the multiplier kept
+// opaque in an SGPR so LLVM does not turn it back into a 64-bit shift + add), and the few
+// bits of lo above the limb (lo >> w < 2^7) join limb k+1 in 32 bits (v_add3 with the
+// unbias).  Per column: 1 MAD + 3 32-bit ops instead of a 64-bit shift, a 64-bit add and 2
+// 32-bit ops; limbs end in [-2^(w-1), 2^(w-1) + 127).  k_verify_each 2.155 -> 2.105 ms per
+// launch (A/B, two alternating runs each, one box).  =0 selects the shift/add chain.
+#ifndef CPZ_CARRY_HI
+#define CPZ_CARRY_HI 1
+#endif
 CPZ_HD fe fe_carry_biased(int64_t H[10]) {
   fe r;
+#if CPZ_CARRY_HI
+  uint32_t small = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    const int w = (k & 1) ? 25 : 26;
+    const int32_t hi = (int32_t)(H[k] >> 32);
+    const uint32_t lo = (uint32_t)H[k];
+    H[k + 1] = acc_pin((int64_t)hi * (int64_t)opaque_sgpr(1 << (32 - w)) + H[k + 1]);
+    r.v[k] = (int32_t)((lo & ((1u << w) - 1u)) - (uint32_t)carry_bias(k) + small);
+    small = lo >> w;
+  }
+  const int32_t hi9 = (int32_t)(H[9] >> 32);
+  const uint32_t lo9 = (uint32_t)H[9];
+  r.v[9] = (int32_t)((lo9 & 0x1ffffffu) - (uint32_t)carry_bias(9) + small);
+  // carry out of limb 9 = hi9 2^7 + (lo9 >> 25), times 19 into limb 0 (biased, then centred)
+  const int64_t h0 = (int64_t)hi9 * (int64_t)opaque_sgpr(19 << 7) +
+                     (int64_t)(uint64_t)(((uint32_t)r.v[0] + (uint32_t)carry_bias(0)) + 19u * (lo9 >> 25));
+#else
 #pragma unroll
   for (int k = 0; k < 9; k++) {
     H[k + 1] += H[k] >> ((k & 1) ? 25 : 26);
@@ -175,6 +213,7 @@ CPZ_HD fe fe_carry_biased(int64_t H[10]) {
   const int64_t c9 = H[9] >> 25;
   r.v[9] = unbias_limb(H[9], 9);
   const int64_t h0 = (int64_t)r.v[0] + 19 * c9 + carry_bias(0);
+#endif
   r.v[1] += (int32_t)(h0 >> 26);
   r.v[0] = unbias_limb(h0, 0);
   return r;

@@ -388,7 +388,28 @@ __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each(
   // digit words and point encodings in LDS, one column per thread (scalarmul.h, DigitRef)
   __shared__ uint32_t dig[16 * kVerifyBlock];
   __shared__ uint32_t rows[32 * kVerifyBlock];
+#if defined(CPZ_CLOCK_PROBE)
+  // Timing variant only (tools/time_verify.py): the shader clock (s_memtime) and the constant
+  // 100 MHz clock (s_memrealtime) around this wave's work and the wave's hardware id, written
+  // over the wave's 64 status bytes (the verdicts are lost) -> the clock the kernel actually
+  // ran at and how many of its waves each SIMD held over time.
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), q0 = __builtin_amdgcn_s_memrealtime();
+#endif
   verify_one_row(a, i, comb_g, comb_h, tab, dig + threadIdx.x, rows + threadIdx.x);
+#if defined(CPZ_CLOCK_PROBE)
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), q1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0 && i + 63 < a.n) {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    uint64_t* out = reinterpret_cast<uint64_t*>(a.status + i);
+    out[0] = t1 - t0;
+    out[1] = q1 - q0;
+    out[2] = q0;  // absolute 100 MHz stamps and the wave's SIMD: a per-SIMD occupancy timeline
+    out[3] = q1;
+    out[4] = (uint64_t)hw | ((uint64_t)xcc << 32);
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------

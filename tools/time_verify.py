@@ -30,6 +30,39 @@ def main():
     v_ms, v_cnt = st.get("verify_each", (0.0, 1))
     print("%-14s verify_each %.3f ms  rejected %d" % (os.path.basename(os.environ.get("CPZ_LIB", "default")),
                                                      v_ms / v_cnt, int((status != 0).sum().item())))
+    if os.environ.get("CLOCK"):
+        # a CPZ_CLOCK_PROBE build (last step's launches): per wave, shader-clock and 100 MHz
+        # ticks of its work, its absolute 100 MHz start / end and its SIMD
+        import numpy as np
+        w = status.cpu().numpy().view("uint64").reshape(-1, 8)[:, :5].astype("int64")
+        ghz = w[:, 0] / (w[:, 1] / 100e6) / 1e9
+        us = w[:, 1] / 100.0
+        print("clock probe: %d waves, shader clock %.3f GHz (p10 %.3f, p90 %.3f), wave time %.0f us (p10 %.0f, p90 %.0f)"
+              % (len(ghz), ghz.mean(), np.percentile(ghz, 10), np.percentile(ghz, 90), us.mean(),
+                 np.percentile(us, 10), np.percentile(us, 90)))
+        hw = w[:, 4]
+        # HW_REG_HW_ID: simd [5:4], cu [11:8], sh [12], se [15:13]; XCC id in the high word
+        simd = ((hw >> 32) << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 7) | (((hw >> 8) & 15) << 3) | \
+            ((hw >> 4) & 3)
+        t0, t1 = w[:, 2], w[:, 3]
+        lo, hi = t0.min(), t1.max()
+        span_us = (hi - lo) / 100.0
+        busy = 0.0
+        occ = np.zeros(4)
+        for sid in np.unique(simd):
+            m = simd == sid
+            ev = sorted([(x, 1) for x in t0[m]] + [(x, -1) for x in t1[m]])
+            cur, last = 0, lo
+            for x, d in ev:
+                occ[min(cur, 3)] += x - last
+                last, cur = x, cur + d
+            occ[0] += hi - last
+            busy += (t1[m] - t0[m]).sum()
+        nsimd = len(np.unique(simd))
+        occ /= occ.sum()
+        print("timeline: %d SIMDs, span %.0f us (first wave start .. last wave end), mean waves/SIMD %.3f; "
+              "time share with 0/1/2/3+ waves resident: %s" % (nsimd, span_us, busy / nsimd / (hi - lo),
+                                                               " / ".join("%.3f" % x for x in occ)))
 
 
 if __name__ == "__main__":
