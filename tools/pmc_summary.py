@@ -70,6 +70,10 @@ if ve:
                         "random 128/160-B gathers alike (MI355X_MICROARCH.md HBM; profiles/r02_gather_calibration.json) "
                         "-> doubled; WRITE_SIZE as reported; units kB")
     ve["algorithmic_bytes_per_launch"] = 194 * n
+    # two launches overlap on two streams, so GRBM_GUI_ACTIVE / duration is not its clock; the
+    # in-kernel probe (s_memtime against s_memrealtime per wave) is
+    ve.pop("effective_clock_ghz", None)
+    ve["clock"] = "in-kernel probe: profiles/%s_verify_clock_probe.json (CPZ_CLOCK_PROBE, tools/time_verify.py)" % rnd
     if "hbm_bytes_per_launch" in ve:
         ve["hbm_bytes_per_proof"] = ve["hbm_bytes_per_launch"] / n
     ve["source"] = "profiles/%s_verify_each_pmc.json (tools/profile.sh + tools/pmc_summary.py)" % rnd
