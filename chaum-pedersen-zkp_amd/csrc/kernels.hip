@@ -384,7 +384,12 @@ __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each(
   const int64_t i = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
   if (i >= a.n) return;
   // this thread's tables: kCachedEntries entries, contiguous (scalarmul.h, SlabTable)
+#if defined(CPZ_EXP_SLAB_MOD)
+  // timing experiment only (wrong verdicts: threads share slots): an L2-sized slab
+  const SlabTable tab{a.scratch, (uint32_t)(i % CPZ_EXP_SLAB_MOD) * (uint32_t)(kCachedEntries * sizeof(ge_cached))};
+#else
   const SlabTable tab{a.scratch, (uint32_t)i * (uint32_t)(kCachedEntries * sizeof(ge_cached))};
+#endif
   // digit words and point encodings in LDS, one column per thread (scalarmul.h, DigitRef)
   __shared__ uint32_t dig[16 * kVerifyBlock];
   __shared__ uint32_t rows[32 * kVerifyBlock];
