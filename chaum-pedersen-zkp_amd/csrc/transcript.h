@@ -53,6 +53,37 @@ CPZ_HD uint64_t KECCAK_RC(int i) {
   return rc[i];
 }
 
+// Three-input bitwise function on 64-bit lanes: gfx950's v_bitop3_b32 on each half
+// (truth table imm = f(S0 = 0xF0, S1 = 0xCC, S2 = 0xAA)), so theta's five-way XOR and chi
+// are one instruction per 32 bits where plain code needs two.  LLVM does not form these
+// from the 64-bit expressions below by itself.
+#ifndef CPZ_KECCAK_BITOP3
+#define CPZ_KECCAK_BITOP3 1  // 0: plain XOR / AND-NOT (A/B variant)
+#endif
+template <int IMM>
+CPZ_HD uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__) && CPZ_KECCAK_BITOP3
+  uint32_t lo, hi;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(lo) : "v"((uint32_t)a), "v"((uint32_t)b), "v"((uint32_t)c),
+      "i"(IMM));
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(hi)
+      : "v"((uint32_t)(a >> 32)), "v"((uint32_t)(b >> 32)), "v"((uint32_t)(c >> 32)), "i"(IMM));
+  return ((uint64_t)hi << 32) | lo;
+#elif !CPZ_KECCAK_BITOP3
+  return IMM == 0x96 ? (a ^ b ^ c) : (a ^ (~b & c));
+#else
+  uint64_t r = 0;
+  for (int k = 0; k < 8; k++)
+    if ((IMM >> k) & 1) {
+      const uint64_t ma = (k & 4) ? a : ~a, mb = (k & 2) ? b : ~b, mc = (k & 1) ? c : ~c;
+      r |= ma & mb & mc;
+    }
+  return r;
+#endif
+}
+constexpr int kXor3 = 0x96;   // a ^ b ^ c
+constexpr int kChi = 0xD2;    // a ^ (~b & c)
+
 // In-place Keccak-f[1600] on 25 lanes, lane index x + 5y.
 CPZ_HD void keccak_f1600(uint64_t a[25]) {
   // rho offsets and pi destinations in lane order.
@@ -61,7 +92,8 @@ CPZ_HD void keccak_f1600(uint64_t a[25]) {
   for (int round = 0; round < 24; round++) {
     uint64_t c[5], b[25];
 #pragma unroll
-    for (int x = 0; x < 5; x++) c[x] = a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20];
+    for (int x = 0; x < 5; x++)
+      c[x] = bitop3_64<kXor3>(bitop3_64<kXor3>(a[x], a[x + 5], a[x + 10]), a[x + 15], a[x + 20]);
 #pragma unroll
     for (int x = 0; x < 5; x++) {
       const uint64_t d = c[(x + 4) % 5] ^ rol64(c[(x + 1) % 5], 1);
@@ -80,7 +112,7 @@ CPZ_HD void keccak_f1600(uint64_t a[25]) {
     for (int y = 0; y < 5; y++) {
 #pragma unroll
       for (int x = 0; x < 5; x++)
-        a[x + 5 * y] = b[x + 5 * y] ^ ((~b[(x + 1) % 5 + 5 * y]) & b[(x + 2) % 5 + 5 * y]);
+        a[x + 5 * y] = bitop3_64<kChi>(b[x + 5 * y], b[(x + 1) % 5 + 5 * y], b[(x + 2) % 5 + 5 * y]);
     }
     a[0] ^= KECCAK_RC(round);
   }
