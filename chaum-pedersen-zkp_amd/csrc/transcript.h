@@ -69,16 +69,9 @@ CPZ_HD uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(hi)
       : "v"((uint32_t)(a >> 32)), "v"((uint32_t)(b >> 32)), "v"((uint32_t)(c >> 32)), "i"(IMM));
   return ((uint64_t)hi << 32) | lo;
-#elif !CPZ_KECCAK_BITOP3
-  return IMM == 0x96 ? (a ^ b ^ c) : (a ^ (~b & c));
 #else
-  uint64_t r = 0;
-  for (int k = 0; k < 8; k++)
-    if ((IMM >> k) & 1) {
-      const uint64_t ma = (k & 4) ? a : ~a, mb = (k & 2) ? b : ~b, mc = (k & 1) ? c : ~c;
-      r |= ma & mb & mc;
-    }
-  return r;
+  static_assert(IMM == 0x96 || IMM == 0xD2, "plain forms of the two truth tables Keccak uses");
+  return IMM == 0x96 ? (a ^ b ^ c) : (a ^ (~b & c));
 #endif
 }
 constexpr int kXor3 = 0x96;   // a ^ b ^ c

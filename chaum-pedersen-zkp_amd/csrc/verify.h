@@ -327,6 +327,15 @@ CPZ_HD uint8_t verify_proof(const DigitRef& y1, const DigitRef& y2, const DigitR
                             const Comb& comb_h, const SlabTable& tab_v, uint32_t* dig, int dstride,
                             const ge_niels* pre = nullptr) {
   bool vneg;
+#if defined(CPZ_EXP_NOSPLIT)
+  // timing experiment only (wrong verdicts): the challenge split, v s and the recodings skipped
+  vneg = c[7] & 1;
+  for (int k = 0; k < 8; k++) {
+    dig[k * dstride] = c[k];
+    dig[(8 + k) * dstride] = s[k];
+  }
+  if (0)
+#endif
   {
     uint32_t u[4], va[4], w[8];
     sc_half_split(c, u, va, vneg);
