@@ -6,6 +6,10 @@ checker; test infrastructure only):
   wrong y1, wrong context, undecodable point, non-canonical s, zero s, identity commitment.
   Statuses AND challenges of the whole sample equal the oracle's (batch.rs:185-231,
   transcript.rs:29-71, gadgets.rs:364-489); every entry outside it is valid.
+* C3 (configs[2]) shaped like the reference service's batches (service.rs:512-517: every entry
+  carries its 32-byte challenge id as transcript context): 2^20 proofs, s + 1 and wrong-context
+  forgeries; the batch partial equals the oracle's partial of the forged entries alone and the
+  fallback's bisection returns exactly the forged set.
 * C5 (configs[4]) and C4 (configs[3]): the RLC partial of a forged batch -- whole batch and
   every shard, weights keyed by the global index -- equals, byte for byte, the oracle's
   partial computed from the forged entries ALONE (valid entries contribute the identity, so
@@ -122,6 +126,28 @@ def _oracle_partial(host, gidx, lo=None, hi=None):
     enc, live = C.rlc_partial({k: host[k][m] for k in KEYS}, gidx[m], WSEED, threads=_threads())
     assert live == int(m.sum())
     return enc
+
+
+def test_c3_service_contexts_partial_and_bisection(gpu):
+    n = 1 << 20
+    rng = np.random.default_rng(33)
+    ctxs = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(n)]
+    rows = gpu.prove_synthetic(n, SX, SK, contexts=ctxs)
+    rows = {k: np.ascontiguousarray(rows[k]) for k in KEYS}
+    # few forgeries, spread out, so the bisection prunes clean parts (no density probe with contexts)
+    forged = np.sort(rng.choice(n, size=24, replace=False))
+    for j, i in enumerate(forged):
+        if j % 2:
+            ctxs[i] = bytes(32)  # replayed under another challenge id
+        else:
+            rows["s"][i] = np.frombuffer(((_le(rows["s"][i]) + 1) % O.L).to_bytes(32, "little"), np.uint8)
+    partial, ok, st = gpu.verify_batch(*(rows[k] for k in KEYS), seed=WSEED, contexts=ctxs)
+    assert not ok
+    assert np.array_equal(np.nonzero(st)[0], forged) and set(st[forged].tolist()) == {1}
+    sub = {k: rows[k][forged] for k in KEYS}
+    want, live = C.rlc_partial(sub, forged, WSEED, contexts=[ctxs[i] for i in forged], threads=_threads())
+    assert live == forged.size
+    assert partial == want
 
 
 def test_c5_partial_from_forged_entries_alone(gpu):
