@@ -367,6 +367,9 @@ __global__ void __launch_bounds__(1024) k_rlc_scan(RlcMsmArgs a) {
 //                 it spans < 1 MB, so its writes still merge in L2.
 // A coarse bin's region of `inter` is the same range of positions its buckets occupy in
 // idx, so both passes share the offsets from k_rlc_scan.
+// Coarse-sorted entries are 32 bits (CPZ_RLC_INTER32, rlc.h): fine bucket (7 bits) << 25 |
+// sign << 24 | flat position t of the point in this MSM (t < kRlcMaxMsmPoints); k_rlc_fine maps
+// t back to the point id.  (64-bit entries with the id itself: CPZ_RLC_INTER32=0.)
 constexpr int kRlcCoarse = 256;
 constexpr int kRlcFinePerCoarse = kRlcBuckets / kRlcCoarse;  // 128
 constexpr int kRlcTile = 8192;
@@ -400,7 +403,11 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_coarse(RlcMsmArgs a) {
   const int64_t c0 = (int64_t)g * a.chunk;
   const int64_t c1 = c0 + a.chunk < total ? c0 + a.chunk : total;
   const int16_t* dig = a.digits + (int64_t)w * a.dstride;
+#if CPZ_RLC_INTER32
+  uint32_t* inter = reinterpret_cast<uint32_t*>(a.inter) + (int64_t)w * a.istride;
+#else
   uint64_t* inter = a.inter + (int64_t)w * a.istride;
+#endif
   constexpr int per_thread = kRlcTile / kRlcSortBlock;  // 8
   for (int64_t t0 = c0; t0 < c1; t0 += kRlcTile) {
     uint64_t ent[per_thread];
@@ -415,8 +422,14 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_coarse(RlcMsmArgs a) {
         if (d != 0) {
           const uint32_t b = (uint32_t)((d < 0 ? -d : d) - 1);
           const uint32_t c = b / kRlcFinePerCoarse;
+#if CPZ_RLC_INTER32
+          (void)j;
+          ent[k] = ((uint64_t)c << 40) | ((uint32_t)(b % kRlcFinePerCoarse) << 25) | (d < 0 ? (1u << 24) : 0u) |
+                   (uint32_t)t;
+#else
           ent[k] = ((uint64_t)c << 40) | ((uint64_t)(b % kRlcFinePerCoarse) << 32) | (uint32_t)j |
                    (d < 0 ? 0x80000000u : 0u);
+#endif
           rank[k] = atomicAdd(&cnt[c], 1u);
         }
       }
@@ -451,7 +464,11 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_coarse(RlcMsmArgs a) {
     for (uint32_t e = tid; e < nt; e += kRlcSortBlock) {
       const uint64_t v = buf[e];
       const uint32_t c = (uint32_t)(v >> 40);
+#if CPZ_RLC_INTER32
+      inter[gbase[c] + (e - start[c])] = (uint32_t)v;
+#else
       inter[gbase[c] + (e - start[c])] = v & 0xffffffffffull;
+#endif
     }
     __syncthreads();
     if (tid < kRlcCoarse) {
@@ -486,9 +503,27 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_fine(RlcMsmArgs a) {
   const bool staged = r1 - r0 <= (uint32_t)kRlcFineCap;
   if (tid < kRlcFinePerCoarse) cur[tid] = off[tid] - (staged ? r0 : 0u);
   __syncthreads();
-  const uint64_t* inter = a.inter + (int64_t)w * a.istride;
   uint32_t* idx = a.idx + (int64_t)w * a.istride;
   constexpr int U = 4;  // loads in flight per thread
+#if CPZ_RLC_INTER32
+  const uint32_t* inter = reinterpret_cast<const uint32_t*>(a.inter) + (int64_t)w * a.istride;
+  for (uint32_t e0 = r0 + tid; e0 < r1; e0 += U * kRlcSortBlock) {
+    uint32_t v[U];
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      const uint32_t e = e0 + k * kRlcSortBlock;
+      v[k] = e < r1 ? inter[e] : ~0u;  // t < 2^24 - 1: an entry is never ~0
+    }
+#pragma unroll
+    for (int k = 0; k < U; k++) {
+      if (v[k] == ~0u) continue;
+      const uint32_t pos = atomicAdd(&cur[v[k] >> 25], 1u);
+      const uint32_t id = (uint32_t)msm_point(a, v[k] & 0xffffffu) | ((v[k] << 7) & 0x80000000u);
+      if (staged) img[pos] = id; else idx[idx_slot(pos)] = id;
+    }
+  }
+#else
+  const uint64_t* inter = a.inter + (int64_t)w * a.istride;
   for (uint32_t e0 = r0 + tid; e0 < r1; e0 += U * kRlcSortBlock) {
     uint64_t v[U];
 #pragma unroll
@@ -503,6 +538,7 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_fine(RlcMsmArgs a) {
       if (staged) img[pos] = (uint32_t)v[k]; else idx[idx_slot(pos)] = (uint32_t)v[k];
     }
   }
+#endif
   if (!staged) return;
   __syncthreads();
   for (uint32_t e = tid; e < r1 - r0; e += kRlcSortBlock) idx[idx_slot(r0 + e)] = img[e];

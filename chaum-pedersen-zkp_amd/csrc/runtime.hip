@@ -554,6 +554,7 @@ cpz::RlcMsmArgs rlc_msm_args(cpz_ctx* ctx, int64_t lo, int64_t hi) {
 // 2.8x the per-entry bucket time of a 2^20 one.
 int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t partial[32], int* identity) {
   static_assert(CPZ_RLC_SPAN % cpz::kRlcPrepBlock == 0, "spans are whole weight blocks");
+  static_assert(4ll * CPZ_RLC_SPAN + 2 <= cpz::kRlcMaxMsmPoints, "a span's MSM exceeds the sort-entry format");
   const int64_t nspan = (hi - lo + CPZ_RLC_SPAN - 1) / CPZ_RLC_SPAN;
   if (nspan > 1) CPZ_HIP(ctx->rl_total.ensure(sizeof(cpz::ge_p3)));
   for (int64_t j = 0; j < nspan; j++) {
@@ -951,6 +952,7 @@ int cpz_verify_batch_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[3
 
 int cpz_msm(cpz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalars, uint8_t out[32]) {
   if (!ctx || !points || !scalars || !out || n == 0) return fail(CPZ_EINVAL, "bad arguments");
+  if ((int64_t)n + 2 > cpz::kRlcMaxMsmPoints) return fail(CPZ_EINVAL, "too many points for one MSM call");
   for (size_t j = 0; j < n; j++)
     if (scalars[32 * j + 31] & 0xe0) return fail(CPZ_EINVAL, "scalars must be below 2^253");
   std::lock_guard<std::mutex> lock(ctx->mu);

@@ -174,8 +174,8 @@ int cpz_verify_batch_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[3
 int cpz_decode_points(cpz_ctx *ctx, size_t n, const uint8_t *points, uint8_t *ok_out, uint8_t *reencoded_out);
 
 /* Multi-scalar multiplication through the same Pippenger kernels: out = enc(sum_j [k_j] P_j)
- * for n encoded points and n scalars (little-endian, < 2^253).  Exposed for testing the MSM
- * against the oracle with adversarial digit patterns. */
+ * for n encoded points and n scalars (little-endian, < 2^253), n <= 2^24 - 3 (CPZ_EINVAL above).
+ * Exposed for testing the MSM against the oracle with adversarial digit patterns. */
 int cpz_msm(cpz_ctx *ctx, size_t n, const uint8_t *points, const uint8_t *scalars, uint8_t out[32]);
 
 /* Sum k 32-byte partials (per-GPU shards) on the device: out = encoding of the sum,
