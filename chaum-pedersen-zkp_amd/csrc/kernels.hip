@@ -396,8 +396,9 @@ __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each(
 #if defined(CPZ_CLOCK_PROBE)
   // Timing variant only (tools/time_verify.py): the shader clock (s_memtime) and the constant
   // 100 MHz clock (s_memrealtime) around this wave's work and the wave's hardware id, written
-  // over the wave's 64 status bytes (the verdicts are lost) -> the clock the kernel actually
-  // ran at and how many of its waves each SIMD held over time.
+  // over the wave's 64 status bytes (the verdicts are lost; the status buffer must be 8-byte
+  // aligned, as the timing harness's is) -> the clock the kernel actually ran at and how many
+  // of its waves each SIMD held over time.
   const uint64_t t0 = __builtin_amdgcn_s_memtime(), q0 = __builtin_amdgcn_s_memrealtime();
 #endif
   verify_one_row(a, i, comb_g, comb_h, tab, dig + threadIdx.x, rows + threadIdx.x);
