@@ -197,7 +197,7 @@ __global__ void __launch_bounds__(64) k_build_niels(const uint32_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------
-// Fixed-base combs (scalarmul.h): comb[b][k][j - 1] = j * 2^(16 k) * base_b, affine Niels.
+// Fixed-base combs (scalarmul.h): comb[b][k][j] = j * 2^(16 k) * base_b, affine Niels (j = 0: identity).
 // k_comb_bases: thread (b, k) doubles base_b 16 k times.  k_comb_fill: one thread per
 // entry, [j] Q_(b,k) by double-and-add over the 15-bit j, then one inversion to affine.
 // 2^20 entries, a few milliseconds, once per (g, h) pair.
@@ -216,8 +216,12 @@ __global__ void __launch_bounds__(64) k_comb_bases(const uint32_t* __restrict__ 
 __global__ void __launch_bounds__(256) k_comb_fill(const ge_p3* __restrict__ q, ge_niels* __restrict__ comb) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= 2 * kCombPerBase) return;
-  const int bk = (int)(t / kCombEntries);  // b * kCombWindows + k
-  const int j = (int)(t % kCombEntries) + 1;
+  const int bk = (int)(t / kCombStride);  // b * kCombWindows + k
+  const int j = (int)(t % kCombStride);
+  if (j == 0) {
+    comb[t] = ge_niels_identity();
+    return;
+  }
   const ge_p3 Q = q[bk];
   ge_p3 acc = Q;  // bit 15 of j set only for j = 2^15
   const int top = 31 - __builtin_clz((unsigned)j);
@@ -558,7 +562,7 @@ hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* 
 
 hipError_t launch_build_comb(const uint32_t* gh_words, ge_p3* bases_scratch, ge_niels* comb, hipStream_t st) {
   hipLaunchKernelGGL(k_comb_bases, dim3(1), dim3(64), 0, st, gh_words, bases_scratch);
-  hipLaunchKernelGGL(k_comb_fill, dim3((unsigned)(2 * kCombPerBase / 256)), dim3(256), 0, st,
+  hipLaunchKernelGGL(k_comb_fill, dim3((unsigned)((2 * kCombPerBase + 255) / 256)), dim3(256), 0, st,
                      (const ge_p3*)bases_scratch, comb);
   return hipGetLastError();
 }

@@ -22,18 +22,20 @@ constexpr int kTableSlots = kTableV + 1;  // + the identity at slot 0 (digit 0 n
 constexpr int kTableB = 128;   // Niels multiples 1..128 of a fixed base (radix-256 digits)
 
 // Fixed-base comb: for each of the 16 radix-2^16 windows k, the affine Niels multiples
-// j * 2^(16 k) * B, j = 1..2^15, of one base (64 MiB per base in HBM).  [s] B for any
-// s < 2^253 is then 16 mixed additions and no doubling.
+// j * 2^(16 k) * B, j = 0..2^15 (slot 0 the identity, so a zero digit needs no select), of one
+// base (64 MiB per base in HBM).  [s] B for any s < 2^253 is then 16 mixed additions and no
+// doubling.
 constexpr int kCombWindows = 16;
-constexpr int kCombEntries = 1 << 15;
-constexpr int64_t kCombPerBase = (int64_t)kCombWindows * kCombEntries;
+constexpr int kCombEntries = 1 << 15;          // nonzero multiples per window
+constexpr int kCombStride = kCombEntries + 1;  // + the identity at slot 0
+constexpr int64_t kCombPerBase = (int64_t)kCombWindows * kCombStride;
 
 // Device view of one base's comb (entries in global memory).
 struct CombTable {
   const ge_niels* p;
   CPZ_HDM ge_niels lookup(int k, int digit) const {
     const int mag = digit < 0 ? -digit : digit;
-    const ge_niels* e = p + (int64_t)k * kCombEntries + (mag == 0 ? 0 : mag - 1);
+    const ge_niels* e = p + (int64_t)k * kCombStride + mag;
     ge_niels r;
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint4* s = reinterpret_cast<const uint4*>(e);
@@ -43,7 +45,7 @@ struct CombTable {
 #else
     r = *e;
 #endif
-    return ge_niels_cneg(mag == 0 ? ge_niels_identity() : r, digit < 0);
+    return ge_niels_cneg(r, digit < 0);
   }
 };
 
