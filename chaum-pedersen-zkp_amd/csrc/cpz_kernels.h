@@ -116,6 +116,9 @@ hipError_t launch_parse_proofs(const ParseArgs& a, hipStream_t st);
 // Fixed-base combs of 2 bases (g, h): bases_scratch holds 2 * kCombWindows ge_p3.
 hipError_t launch_build_comb(const uint32_t* gh_words, ge_p3* bases_scratch, ge_niels* comb, hipStream_t st);
 hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st);
+#if defined(CPZ_VERIFY_DYNAMIC)
+hipError_t launch_verify_each_queue(const VerifyArgs& a, int grid, unsigned* work, hipStream_t st);
+#endif
 int verify_each_blocks_per_cu();  // resident k_verify_each blocks per CU (occupancy API)
 hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st);
 hipError_t launch_prove_response(const ProveArgs& a, hipStream_t st);

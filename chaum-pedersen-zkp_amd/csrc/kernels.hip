@@ -422,6 +422,36 @@ __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each(
 #endif
 }
 
+#if defined(CPZ_VERIFY_DYNAMIC)
+// Work-queue variant (A/B only): one launch of the resident grid; each wave takes the next 64
+// proofs from a global counter until the batch is exhausted (every wave leaves once the
+// counter passes n), so no launch boundary inside a batch leaves SIMDs half occupied.
+__global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each_queue(VerifyArgs a, unsigned* work) {
+  const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
+  const int64_t gtid = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
+  const SlabTable tab{a.scratch, (uint32_t)gtid * (uint32_t)(kCachedEntries * sizeof(ge_cached))};
+  __shared__ uint32_t dig[16 * kVerifyBlock];
+  __shared__ uint32_t rows[32 * kVerifyBlock];
+  const int lane = threadIdx.x & 63;
+  for (;;) {
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(work, 64u);
+    base = (unsigned)__shfl((int)base, 0, 64);
+    if ((int64_t)base >= a.n) break;
+    const int64_t i = (int64_t)base + lane;
+    if (i < a.n) verify_one_row(a, i, comb_g, comb_h, tab, dig + threadIdx.x, rows + threadIdx.x);
+  }
+}
+
+hipError_t launch_verify_each_queue(const VerifyArgs& a, int grid, unsigned* work, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_verify_each_queue, dim3(grid), dim3(kVerifyBlock), 0, st, a, work);
+  return hipGetLastError();
+}
+#endif
+
 // ---------------------------------------------------------------------------------------
 // Synthetic prover (input generator): x_i, k_i = wide(ChaCha20(seed_x / seed_k, block i)).
 // ---------------------------------------------------------------------------------------

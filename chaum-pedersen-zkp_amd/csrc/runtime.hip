@@ -99,6 +99,7 @@ struct cpz_ctx {
   DevBuf c;         // n x 32
   DevBuf st;        // n
   DevBuf scratch;   // per-stream table slabs (kCachedEntries ge_cached per thread)
+  DevBuf work;      // work-queue counter (CPZ_VERIFY_DYNAMIC variant)
   // host-API staging (y1, y2, r1, r2, s, and challenges / witnesses / nonces)
   DevBuf in[7];
   DevBuf ctxb, ctxo, ctxp;
@@ -416,6 +417,21 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
     // itself (c_buf is left unwritten; no caller reads it after a verify)
     va.fused = static_cast<const uint32_t*>(ctx->chal_fused.p);
     return launch_verify_chunks(ctx, va, 1, st, rr, join);
+  }
+#endif
+#if defined(CPZ_VERIFY_DYNAMIC)
+  if (rr == nullptr) {  // device-resident batch: challenges up front, then one work-queue launch
+    {
+      StageTimer tc(ctx, 0, st);
+      CPZ_HIP(cpz::launch_challenge(ca, st));
+    }
+    const int g = verify_grid(ctx, n);
+    CPZ_HIP(ctx->scratch.ensure((size_t)g * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached)));
+    CPZ_HIP(ctx->work.ensure(64));
+    va.scratch = static_cast<char*>(ctx->scratch.p);
+    StageTimer t(ctx, 1, st);
+    CPZ_HIP(cpz::launch_verify_each_queue(va, g, static_cast<unsigned*>(ctx->work.p), st));
+    return CPZ_OK;
   }
 #endif
 #if CPZ_CHALLENGE_PER_CHUNK
@@ -1197,6 +1213,7 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->c.release();
   ctx->st.release();
   ctx->scratch.release();
+  ctx->work.release();
   for (auto& b : ctx->in) b.release();
   ctx->ctxb.release();
   ctx->ctxo.release();
