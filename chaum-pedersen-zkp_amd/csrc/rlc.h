@@ -10,7 +10,10 @@ namespace cpz {
 
 constexpr int kRlcWindows = 16;          // 16-bit signed windows cover scalars < 2^255
 constexpr int kRlcBuckets = 1 << 15;     // |digit| in [1, 2^15]
-constexpr int kRlcSegLen = 16;           // buckets per reduction segment
+#ifndef CPZ_RLC_SEGLEN
+#define CPZ_RLC_SEGLEN 32
+#endif
+constexpr int kRlcSegLen = CPZ_RLC_SEGLEN;  // buckets per reduction segment
 constexpr int kRlcPrepBlock = 256;       // proofs per prepare block (= block_sums granule)
 constexpr int kRlcSortBlock = 1024;
 #ifndef CPZ_RLC_SORT_CHUNK
