@@ -837,7 +837,10 @@ __global__ void __launch_bounds__(256, 2) k_rlc_segment(RlcMsmArgs a) {
 // .. L t + L (L = kRlcSegLen):  T_w = sum_t W_t + L * sum_t t S_t.  Quad u owns the
 // P = nseg / 128 segments P u .. P u + P - 1:  A_u = sum_j S_{Pu+j},  M_u = sum_j j S_{Pu+j},
 //   sum_t t S_t = P sum_u u A_u + sum_u M_u,   sum_u u A_u = sum_{k>=1} suffix_k(A).
-constexpr int kRlcWinQuads = 128;  // 512 threads: 256 VGPRs without spills (1024 spill)
+#ifndef CPZ_RLC_WIN_QUADS
+#define CPZ_RLC_WIN_QUADS 128
+#endif
+constexpr int kRlcWinQuads = CPZ_RLC_WIN_QUADS;  // 512 threads: 256 VGPRs without spills (1024 spill)
 __global__ void __launch_bounds__(4 * kRlcWinQuads) k_rlc_window(RlcMsmArgs a) {
   __shared__ ge_p3 lds[kRlcWinQuads], lds_m[kRlcWinQuads], lds_w[kRlcWinQuads];
   __builtin_amdgcn_s_setprio(3);
