@@ -19,8 +19,10 @@ verification result on the CPU.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import struct
+import threading
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -285,16 +287,25 @@ def _torch_stream(stream):
 class Gpu:
     """A verifier context on one GPU (cpz_ctx).  Bulk entry points, no batch cap."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, timing_only: bool = False):
+        """timing_only: open the context of a timing-only build (tools/time_verify.py); the
+        product library has no such entry point and its verdicts are the only ones."""
         lib = _native.load()
         ndev = lib.cpz_device_count()
         if ndev <= 0:
             raise CpzError(_native.CPZ_EHIP, "no GPU visible to the HIP runtime")
         h = ctypes.c_void_p()
-        _native.check(lib.cpz_ctx_create(device, ctypes.byref(h)))
+        create = lib.cpz_ctx_create
+        if timing_only:
+            if not hasattr(lib, "cpz_ctx_create_timing_only"):
+                raise CpzError(_native.CPZ_EINVAL, "not a timing-only build")
+            create = lib.cpz_ctx_create_timing_only
+        _native.check(create(device, ctypes.byref(h)))
         self._lib = lib
         self._h = h
         self.device = device
+        self._checks = True
+        self._mode_lock = threading.RLock()
 
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -324,8 +335,29 @@ class Gpu:
         """{stage: (total_ms, launches)} since the previous call (synchronises)."""
         ms = (ctypes.c_double * _native.NUM_STAGES)()
         cnt = (ctypes.c_int * _native.NUM_STAGES)()
-        _native.check(self._lib.cpz_ctx_stage_times(self._h, ms, cnt))
+        _native.check(self._lib.cpz_ctx_stage_times_n(self._h, _native.NUM_STAGES, ms, cnt))
         return {self.STAGES[k]: (ms[k], cnt[k]) for k in range(_native.NUM_STAGES) if cnt[k]}
+
+    # -- commitment checks (cpz_ctx_set_commitment_checks) ------------------------------------
+    def set_commitment_checks(self, enable: bool) -> None:
+        """On (default): statuses 4 / 5 for identity commitments and zero s, the rejections of
+        Proof::from_bytes (gadgets.rs:474-482).  Off: the equations alone decide, as
+        verify_one (batch.rs:185-231) does for a Proof built with Proof::new."""
+        with self._mode_lock:
+            _native.check(self._lib.cpz_ctx_set_commitment_checks(self._h, 1 if enable else 0))
+            self._checks = bool(enable)
+
+    @contextlib.contextmanager
+    def commitment_checks(self, enable: bool):
+        """Scoped set_commitment_checks (restores the previous mode; calls on this object from
+        other threads wait for the scope)."""
+        with self._mode_lock:
+            prev = self._checks
+            self.set_commitment_checks(enable)
+            try:
+                yield self
+            finally:
+                self.set_commitment_checks(prev)
 
     # -- host-buffer entry points ---------------------------------------------------------
     def verify_each(self, y1, y2, r1, r2, s, contexts=None, params: Optional[Parameters] = None) -> np.ndarray:
@@ -580,6 +612,25 @@ class Transcript:
         self.context = bytes(context)
 
 
+_VALID_STATEMENTS: "dict" = {}   # (y1, y2) -> decodes; a registered user's statement repeats
+
+
+def _validate_statement(gpu: Gpu, statement: "Statement") -> None:
+    """Statement::validate (gadgets.rs:234-238 -> ristretto.rs:173-185): both elements must be
+    group elements -- here, both encodings must decode (device decode, cpz_decode_points).
+    A Rust Statement holds decoded points, so its validate() cannot fail; bytes can.
+    Statements already seen to decode are remembered (bounded), so a batch of one user's
+    proofs costs one device call."""
+    key = (statement.y1, statement.y2)
+    if key not in _VALID_STATEMENTS:
+        ok, _ = gpu.decode_points(np.frombuffer(statement.y1 + statement.y2, np.uint8).reshape(2, 32))
+        if not ok.all():
+            raise InvalidGroupElement("Element failed recompression validation")
+        if len(_VALID_STATEMENTS) >= 4096:
+            _VALID_STATEMENTS.clear()
+        _VALID_STATEMENTS[key] = True
+
+
 def _raise_status(st: int) -> None:
     if st != STATUS_OK:
         raise VerifyResult(st).error()
@@ -599,17 +650,20 @@ class Verifier:
     def verify_with_transcript(self, proof: Proof, transcript: Transcript) -> None:
         """verifier/mod.rs:120-139; raises the reference's error, returns None on Ok(())."""
         g = self._gpu or _gpu()
+        _validate_statement(g, self.statement)  # verifier/mod.rs:121
         one = lambda b: np.frombuffer(b, np.uint8).reshape(1, 32)
-        st = g.verify_each(one(self.statement.y1), one(self.statement.y2), one(proof.r1), one(proof.r2),
-                           one(proof.s), contexts=[transcript.context], params=self.params)
+        with g.commitment_checks(False):  # the equations only (verifier/mod.rs:144-171)
+            st = g.verify_each(one(self.statement.y1), one(self.statement.y2), one(proof.r1), one(proof.r2),
+                               one(proof.s), contexts=[transcript.context], params=self.params)
         _raise_status(int(st[0]))
 
     def verify_response(self, challenge, proof: Proof) -> None:
         """verifier/mod.rs:144-171: the caller's challenge (int mod l or 32 canonical bytes)."""
         g = self._gpu or _gpu()
         one = lambda b: np.frombuffer(b, np.uint8).reshape(1, 32)
-        st = g.verify_response(one(self.statement.y1), one(self.statement.y2), one(proof.r1), one(proof.r2),
-                               one(proof.s), one(_scalar_bytes(challenge)), params=self.params)
+        with g.commitment_checks(False):
+            st = g.verify_response(one(self.statement.y1), one(self.statement.y2), one(proof.r1), one(proof.r2),
+                                   one(proof.s), one(_scalar_bytes(challenge)), params=self.params)
         _raise_status(int(st[0]))
 
 
@@ -669,17 +723,19 @@ class BatchVerifier:
     back to per-entry verification and its n == 1 path is verify_one.
     """
 
-    def __init__(self, gpu: Optional[Gpu] = None):
+    def __init__(self, gpu: Optional[Gpu] = None, capacity: int = 0):
         self._entries: List[_Entry] = []
         self._gpu = gpu
+        self.capacity = min(int(capacity), MAX_BATCH_SIZE)   # batch.rs:113-118 (a reservation only)
 
     @classmethod
     def new(cls) -> "BatchVerifier":
         return cls()
 
     @classmethod
-    def with_capacity(cls, capacity: int) -> "BatchVerifier":
-        return cls()
+    def with_capacity(cls, capacity: int, gpu: Optional[Gpu] = None) -> "BatchVerifier":
+        """batch.rs:113-118: capacity.min(MAX_BATCH_SIZE) reserved; no effect on results."""
+        return cls(gpu, capacity)
 
     def len(self) -> int:
         return len(self._entries)
@@ -699,6 +755,7 @@ class BatchVerifier:
                          context: Optional[bytes]) -> None:
         if len(self._entries) >= MAX_BATCH_SIZE:
             raise InvalidParams("Batch size limit exceeded (max %d)" % MAX_BATCH_SIZE)
+        _validate_statement(self._gpu or _gpu(), statement)   # batch.rs:158
         self._entries.append(_Entry(params, statement, proof, None if context is None else bytes(context)))
 
     def clear(self) -> None:
@@ -706,7 +763,9 @@ class BatchVerifier:
 
     def verify(self, rng=None) -> List[VerifyResult]:
         """batch.rs:171-183.  `rng` is accepted for signature parity; per-entry
-        verification consumes no randomness."""
+        verification consumes no randomness.  Entries are `Proof` values, which may have been
+        built with Proof(...) (Proof::new: no identity / zero-s checks), so the context runs
+        with commitment checks off: verify_one's equations alone decide (batch.rs:185-231)."""
         if not self._entries:
             raise InvalidParams("Cannot verify empty batch")
         gpu = self._gpu or _gpu()
@@ -717,12 +776,13 @@ class BatchVerifier:
             groups.setdefault((e.params.g, e.params.h), []).append(i)
         for (g, h), idx in groups.items():
             ents = [self._entries[i] for i in idx]
-            st = gpu.verify_each(
-                np.frombuffer(b"".join(e.statement.y1 for e in ents), np.uint8).reshape(-1, 32),
-                np.frombuffer(b"".join(e.statement.y2 for e in ents), np.uint8).reshape(-1, 32),
-                np.frombuffer(b"".join(e.proof.r1 for e in ents), np.uint8).reshape(-1, 32),
-                np.frombuffer(b"".join(e.proof.r2 for e in ents), np.uint8).reshape(-1, 32),
-                np.frombuffer(b"".join(e.proof.s for e in ents), np.uint8).reshape(-1, 32),
-                contexts=[e.context for e in ents], params=Parameters(g, h))
+            with gpu.commitment_checks(False):
+                st = gpu.verify_each(
+                    np.frombuffer(b"".join(e.statement.y1 for e in ents), np.uint8).reshape(-1, 32),
+                    np.frombuffer(b"".join(e.statement.y2 for e in ents), np.uint8).reshape(-1, 32),
+                    np.frombuffer(b"".join(e.proof.r1 for e in ents), np.uint8).reshape(-1, 32),
+                    np.frombuffer(b"".join(e.proof.r2 for e in ents), np.uint8).reshape(-1, 32),
+                    np.frombuffer(b"".join(e.proof.s for e in ents), np.uint8).reshape(-1, 32),
+                    contexts=[e.context for e in ents], params=Parameters(g, h))
             status[np.array(idx)] = st
         return [VerifyResult(s) for s in status]

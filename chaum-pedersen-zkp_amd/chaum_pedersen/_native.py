@@ -33,8 +33,10 @@ EXPORTED = (
     "cpz_verify_batch", "cpz_verify_batch_device", "cpz_combine_partials", "cpz_msm",
     "cpz_parse_proofs", "cpz_parse_proofs_device", "cpz_verify_each_multi", "cpz_verify_batch_multi",
     "cpz_verify_response", "cpz_verify_response_device", "cpz_prove", "cpz_prove_device", "cpz_decode_points",
+    "cpz_abi_version", "cpz_ctx_set_commitment_checks", "cpz_ctx_stage_times_n",
 )
 NUM_STAGES = 16
+ABI_VERSION = 3     # CPZ_ABI_VERSION of the cpz.h these declarations follow
 
 
 class CpzError(RuntimeError):
@@ -103,6 +105,15 @@ def _declare(lib):
     lib.cpz_prove_device.argtypes = [_p, _p, _p, ctypes.c_size_t, _p, _p, _p, _p, _p] + [_p] * 5 + [_p]
     lib.cpz_decode_points.restype = ctypes.c_int
     lib.cpz_decode_points.argtypes = [_p, ctypes.c_size_t, _p, _p, _p]
+    lib.cpz_abi_version.restype = ctypes.c_int
+    lib.cpz_abi_version.argtypes = []
+    lib.cpz_ctx_set_commitment_checks.restype = ctypes.c_int
+    lib.cpz_ctx_set_commitment_checks.argtypes = [_p, ctypes.c_int]
+    lib.cpz_ctx_stage_times_n.restype = ctypes.c_int
+    lib.cpz_ctx_stage_times_n.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(ctypes.c_int)]
+    lib.cpz_ctx_create_timing_only.restype = ctypes.c_int
+    lib.cpz_ctx_create_timing_only.argtypes = [ctypes.c_int, ctypes.POINTER(_p)]
     lib.cpz_prove_synthetic_device.restype = ctypes.c_int
     lib.cpz_prove_synthetic_device.argtypes = ([_p, _p, _p, ctypes.c_size_t, ctypes.c_uint64, _p, _p, _p, _p,
                                                 _p] + [_p] * 5 + [_p])
@@ -139,12 +150,15 @@ def load(path: str = LIB_PATH):
             except Exception:
                 pass
             lib = ctypes.CDLL(path)
-            if os.environ.get("CPZ_LIB"):
-                # a tuning variant (tools/variants.sh) may predate newer entry points: declare
-                # what it exports; the product library must export everything (test_abi)
-                _declare(_Tolerant(lib))
-            else:
-                _declare(lib)
+            # every library declares what it exports: cpz_ctx_create_timing_only exists only in
+            # timing-only builds, and a tuning variant (tools/variants.sh) may predate newer
+            # entry points; the product library must export all of EXPORTED (test_abi)
+            _declare(_Tolerant(lib))
+            if not os.environ.get("CPZ_LIB"):
+                got = lib.cpz_abi_version()
+                if got != ABI_VERSION:
+                    raise CpzError(CPZ_EINVAL, "%s has ABI version %d, these bindings follow %d: rebuild it"
+                                   % (path, got, ABI_VERSION))
             _lib = lib
         return _lib
 

@@ -45,6 +45,14 @@ MAX_USER_ID_LEN = 256          # service.rs:42
 class InvalidArgument(Exception):
     """`Status::invalid_argument` for the whole request (service.rs:419-433)."""
 
+    code = "INVALID_ARGUMENT"
+
+
+class AlreadyExists(Exception):
+    """`Status::already_exists`: the user id is taken (service.rs:108-112)."""
+
+    code = "ALREADY_EXISTS"
+
 
 @dataclass
 class VerificationResult:
@@ -143,8 +151,8 @@ def register(state, user_id: str, y1: bytes, y2: bytes, gpu=None) -> None:
     """The `register` handler (service.rs:61-131) minus rate limiting and metrics: user id
     checks, sizes, element_from_bytes of y1 and y2 (on the device, cpz_decode_points),
     identity statements rejected, then state.register_user.  Raises InvalidArgument with
-    the reference's status message (AlreadyExists for a taken id is InvalidArgument here,
-    with the reference's "Registration failed: ..." text)."""
+    the reference's status message, or AlreadyExists ("Registration failed: ...",
+    service.rs:108-112) for a taken id."""
     msg = validate_user_id(user_id)
     if msg:
         raise InvalidArgument(msg)
@@ -170,7 +178,7 @@ def register(state, user_id: str, y1: bytes, y2: bytes, gpu=None) -> None:
     try:
         state.register_user(user_id, y1, y2)
     except Error as e:
-        raise InvalidArgument("Registration failed: %s" % error_display(e))
+        raise AlreadyExists("Registration failed: %s" % error_display(e))
 
 
 def verify_proof_batch(state, user_ids: Sequence[str], challenge_ids: Sequence[bytes], proofs: Sequence[bytes],

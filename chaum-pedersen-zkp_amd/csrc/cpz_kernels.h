@@ -49,6 +49,7 @@ struct ChallengeArgs {
   uint32_t k2[50];
   int fast_ctx32 = 0;            // prefix[0] at the fixed position: 32-byte contexts take
   uint32_t c32[3][50];           // challenge_fixed_ctx32 with these masks (challenge_masks_ctx32)
+  int eq_only = 0;               // commitment checks off: a zero s is not reported (response_status)
 };
 
 // Proof::from_bytes outcome codes (gadgets.rs:364-489); kept equal to CPZ_PARSE_* in cpz.h.
@@ -89,6 +90,8 @@ struct VerifyArgs {
                                     // the kernel computes c and the response status itself from these
                                     // 100 words (prefix ^ k1, then k2: challenge_fixed's constants)
                                     // instead of reading c / status from k_challenge
+  int eq_only = 0;                  // commitment checks off: identity r1 / r2 and zero s are not
+                                    // reported, the equations alone decide (verify_proof)
 };
 
 struct ProveArgs {
@@ -126,6 +129,6 @@ hipError_t launch_prove_response(const ProveArgs& a, hipStream_t st);
 hipError_t launch_decode_encode(int64_t n, const uint32_t* pts, uint8_t* ok, uint32_t* out, hipStream_t st);
 // cpz_verify_response: response status of s and the caller's challenge (sanitised copy to c_out).
 hipError_t launch_response_prep(int64_t n, const uint32_t* s, const uint32_t* c_in, uint32_t* c_out, uint8_t* status,
-                                hipStream_t st);
+                                int eq_only, hipStream_t st);
 
 }  // namespace cpz

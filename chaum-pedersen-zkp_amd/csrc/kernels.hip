@@ -152,7 +152,7 @@ __global__ void __launch_bounds__(kChallengeBlock) k_challenge(ChallengeArgs a) 
   if (a.s != nullptr) {
     uint32_t w[8];
     load_words8(w, a.s, i);
-    a.status_out[i] = response_status(w);
+    a.status_out[i] = response_status(w, a.eq_only != 0);
   }
 }
 // No-context fast path (verify.h, challenge_fixed): the sponge in 50 registers, the
@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(256) k_challenge_noctx(ChallengeArgs a) {
   if (a.s != nullptr) {
     uint32_t w[8];
     load_words8(w, a.s, i);
-    a.status_out[i] = response_status(w);
+    a.status_out[i] = response_status(w, a.eq_only != 0);
   }
 }
 
@@ -344,7 +344,7 @@ __device__ __forceinline__ void verify_one_row(const VerifyArgs& a, int64_t i, c
     const sc c = challenge_fixed_pk(a.fused, a.fused + 50, w[0], w[1], w[2], w[3]);
 #pragma unroll
     for (int k = 0; k < 8; k++) cw[k] = c.w[k];
-    st_s = response_status(sw);
+    st_s = response_status(sw, a.eq_only != 0);
   } else {
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -359,7 +359,8 @@ __device__ __forceinline__ void verify_one_row(const VerifyArgs& a, int64_t i, c
   }
   const DigitRef y1{rows, kVerifyBlock}, y2{rows + 8 * kVerifyBlock, kVerifyBlock},
       r1{rows + 16 * kVerifyBlock, kVerifyBlock}, r2{rows + 24 * kVerifyBlock, kVerifyBlock};
-  a.status[i] = verify_proof(y1, y2, r1, r2, sw, cw, st_s, comb_g, comb_h, tab, dig, kVerifyBlock);
+  a.status[i] = verify_proof(y1, y2, r1, r2, sw, cw, st_s, comb_g, comb_h, tab, dig, kVerifyBlock, nullptr,
+                             a.eq_only != 0);
 }
 
 // The RLC fallback's per-proof pass (rlc_fallback): points, challenges and decode-level
@@ -377,7 +378,7 @@ __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_prepa
     load_words8(cw, a.c, i);
     const DigitRef none{nullptr, 0};
     a.status[i] = verify_proof<true>(none, none, none, none, sw, cw, kStOk, comb_g, comb_h, tab, dig + threadIdx.x,
-                                     kVerifyBlock, a.pre + 4 * i);
+                                     kVerifyBlock, a.pre + 4 * i, a.eq_only != 0);
   }
 }
 
@@ -389,7 +390,7 @@ __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each(
   if (i >= a.n) return;
   // this thread's tables: kCachedEntries entries, contiguous (scalarmul.h, SlabTable)
 #if defined(CPZ_EXP_SLAB_MOD)
-  // timing experiment only (wrong verdicts: threads share slots): an L2-sized slab
+  // timing experiment only (wrong verdicts: threads share slots; timing_only.h): an L2-sized slab
   const SlabTable tab{a.scratch, (uint32_t)(i % CPZ_EXP_SLAB_MOD) * (uint32_t)(kCachedEntries * sizeof(ge_cached))};
 #else
   const SlabTable tab{a.scratch, (uint32_t)i * (uint32_t)(kCachedEntries * sizeof(ge_cached))};
@@ -398,7 +399,7 @@ __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each(
   __shared__ uint32_t dig[16 * kVerifyBlock];
   __shared__ uint32_t rows[32 * kVerifyBlock];
 #if defined(CPZ_CLOCK_PROBE)
-  // Timing variant only (tools/time_verify.py): the shader clock (s_memtime) and the constant
+  // Timing variant only (tools/time_verify.py; timing_only.h): the shader clock (s_memtime) and the constant
   // 100 MHz clock (s_memrealtime) around this wave's work and the wave's hardware id, written
   // over the wave's 64 status bytes (the verdicts are lost; the status buffer must be 8-byte
   // aligned, as the timing harness's is) -> the clock the kernel actually ran at and how many
@@ -542,13 +543,13 @@ hipError_t launch_decode_encode(int64_t n, const uint32_t* pts, uint8_t* ok, uin
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_response_prep(int64_t n, const uint32_t* __restrict__ s,
                                                        const uint32_t* __restrict__ c_in, uint32_t* __restrict__ c_out,
-                                                       uint8_t* __restrict__ status) {
+                                                       uint8_t* __restrict__ status, int eq_only) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   uint32_t w[8], c[8];
   load_words8(w, s, i);
   load_words8(c, c_in, i);
-  uint8_t st = response_status(w);
+  uint8_t st = response_status(w, eq_only != 0);
   const bool c_ok = sc_is_canonical(c);
   if (st == kStOk && !c_ok) st = kStBadChallenge;
 #pragma unroll
@@ -627,9 +628,10 @@ hipError_t launch_parse_proofs(const ParseArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_response_prep(int64_t n, const uint32_t* s, const uint32_t* c_in, uint32_t* c_out, uint8_t* status,
-                                hipStream_t st) {
+                                int eq_only, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_response_prep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, s, c_in, c_out, status);
+  hipLaunchKernelGGL(k_response_prep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, s, c_in, c_out, status,
+                     eq_only);
   return hipGetLastError();
 }
 

@@ -46,6 +46,7 @@ struct RlcPrepArgs {
   int64_t dstride;
   sc* block_sums;                // [ceil(n/256)][2]
   int* any_bad;                  // set to 1 if some proof has a non-zero decode-level status
+  int eq_only = 0;               // commitment checks off: identity r1 / r2 keep their weight
 };
 
 struct RlcMsmArgs {

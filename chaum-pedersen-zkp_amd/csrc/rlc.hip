@@ -31,6 +31,8 @@
 //   k_rlc_final     2^(16w) combine, encode -> 32-byte partial + identity flag.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "rlc.h"
 #include "verify.h"
 
@@ -184,7 +186,7 @@ __global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_prepare(RlcPrepArgs a)
     uint8_t st;
     if (!ok) st = kStBadPoint;
     else if (st_s == kStBadScalar) st = kStBadScalar;
-    else if (ident) st = kStIdentity;
+    else if (ident && !a.eq_only) st = kStIdentity;
     else if (st_s == kStZeroS) st = kStZeroS;
     else st = kStOk;
     a.status[i] = st;
@@ -1022,12 +1024,17 @@ hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0,
   hipLaunchKernelGGL(k_rlc_extra, dim3(1), dim3(256), 0, st, a, block_sums, b0, b1, tab);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const size_t lds = sizeof(uint32_t) * kRlcBuckets;  // 128 KB of the 160 KB LDS
-  static bool attr_set = false;
-  if (!attr_set) {
+  // The attribute is per device: one bit per ordinal (contexts on several GPUs launch from
+  // their own threads, cpz_verify_batch_multi; setting it twice is harmless).
+  static std::atomic<uint64_t> attr_set{0};
+  int dev = 0;
+  if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+  const uint64_t bit = dev < 64 ? (uint64_t)1 << dev : 0;
+  if (!bit || !(attr_set.load(std::memory_order_acquire) & bit)) {
     if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rlc_hist),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) != hipSuccess)
       return e;
-    attr_set = true;
+    attr_set.fetch_or(bit, std::memory_order_release);
   }
   const int64_t nb = (int64_t)kRlcWindows * kRlcBuckets;
   hipLaunchKernelGGL(k_rlc_hist, dim3(a.groups, kRlcWindows), dim3(kRlcSortBlock), lds, st, a);

@@ -73,6 +73,39 @@ constexpr size_t kPipeChunk = size_t(1) << 17;
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// partial_out of a batch check that skipped its MSM (dense fallback): 32 x 0xff, not an encoding
+bool is_no_partial(const uint8_t p[32]) {
+  for (int k = 0; k < 32; k++)
+    if (p[k] != 0xff) return false;
+  return true;
+}
+
+// RLC buffers come in two sets with their own capacities, and an MSM's arguments are derived
+// from the sets it is handed, never from a context-wide size (rlc_msm_args):
+//   RlcPrepared  the batch's prepared MSM input: 4 n + 2 negated Niels points, the digit rows
+//                [16][dstride], per-256-proof block sums.  Capacity: proofs of the batch.
+//   RlcMsmSet    sort / bucket / reduction buffers of ONE MSM, its partial and identity flag.
+//                Capacity: proofs of one MSM (a span of at most CPZ_RLC_SPAN proofs).
+struct RlcPrepared {
+  DevBuf pts, dig, bsum;
+  int64_t cap = 0;
+  void release() {
+    for (DevBuf* b : {&pts, &dig, &bsum}) b->release();
+    cap = 0;
+  }
+};
+
+struct RlcMsmSet {
+  DevBuf counts, offsets, bhist, idx, inter, buckets, heads, segs, segw, win, acc, total, partial, flags;
+  int64_t cap = 0;
+  void release() {
+    for (DevBuf* b : {&counts, &offsets, &bhist, &idx, &inter, &buckets, &heads, &segs, &segw, &win, &acc, &total,
+                      &partial, &flags})
+      b->release();
+    cap = 0;
+  }
+};
+
 }  // namespace
 
 struct cpz_ctx {
@@ -117,11 +150,14 @@ struct cpz_ctx {
   DevBuf probe;
   hipStream_t probe_stream = nullptr;
   hipEvent_t probe_done = nullptr;
-  // RLC / Pippenger buffers (sized for the largest batch seen)
-  DevBuf rl_pts, rl_dig, rl_bsum, rl_counts, rl_offsets, rl_bhist, rl_idx, rl_inter, rl_buckets, rl_heads, rl_segs,
-      rl_segw, rl_win, rl_acc, rl_total,
-      rl_partial, rl_flags, rl_parts;
-  int64_t rl_cap = 0;  // proofs
+  // RLC / Pippenger buffers: the prepared batch and one MSM set (each sized for the largest
+  // batch / span seen), plus flags (any_bad at [3], cpz_msm's bad point at [2], the combine's
+  // decode / identity flags at [0..1]) and the combine's inputs
+  RlcPrepared rl_prep;
+  RlcMsmSet rl_msm;
+  DevBuf rl_flags, rl_parts;
+  // commitment checks (statuses 4 and 5: the Proof::from_bytes rejections); off = equations only
+  bool eq_only = false;
   // pipelined MSM tails (cpz::RlcPipe): a high-priority side stream and its events
   cpz::RlcPipe rl_pipe;
   // Completion of the last call's work on whatever stream it used: the *_device entry points
@@ -250,6 +286,7 @@ int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32]) {
 
 // The fixed-schedule challenge paths and their masks (set per (g, h) by ensure_generators).
 void set_challenge_schedules(const cpz_ctx* ctx, cpz::ChallengeArgs& ca) {
+  ca.eq_only = ctx->eq_only ? 1 : 0;
   ca.fast_noctx = ctx->prefix_fixed ? 1 : 0;
   std::memcpy(ca.k1, ctx->chal_k1, sizeof(ca.k1));
   std::memcpy(ca.k2, ctx->chal_k2, sizeof(ca.k2));
@@ -410,6 +447,7 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   va.status = status;
   va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
   va.scratch = nullptr;  // set per launch
+  va.eq_only = ca.eq_only;
   StageTimer span(ctx, 5, st);  // all chunks, all streams (the launches overlap)
 #if CPZ_VERIFY_FUSED
   if (ca.ctx_off == nullptr && ctx->prefix_fixed) {
@@ -505,79 +543,110 @@ int64_t rlc_dstride(int64_t cap) { return (4 * cap + 2 + 7) & ~(int64_t)7; }
 // sorted-entry row stride: whole 4096-entry groups (k_rlc_fine stores them transposed)
 int64_t rlc_istride(int64_t cap) { return (4 * cap + 2 + 4095) & ~(int64_t)4095; }
 
-int rlc_reserve(cpz_ctx* ctx, int64_t n) {
-  if (n <= ctx->rl_cap) return CPZ_OK;
+// The prepared set for a batch of n proofs.
+int rlc_reserve_prepared(RlcPrepared& P, int64_t n) {
+  if (n <= P.cap) return CPZ_OK;
   const int64_t npts = 4 * n + 2;
   const int64_t nblk = (n + cpz::kRlcPrepBlock - 1) / cpz::kRlcPrepBlock;
-  CPZ_HIP(ctx->rl_pts.ensure((size_t)npts * sizeof(cpz::ge_niels)));
-  CPZ_HIP(ctx->rl_dig.ensure((size_t)rlc_dstride(n) * cpz::kRlcWindows * sizeof(int16_t)));
-  CPZ_HIP(ctx->rl_bsum.ensure((size_t)nblk * 2 * sizeof(cpz::sc)));
-  CPZ_HIP(ctx->rl_counts.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcBuckets));
-  CPZ_HIP(ctx->rl_offsets.ensure(sizeof(uint32_t) * cpz::kRlcWindows * (cpz::kRlcBuckets + 1)));
-  CPZ_HIP(ctx->rl_bhist.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcSortGroups * cpz::kRlcBuckets));
-  CPZ_HIP(ctx->rl_idx.ensure((size_t)rlc_istride(n) * cpz::kRlcWindows * sizeof(uint32_t)));
-  CPZ_HIP(ctx->rl_inter.ensure((size_t)rlc_istride(n) * cpz::kRlcWindows * sizeof(uint64_t)));
-  CPZ_HIP(ctx->rl_buckets.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * cpz::kRlcBuckets));
-  CPZ_HIP(ctx->rl_heads.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * (size_t)(rlc_istride(n) / cpz::kRlcChunk)));
-  const size_t nseg = (size_t)cpz::kRlcWindows * (cpz::kRlcBuckets / cpz::kRlcSegLen);
-  CPZ_HIP(ctx->rl_segs.ensure(sizeof(cpz::ge_p3) * nseg));
-  CPZ_HIP(ctx->rl_segw.ensure(sizeof(cpz::ge_p3) * nseg));
-  CPZ_HIP(ctx->rl_win.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows));
-  CPZ_HIP(ctx->rl_acc.ensure(sizeof(cpz::ge_p3)));
-  CPZ_HIP(ctx->rl_partial.ensure(64));
-  CPZ_HIP(ctx->rl_flags.ensure(4 * sizeof(int)));
-  ctx->rl_cap = n;
+  P.cap = 0;  // stays 0 unless every buffer is in place
+  CPZ_HIP(P.pts.ensure((size_t)npts * sizeof(cpz::ge_niels)));
+  CPZ_HIP(P.dig.ensure((size_t)rlc_dstride(n) * cpz::kRlcWindows * sizeof(int16_t)));
+  CPZ_HIP(P.bsum.ensure((size_t)nblk * 2 * sizeof(cpz::sc)));
+  P.cap = n;
   return CPZ_OK;
 }
 
-cpz::RlcMsmArgs rlc_msm_args(cpz_ctx* ctx, int64_t lo, int64_t hi) {
-  cpz::RlcMsmArgs m;
-  m.p0 = 4 * lo;
-  m.p1 = 4 * hi;
-  m.e0 = 4 * ctx->rl_cap;
-  m.pts = static_cast<cpz::ge_niels*>(ctx->rl_pts.p);
-  m.digits = static_cast<int16_t*>(ctx->rl_dig.p);
-  m.dstride = rlc_dstride(ctx->rl_cap);
-  m.counts = static_cast<uint32_t*>(ctx->rl_counts.p);
-  m.offsets = static_cast<uint32_t*>(ctx->rl_offsets.p);
-  m.bhist = static_cast<uint32_t*>(ctx->rl_bhist.p);
-  cpz::rlc_sort_geometry(m, (m.p1 - m.p0) + 2);
-  m.idx = static_cast<uint32_t*>(ctx->rl_idx.p);
-  m.inter = static_cast<uint64_t*>(ctx->rl_inter.p);
-  m.istride = rlc_istride(ctx->rl_cap);
-  m.buckets = static_cast<cpz::ge_p3*>(ctx->rl_buckets.p);
-  m.heads = static_cast<cpz::ge_p3*>(ctx->rl_heads.p);
-  m.hstride = (m.istride + cpz::kRlcChunk - 1) / cpz::kRlcChunk;
-  m.seg_s = static_cast<cpz::ge_p3*>(ctx->rl_segs.p);
-  m.seg_w = static_cast<cpz::ge_p3*>(ctx->rl_segw.p);
-  m.win = static_cast<cpz::ge_p3*>(ctx->rl_win.p);
-  m.acc = static_cast<cpz::ge_p3*>(ctx->rl_acc.p);
-  m.partial_out = static_cast<uint32_t*>(ctx->rl_partial.p);
-  m.identity_out = static_cast<int*>(ctx->rl_flags.p);
-  return m;
+// An MSM set for MSMs over at most `span` proofs (4 span + 2 points).
+int rlc_reserve_msm(RlcMsmSet& S, int64_t span) {
+  if (span <= S.cap) return CPZ_OK;
+  S.cap = 0;
+  const size_t inter_entry = CPZ_RLC_INTER32 ? sizeof(uint32_t) : sizeof(uint64_t);
+  CPZ_HIP(S.counts.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcBuckets));
+  CPZ_HIP(S.offsets.ensure(sizeof(uint32_t) * cpz::kRlcWindows * (cpz::kRlcBuckets + 1)));
+  CPZ_HIP(S.bhist.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcSortGroups * cpz::kRlcBuckets));
+  CPZ_HIP(S.idx.ensure((size_t)rlc_istride(span) * cpz::kRlcWindows * sizeof(uint32_t)));
+  CPZ_HIP(S.inter.ensure((size_t)rlc_istride(span) * cpz::kRlcWindows * inter_entry));
+  CPZ_HIP(S.buckets.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * cpz::kRlcBuckets));
+  CPZ_HIP(S.heads.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * (size_t)(rlc_istride(span) / cpz::kRlcChunk)));
+  const size_t nseg = (size_t)cpz::kRlcWindows * (cpz::kRlcBuckets / cpz::kRlcSegLen);
+  CPZ_HIP(S.segs.ensure(sizeof(cpz::ge_p3) * nseg));
+  CPZ_HIP(S.segw.ensure(sizeof(cpz::ge_p3) * nseg));
+  CPZ_HIP(S.win.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows));
+  CPZ_HIP(S.acc.ensure(sizeof(cpz::ge_p3)));
+  CPZ_HIP(S.total.ensure(sizeof(cpz::ge_p3)));
+  CPZ_HIP(S.partial.ensure(64));
+  CPZ_HIP(S.flags.ensure(4 * sizeof(int)));
+  S.cap = span;
+  return CPZ_OK;
 }
 
-// MSM over proofs [lo, hi) (lo a multiple of kRlcPrepBlock) of the prepared batch.
-// Synchronises; returns the partial encoding and identity flag.
+// Proofs per MSM: the points of a span (1 GiB) stay gather-friendly.
 #ifndef CPZ_RLC_SPAN
-#define CPZ_RLC_SPAN (1 << 21)  // proofs per MSM: the points of a span (1 GiB) stay gather-friendly
+#define CPZ_RLC_SPAN (1 << 21)
 #endif
 
-// P over proofs [lo, hi): one MSM per span of CPZ_RLC_SPAN proofs (aligned to the weight
-// blocks), each span's P added on the device (RlcMsmArgs::total).  Random 128-byte gathers
-// run at ~7 TB/s over a 512 MiB array but ~1.8 TB/s over 4 GiB (translation misses,
-// tools/ubench/gather_bytes.hip), so a 2^26-proof MSM over one 32 GiB points array spent
-// 2.8x the per-entry bucket time of a 2^20 one.
+// Both sets for a batch of n proofs (the MSM set for one span of it).
+int rlc_reserve(cpz_ctx* ctx, int64_t n) {
+  int rc = rlc_reserve_prepared(ctx->rl_prep, n);
+  if (rc) return rc;
+  if ((rc = rlc_reserve_msm(ctx->rl_msm, std::min<int64_t>(n, CPZ_RLC_SPAN)))) return rc;
+  CPZ_HIP(ctx->rl_flags.ensure(4 * sizeof(int)));
+  return CPZ_OK;
+}
+
+// Arguments of the MSM over proofs [lo, hi) of the prepared set P, sorted / accumulated /
+// reduced in the MSM set S.  Every stride and extra-point position comes from the set that
+// owns the buffer: the prepared points' extras (g, h) sit at 4 P.cap, the digit rows have
+// P's stride; the sorted-entry rows and bucket heads have S's strides.  (Round 2's attempt
+// at a second, span-sized MSM set for overlapping spans took all of them from the prepared
+// capacity, so a second set smaller than the batch was indexed with the batch's row stride:
+// windows 1..15 of its sorted ids and heads fell outside the set -- the identity partials
+// seen for every span that used it.  Fails with CPZ_EINVAL instead of misaddressing.)
+int rlc_msm_args(const RlcPrepared& P, RlcMsmSet& S, int64_t lo, int64_t hi, cpz::RlcMsmArgs& m) {
+  if (lo < 0 || hi < lo || hi > P.cap) return fail(CPZ_EINVAL, "MSM range outside the prepared set");
+  if (hi - lo > S.cap) return fail(CPZ_EINVAL, "MSM range larger than its MSM set");
+  m.p0 = 4 * lo;
+  m.p1 = 4 * hi;
+  m.e0 = 4 * P.cap;
+  m.pts = static_cast<cpz::ge_niels*>(P.pts.p);
+  m.digits = static_cast<int16_t*>(P.dig.p);
+  m.dstride = rlc_dstride(P.cap);
+  m.counts = static_cast<uint32_t*>(S.counts.p);
+  m.offsets = static_cast<uint32_t*>(S.offsets.p);
+  m.bhist = static_cast<uint32_t*>(S.bhist.p);
+  cpz::rlc_sort_geometry(m, (m.p1 - m.p0) + 2);
+  m.idx = static_cast<uint32_t*>(S.idx.p);
+  m.inter = static_cast<uint64_t*>(S.inter.p);
+  m.istride = rlc_istride(S.cap);
+  m.buckets = static_cast<cpz::ge_p3*>(S.buckets.p);
+  m.heads = static_cast<cpz::ge_p3*>(S.heads.p);
+  m.hstride = (m.istride + cpz::kRlcChunk - 1) / cpz::kRlcChunk;
+  m.seg_s = static_cast<cpz::ge_p3*>(S.segs.p);
+  m.seg_w = static_cast<cpz::ge_p3*>(S.segw.p);
+  m.win = static_cast<cpz::ge_p3*>(S.win.p);
+  m.acc = static_cast<cpz::ge_p3*>(S.acc.p);
+  m.partial_out = static_cast<uint32_t*>(S.partial.p);
+  m.identity_out = static_cast<int*>(S.flags.p);
+  return CPZ_OK;
+}
+
+// P over proofs [lo, hi) (lo a multiple of kRlcPrepBlock) of the prepared batch: one MSM per
+// span of CPZ_RLC_SPAN proofs (aligned to the weight blocks), each span's P added on the
+// device (RlcMsmArgs::total).  Random 128-byte gathers run at ~7 TB/s over a 512 MiB array
+// but ~1.8 TB/s over 4 GiB (translation misses, tools/ubench/gather_bytes.hip), so a
+// 2^26-proof MSM over one 32 GiB points array spent 2.8x the per-entry bucket time of a 2^20
+// one.  Synchronises; returns the partial encoding and identity flag.
 int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t partial[32], int* identity) {
   static_assert(CPZ_RLC_SPAN % cpz::kRlcPrepBlock == 0, "spans are whole weight blocks");
   static_assert(4ll * CPZ_RLC_SPAN + 2 <= cpz::kRlcMaxMsmPoints, "a span's MSM exceeds the sort-entry format");
+  RlcMsmSet& S = ctx->rl_msm;
   const int64_t nspan = (hi - lo + CPZ_RLC_SPAN - 1) / CPZ_RLC_SPAN;
-  if (nspan > 1) CPZ_HIP(ctx->rl_total.ensure(sizeof(cpz::ge_p3)));
   for (int64_t j = 0; j < nspan; j++) {
     const int64_t slo = lo + j * CPZ_RLC_SPAN, shi = std::min<int64_t>(hi, slo + CPZ_RLC_SPAN);
-    cpz::RlcMsmArgs m = rlc_msm_args(ctx, slo, shi);
+    cpz::RlcMsmArgs m;
+    if (int rc = rlc_msm_args(ctx->rl_prep, S, slo, shi, m)) return rc;
     if (nspan > 1) {
-      m.total = static_cast<cpz::ge_p3*>(ctx->rl_total.p);
+      m.total = static_cast<cpz::ge_p3*>(S.total.p);
       m.total_first = j == 0;
       m.total_last = j == nspan - 1;
     }
@@ -594,14 +663,14 @@ int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t part
         if (marks[k]) ctx->free_events.push_back(marks[k]);
     const cpz::RlcPipe* pipe;
     if (int rc = rlc_pipe(ctx, &pipe)) return rc;
-    CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_bsum.p), b0, b1,
+    CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_prep.bsum.p), b0, b1,
                                 static_cast<const cpz::ge_niels*>(ctx->tab.p), st, timed ? marks : nullptr, pipe));
     if (timed)
       for (int k = 0; k + 1 < cpz::kRlcMsmMarks; k++) ctx->marks.push_back({8 + k, marks[k], marks[k + 1]});
   }
   int flags[1];
-  CPZ_HIP(hipMemcpyAsync(partial, ctx->rl_partial.p, 32, hipMemcpyDeviceToHost, st));
-  CPZ_HIP(hipMemcpyAsync(flags, ctx->rl_flags.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipMemcpyAsync(partial, S.partial.p, 32, hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipMemcpyAsync(flags, S.flags.p, sizeof(int), hipMemcpyDeviceToHost, st));
   CPZ_HIP(hipStreamSynchronize(st));
   *identity = flags[0];
   return CPZ_OK;
@@ -648,10 +717,11 @@ int rlc_prepare_points(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, c
   pa.s = static_cast<const uint32_t*>(s);
   pa.c = static_cast<const uint32_t*>(ctx->c.p);
   pa.status = status;
-  pa.pts = static_cast<cpz::ge_niels*>(ctx->rl_pts.p);
-  pa.digits = static_cast<int16_t*>(ctx->rl_dig.p);
-  pa.dstride = rlc_dstride(ctx->rl_cap);
-  pa.block_sums = static_cast<cpz::sc*>(ctx->rl_bsum.p);
+  pa.pts = static_cast<cpz::ge_niels*>(ctx->rl_prep.pts.p);
+  pa.digits = static_cast<int16_t*>(ctx->rl_prep.dig.p);
+  pa.dstride = rlc_dstride(ctx->rl_prep.cap);
+  pa.block_sums = static_cast<cpz::sc*>(ctx->rl_prep.bsum.p);
+  pa.eq_only = ctx->eq_only ? 1 : 0;
   pa.any_bad = static_cast<int*>(ctx->rl_flags.p) + 3;
   CPZ_HIP(hipMemsetAsync(pa.any_bad, 0, sizeof(int), st));
   {
@@ -700,7 +770,8 @@ int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const voi
     va.status = status + a;  // decode-level status in, final status out
     va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
     va.scratch = nullptr;  // set per launch
-    va.pre = static_cast<const cpz::ge_niels*>(ctx->rl_pts.p) + 4 * a;
+    va.eq_only = ctx->eq_only ? 1 : 0;
+    va.pre = static_cast<const cpz::ge_niels*>(ctx->rl_prep.pts.p) + 4 * a;
     return launch_verify_chunks(ctx, va, 4, st, nullptr, true);
   };
   if (hi - lo <= kLeaf || depth > 12) return per_proof(lo, hi);
@@ -838,6 +909,7 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
       va.status = d_status;  // response statuses from batch_challenges -> final statuses
       va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
       va.scratch = nullptr;  // set per launch
+      va.eq_only = ctx->eq_only ? 1 : 0;
       {
         StageTimer span(ctx, 4, st);  // wall time of the fallback; launches timed as verify_each
         if ((rc = launch_verify_chunks(ctx, va, 1, st, nullptr, true))) return rc;
@@ -891,7 +963,11 @@ void cpz_default_generators(uint8_t g[32], uint8_t h[32]) {
   if (h) std::memcpy(h, kDefaultH, 32);
 }
 
-int cpz_ctx_create(int device_ordinal, cpz_ctx** out) {
+}  // extern "C"
+
+namespace {
+
+int ctx_create(int device_ordinal, cpz_ctx** out) {
   if (!out) return fail(CPZ_EINVAL, "out is null");
   *out = nullptr;
   int ndev = 0;
@@ -914,6 +990,36 @@ int cpz_ctx_create(int device_ordinal, cpz_ctx** out) {
   ctx->cus = prop.multiProcessorCount;
   ctx->verify_blocks_per_cu = cpz::verify_each_blocks_per_cu();  // the grid-stride verify grid fills the chip once
   *out = ctx;
+  return CPZ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cpz_ctx_create(int device_ordinal, cpz_ctx** out) {
+#if defined(CPZ_WRONG_VERDICT_FLAG)
+  // a timing-only build (timing_only.h): its verdicts are wrong by construction
+  if (out) *out = nullptr;
+  (void)device_ordinal;
+  return fail(CPZ_EINVAL, std::string("timing-only build (") + CPZ_WRONG_VERDICT_FLAG +
+                              "): verdicts are wrong by design; only cpz_ctx_create_timing_only opens a context");
+#else
+  return ctx_create(device_ordinal, out);
+#endif
+}
+
+#if defined(CPZ_WRONG_VERDICT_FLAG)
+// Timing harness entry (tools/time_verify.py): exported by timing-only builds alone.
+int cpz_ctx_create_timing_only(int device_ordinal, cpz_ctx** out) { return ctx_create(device_ordinal, out); }
+#endif
+
+int cpz_abi_version(void) { return CPZ_ABI_VERSION; }
+
+int cpz_ctx_set_commitment_checks(cpz_ctx* ctx, int enable) {
+  if (!ctx) return fail(CPZ_EINVAL, "null context");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  ctx->eq_only = enable == 0;
   return CPZ_OK;
 }
 
@@ -973,35 +1079,37 @@ int cpz_msm(cpz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalar
     if (scalars[32 * j + 31] & 0xe0) return fail(CPZ_EINVAL, "scalars must be below 2^253");
   std::lock_guard<std::mutex> lock(ctx->mu);
   CPZ_HIP(hipSetDevice(ctx->device));
-  static const uint8_t zero[32] = {0};
   uint8_t g[32], h[32];
   cpz_default_generators(g, h);
   int rc = ctx->have_gh ? CPZ_OK : ensure_generators(ctx, g, h);
   if (rc) return rc;
   if ((rc = order_after_last(ctx, ctx->stream))) return rc;
+  // n points occupy the prepared set's point / digit rows from 0 (room for ceil(n / 4)
+  // proofs), and the MSM set must hold all of them in one MSM
   const int64_t nproofs = (int64_t)(n + 3) / 4;
-  rc = rlc_reserve(ctx, nproofs);
-  if (rc) return rc;
+  if ((rc = rlc_reserve_prepared(ctx->rl_prep, nproofs))) return rc;
+  if ((rc = rlc_reserve_msm(ctx->rl_msm, nproofs))) return rc;
+  CPZ_HIP(ctx->rl_flags.ensure(4 * sizeof(int)));
   CPZ_HIP(ctx->in[0].ensure(n * 32));
   CPZ_HIP(ctx->in[1].ensure(n * 32));
   CPZ_HIP(hipMemcpyAsync(ctx->in[0].p, points, n * 32, hipMemcpyHostToDevice, ctx->stream));
   CPZ_HIP(hipMemcpyAsync(ctx->in[1].p, scalars, n * 32, hipMemcpyHostToDevice, ctx->stream));
   CPZ_HIP(hipMemsetAsync(ctx->rl_flags.p, 0, 4 * sizeof(int), ctx->stream));
-  cpz::RlcMsmArgs m = rlc_msm_args(ctx, 0, 0);
+  cpz::RlcMsmArgs m;
+  if ((rc = rlc_msm_args(ctx->rl_prep, ctx->rl_msm, 0, nproofs, m))) return rc;
   m.p0 = 0;
-  m.p1 = (int64_t)n;
+  m.p1 = (int64_t)n;  // the points themselves, not 4 per proof
   cpz::rlc_sort_geometry(m, (int64_t)n + 2);
   CPZ_HIP(cpz::launch_msm_load((int64_t)n, static_cast<const uint32_t*>(ctx->in[0].p),
                                static_cast<const uint32_t*>(ctx->in[1].p), m.pts, m.digits, m.dstride,
                                static_cast<int*>(ctx->rl_flags.p) + 2, ctx->stream));
-  (void)zero;
-  // extra points get zero scalars (empty block range)
+  // the extra points (g, h at e0) get zero scalars: empty block range
   const cpz::RlcPipe* pipe;
   if ((rc = rlc_pipe(ctx, &pipe))) return rc;
-  CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_bsum.p), 0, 0,
+  CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_prep.bsum.p), 0, 0,
                               static_cast<const cpz::ge_niels*>(ctx->tab.p), ctx->stream, nullptr, pipe));
   int flags[3];
-  CPZ_HIP(hipMemcpyAsync(out, ctx->rl_partial.p, 32, hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipMemcpyAsync(out, ctx->rl_msm.partial.p, 32, hipMemcpyDeviceToHost, ctx->stream));
   CPZ_HIP(hipMemcpyAsync(flags, ctx->rl_flags.p, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
   CPZ_HIP(hipStreamSynchronize(ctx->stream));
   if (flags[2]) return fail(CPZ_EINVAL, "a point does not decode");
@@ -1030,6 +1138,14 @@ int cpz_decode_points(cpz_ctx* ctx, size_t n, const uint8_t* points, uint8_t* ok
 
 int cpz_combine_partials(cpz_ctx* ctx, size_t k, const uint8_t* partials, uint8_t out[32], int* is_identity) {
   if (!ctx || !partials || !out || k == 0 || k > 4096) return fail(CPZ_EINVAL, "bad arguments");
+  // A shard whose fallback found it dense skipped its MSM and reports the no-partial marker
+  // (cpz_verify_batch): the batch cannot pass, and the sum is the marker too.
+  for (size_t j = 0; j < k; j++)
+    if (is_no_partial(partials + 32 * j)) {
+      std::memset(out, 0xff, 32);
+      if (is_identity) *is_identity = 0;
+      return CPZ_OK;
+    }
   std::lock_guard<std::mutex> lock(ctx->mu);
   CPZ_HIP(hipSetDevice(ctx->device));
   {
@@ -1137,15 +1253,6 @@ int cpz_verify_batch_multi(cpz_ctx* const* ctxs, int nctx, const uint8_t g[32], 
                             &ok[k], status_out ? status_out + lo : nullptr);
   });
   if (rc) return rc;
-  static const uint8_t kNoPartial[32] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
-                                         0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
-                                         0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff};
-  for (int k = 0; k < nctx; k++)
-    if (std::memcmp(partials_out + 32 * k, kNoPartial, 32) == 0) {  // a dense shard skipped its MSM
-      std::memcpy(total_out, kNoPartial, 32);
-      *batch_ok = 0;
-      return CPZ_OK;
-    }
   int ident = 0;
   rc = cpz_combine_partials(ctxs[0], (size_t)nctx, partials_out, total_out, &ident);
   if (rc) return rc;
@@ -1163,10 +1270,14 @@ int cpz_ctx_set_timing(cpz_ctx* ctx, int enable) {
 }
 
 int cpz_ctx_stage_times(cpz_ctx* ctx, double ms_out[CPZ_NUM_STAGES], int launches_out[CPZ_NUM_STAGES]) {
-  if (!ctx || !ms_out) return fail(CPZ_EINVAL, "null argument");
+  return cpz_ctx_stage_times_n(ctx, CPZ_NUM_STAGES, ms_out, launches_out);
+}
+
+int cpz_ctx_stage_times_n(cpz_ctx* ctx, int nstages, double* ms_out, int* launches_out) {
+  if (!ctx || !ms_out || nstages <= 0) return fail(CPZ_EINVAL, "null argument or no stages");
   std::lock_guard<std::mutex> lock(ctx->mu);
   CPZ_HIP(hipSetDevice(ctx->device));
-  for (int k = 0; k < CPZ_NUM_STAGES; k++) {
+  for (int k = 0; k < nstages; k++) {
     ms_out[k] = 0.0;
     if (launches_out) launches_out[k] = 0;
   }
@@ -1175,7 +1286,7 @@ int cpz_ctx_stage_times(cpz_ctx* ctx, double ms_out[CPZ_NUM_STAGES], int launche
     CPZ_HIP(hipEventSynchronize(m.b));
     float ms = 0.f;
     CPZ_HIP(hipEventElapsedTime(&ms, m.a, m.b));
-    if (m.stage >= 0 && m.stage < CPZ_NUM_STAGES) {
+    if (m.stage >= 0 && m.stage < nstages) {
       ms_out[m.stage] += ms;
       if (launches_out) launches_out[m.stage] += 1;
     }
@@ -1245,10 +1356,10 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
     if (e) (void)hipEventDestroy(e);
   if (ctx->rl_pipe.done) (void)hipEventDestroy(ctx->rl_pipe.done);
   for (DevBuf* b : {&ctx->pz_blob, &ctx->pz_off, &ctx->pz_rows, &ctx->pz_code, &ctx->pz_aux}) b->release();
-  for (DevBuf* b : {&ctx->rl_pts, &ctx->rl_dig, &ctx->rl_bsum, &ctx->rl_counts, &ctx->rl_offsets, &ctx->rl_bhist,
-                    &ctx->rl_idx, &ctx->rl_inter, &ctx->rl_buckets, &ctx->rl_heads, &ctx->rl_segs, &ctx->rl_segw, &ctx->rl_win, &ctx->rl_acc, &ctx->rl_total, &ctx->rl_partial,
-                    &ctx->rl_flags, &ctx->rl_parts})
-    b->release();
+  ctx->rl_prep.release();
+  ctx->rl_msm.release();
+  ctx->rl_flags.release();
+  ctx->rl_parts.release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -1564,7 +1675,7 @@ int verify_response_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2,
                          const void* s, const void* c, uint8_t* status, hipStream_t st) {
   CPZ_HIP(ctx->c.ensure(n * 32));
   CPZ_HIP(cpz::launch_response_prep((int64_t)n, static_cast<const uint32_t*>(s), static_cast<const uint32_t*>(c),
-                                    static_cast<uint32_t*>(ctx->c.p), status, st));
+                                    static_cast<uint32_t*>(ctx->c.p), status, ctx->eq_only ? 1 : 0, st));
   cpz::VerifyArgs va;
   va.n = (int64_t)n;
   va.y1 = static_cast<const uint32_t*>(y1);
@@ -1576,6 +1687,7 @@ int verify_response_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2,
   va.status = status;
   va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
   va.scratch = nullptr;  // set per launch
+  va.eq_only = ctx->eq_only ? 1 : 0;
   StageTimer span(ctx, 5, st);
   return launch_verify_chunks(ctx, va, 1, st, nullptr, true);
 }

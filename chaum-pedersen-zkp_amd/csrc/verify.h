@@ -10,6 +10,7 @@
 //   4. s != 0                                        -> 5  (gadgets.rs:480-482)
 //   5. g^s == r1 y1^c  and  h^s == r2 y2^c           -> 0 / 1 (batch.rs:216-228)
 #pragma once
+#include "timing_only.h"
 #include "ristretto.h"
 #include "scalar25519.h"
 #include "scalarmul.h"
@@ -39,10 +40,12 @@ CPZ_HD bool words8_zero(const uint32_t w[8]) {
   return acc == 0;
 }
 
-// Status contributed by the response scalar alone.
-CPZ_HD uint8_t response_status(const uint32_t s[8]) {
+// Status contributed by the response scalar alone.  eq_only (cpz_ctx_set_commitment_checks
+// off): a zero s is not reported -- the entry stands for a Proof built with Response::new
+// (gadgets.rs:278, no zero check), which verify_one judges by its equations alone.
+CPZ_HD uint8_t response_status(const uint32_t s[8], bool eq_only = false) {
   if (!sc_is_canonical(s)) return kStBadScalar;
-  if (sc_is_zero(s)) return kStZeroS;
+  if (sc_is_zero(s) && !eq_only) return kStZeroS;
   return kStOk;
 }
 
@@ -320,15 +323,18 @@ CPZ_EQ_LOOP
 // rows: the encodings y1, y2, r1, r2 (words at rows[4 q + ...], see DigitRef: the verify kernel
 // stages them in LDS so that no per-row address stays live in registers); pre (kPre only):
 // the entry's 4 prepared Niels points (-r1, -y1, -r2, -y2), st_s its decode-level status,
-// which must be 0.
+// which must be 0.  eq_only: an identity commitment is not reported (Commitment::new,
+// gadgets.rs:252, has no identity check; verify_one, batch.rs:185-231, checks the equations
+// only).
 template <bool kPre = false, class Comb>
 CPZ_HD uint8_t verify_proof(const DigitRef& y1, const DigitRef& y2, const DigitRef& r1, const DigitRef& r2,
                             const uint32_t s[8], const uint32_t c[8], uint8_t st_s, const Comb& comb_g,
                             const Comb& comb_h, const SlabTable& tab_v, uint32_t* dig, int dstride,
-                            const ge_niels* pre = nullptr) {
+                            const ge_niels* pre = nullptr, bool eq_only = false) {
   bool vneg;
 #if defined(CPZ_EXP_NOSPLIT)
-  // timing experiment only (wrong verdicts): the challenge split, v s and the recodings skipped
+  // timing experiment only (wrong verdicts, timing_only.h): the challenge split, v s and the
+  // recodings skipped
   vneg = c[7] & 1;
   for (int k = 0; k < 8; k++) {
     dig[k * dstride] = c[k];
@@ -367,7 +373,7 @@ CPZ_EQ_LOOP
   }
   if (!dec) return kStBadPoint;
   if (st_s == kStBadScalar) return kStBadScalar;
-  if (id) return kStIdentity;
+  if (id && !eq_only) return kStIdentity;
   if (st_s == kStZeroS) return kStZeroS;
   if (st_s == kStBadChallenge) return kStBadScalar;
   return eq ? kStOk : kStEqFail;

@@ -51,7 +51,16 @@ extern "C" {
 #define CPZ_STATUS_IDENTITY 4
 #define CPZ_STATUS_ZERO_S 5
 
+/* ABI revision of this header (cpz_abi_version): bumped whenever an entry point's signature or
+ * an array size it writes changes, so that callers built against another header can refuse
+ * to run instead of passing wrongly sized buffers.  3: CPZ_NUM_STAGES = 16,
+ * cpz_ctx_stage_times_n, cpz_ctx_set_commitment_checks. */
+#define CPZ_ABI_VERSION 3
+
 typedef struct cpz_ctx cpz_ctx;
+
+/* The CPZ_ABI_VERSION the library was built with. */
+int cpz_abi_version(void);
 
 /* Number of visible GPUs (0 when none / no HIP runtime). */
 int cpz_device_count(void);
@@ -60,6 +69,17 @@ int cpz_device_count(void);
  * reusable device buffers).  Contexts serialise concurrent calls internally. */
 int cpz_ctx_create(int device_ordinal, cpz_ctx **out);
 void cpz_ctx_destroy(cpz_ctx *ctx);
+
+/* Commitment checks (default on): statuses 4 (identity r1 / r2) and 5 (zero s) are the
+ * rejections Proof::from_bytes applies (gadgets.rs:474-482) before a proof can reach the
+ * service's batch (service.rs:501-507).  A Proof built with Proof::new(Commitment::new(..),
+ * Response::new(..)) (gadgets.rs:252, 278, 317) skips them, and the reference's verify_one
+ * (batch.rs:185-231) / verify_with_transcript (verifier/mod.rs:120-171) judge it by the two
+ * equations alone -- e.g. a nonce k = 0 gives r1 = r2 = identity and an accepted proof.
+ * enable = 0 gives exactly that: identity commitments and zero s are not reported, the
+ * equations decide (and such entries keep their RLC weight).  Applies to every later call
+ * on the context. */
+int cpz_ctx_set_commitment_checks(cpz_ctx *ctx, int enable);
 
 /* Thread-local description of the last error returned on this thread. */
 const char *cpz_last_error(void);
@@ -179,7 +199,9 @@ int cpz_decode_points(cpz_ctx *ctx, size_t n, const uint8_t *points, uint8_t *ok
 int cpz_msm(cpz_ctx *ctx, size_t n, const uint8_t *points, const uint8_t *scalars, uint8_t out[32]);
 
 /* Sum k 32-byte partials (per-GPU shards) on the device: out = encoding of the sum,
- * *is_identity = 1 iff the combined batch equation holds. */
+ * *is_identity = 1 iff the combined batch equation holds.  A partial of 32 x 0xff (a shard
+ * whose fallback skipped its MSM, cpz_verify_batch) makes out 32 x 0xff and *is_identity 0:
+ * the batch cannot pass.  CPZ_EINVAL if a partial does not decode. */
 int cpz_combine_partials(cpz_ctx *ctx, size_t k, const uint8_t *partials, uint8_t out[32], int *is_identity);
 
 /* Bulk wire-format ingestion: Proof::from_bytes (gadgets.rs:364-489) for n
@@ -251,6 +273,9 @@ int cpz_verify_batch_multi(cpz_ctx *const *ctxs, int nctx, const uint8_t g[32], 
 #define CPZ_NUM_STAGES 16
 int cpz_ctx_set_timing(cpz_ctx *ctx, int enable);
 int cpz_ctx_stage_times(cpz_ctx *ctx, double ms_out[CPZ_NUM_STAGES], int launches_out[CPZ_NUM_STAGES]);
+/* The same for the first nstages stages only (arrays of nstages entries; launches_out may be
+ * NULL): callers built against a header with another CPZ_NUM_STAGES pass their own size. */
+int cpz_ctx_stage_times_n(cpz_ctx *ctx, int nstages, double *ms_out, int *launches_out);
 
 #ifdef __cplusplus
 }

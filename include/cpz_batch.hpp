@@ -15,7 +15,11 @@
 //
 // Errors are returned, never thrown across the ABI; `Result` carries the reference's
 // error kind (src/error.rs:5-17).  Points and scalars stay as their 32-byte encodings:
-// decoding and all checks run on the GPU.
+// decoding and all checks run on the GPU.  Verifier and BatchVerifier hold Proof values,
+// which may have been built directly (Proof::new, gadgets.rs:317: no identity / zero-s
+// checks), so they verify with commitment checks off -- the equations alone decide, as
+// verify_one (batch.rs:185-231) and verify_with_transcript (verifier/mod.rs:120-171) do;
+// proof_from_bytes still applies from_bytes' checks.
 #pragma once
 
 #include <array>
@@ -122,11 +126,38 @@ class Device {
   Device& operator=(const Device&) = delete;
   bool ok() const { return rc_ == CPZ_OK && ctx_ != nullptr; }
   cpz_ctx* get() const { return ctx_; }
+  // cpz_ctx_set_commitment_checks; the mirrors below switch it off around their calls
+  int set_commitment_checks(bool on) { return cpz_ctx_set_commitment_checks(ctx_, on ? 1 : 0); }
 
  private:
   cpz_ctx* ctx_ = nullptr;
   int rc_ = CPZ_EINVAL;
 };
+
+// Commitment checks off for the lifetime of the guard (restored to the default, on).
+class EquationsOnly {
+ public:
+  explicit EquationsOnly(Device& dev) : dev_(dev) { rc_ = dev_.set_commitment_checks(false); }
+  ~EquationsOnly() { (void)dev_.set_commitment_checks(true); }
+  EquationsOnly(const EquationsOnly&) = delete;
+  EquationsOnly& operator=(const EquationsOnly&) = delete;
+  int rc() const { return rc_; }
+
+ private:
+  Device& dev_;
+  int rc_ = CPZ_OK;
+};
+
+// Statement::validate (gadgets.rs:234-238 -> ristretto.rs:173-185): y1 and y2 must be group
+// elements, i.e. their encodings must decode (on the device).
+inline Result validate_statement(Device& dev, const Statement& st) {
+  uint8_t pts[64], ok[2] = {0, 0};
+  std::memcpy(pts, st.y1.data(), 32);
+  std::memcpy(pts + 32, st.y2.data(), 32);
+  if (cpz_decode_points(dev.get(), 2, pts, ok, nullptr) != CPZ_OK) return Result::err(ErrorKind::Device, cpz_last_error());
+  if (!ok[0] || !ok[1]) return Result::err(ErrorKind::InvalidGroupElement, "Element failed recompression validation");
+  return Result::ok();
+}
 
 // Proof::from_bytes (gadgets.rs:364-489) through the device parser: the reference's checks
 // in its order (point decodes and canonical-scalar checks included), first failure wins.
@@ -151,6 +182,10 @@ class Verifier {
   // verifier/mod.rs:85-88 (fresh transcript) and :120-139 (transcript with an optional context)
   Result verify(const Proof& pr) const { return verify_with_transcript(pr, std::nullopt); }
   Result verify_with_transcript(const Proof& pr, const std::optional<std::vector<uint8_t>>& context) const {
+    Result v = validate_statement(*dev_, st_);  // verifier/mod.rs:121
+    if (v.is_err()) return v;
+    EquationsOnly eq(*dev_);
+    if (eq.rc() != CPZ_OK) return Result::err(ErrorKind::Device, cpz_last_error());
     uint8_t st = 0, present = context ? 1 : 0, pad = 0;
     const uint64_t off[2] = {0, context ? context->size() : 0};
     const uint8_t* cb = (context && !context->empty()) ? context->data() : &pad;
@@ -162,6 +197,8 @@ class Verifier {
   }
   // verifier/mod.rs:144-171: the caller's challenge (32 canonical little-endian bytes)
   Result verify_response(const Bytes32& challenge, const Proof& pr) const {
+    EquationsOnly eq(*dev_);
+    if (eq.rc() != CPZ_OK) return Result::err(ErrorKind::Device, cpz_last_error());
     uint8_t st = 0;
     const int rc = cpz_verify_response(dev_->get(), params_.g.data(), params_.h.data(), 1, st_.y1.data(),
                                        st_.y2.data(), pr.r1.data(), pr.r2.data(), pr.s.data(), challenge.data(), &st);
@@ -222,6 +259,8 @@ class BatchVerifier {
                           std::optional<std::vector<uint8_t>> context) {
     if (entries_.size() >= MAX_BATCH_SIZE)
       return Result::err(ErrorKind::InvalidParams, "Batch size limit exceeded (max 1000)");
+    Result v = validate_statement(*dev_, st);  // batch.rs:158
+    if (v.is_err()) return v;
     entries_.push_back(Entry{p, st, pr, std::move(context)});
     return Result::ok();
   }
@@ -237,6 +276,11 @@ class BatchVerifier {
       return {};
     }
     std::vector<Result> out(entries_.size());
+    EquationsOnly eq(*dev_);  // Proof values: verify_one's equations alone
+    if (eq.rc() != CPZ_OK) {
+      if (overall) *overall = Result::err(ErrorKind::Device, cpz_last_error());
+      return {};
+    }
     std::map<Parameters, std::vector<std::size_t>> groups;  // one bulk call per Parameters
     for (std::size_t i = 0; i < entries_.size(); i++) groups[entries_[i].params].push_back(i);
     for (const auto& kv : groups) {

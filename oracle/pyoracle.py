@@ -532,12 +532,15 @@ def prove(x: int, k: int, ctx: Optional[bytes] = None, g: Point = BASEPOINT,
     return ProofRecord(y1, y2, r1, r2, scalar_bytes(s), ctx)
 
 
-def decode_status(rec: ProofRecord):
+def decode_status(rec: ProofRecord, commitment_checks: bool = True):
     """Decode-time rejections, in the order the reference meets them.
 
     Statement points are decoded when the Statement is built (service.rs:82-86);
     then `Proof::from_bytes` (gadgets.rs:364-489): r1, r2 decode -> InvalidGroupElement,
     s non-canonical -> InvalidScalar, identity r1/r2 -> InvalidParams, zero s -> InvalidParams.
+    commitment_checks=False: a Proof built with Proof::new(Commitment::new, Response::new)
+    (gadgets.rs:252, 278, 317), which has no identity / zero-s checks -- verify_one judges it
+    by the equations alone (cpz_ctx_set_commitment_checks(ctx, 0)).
     Returns (status, points or None, s or None).
     """
     y1 = ristretto_decode(rec.y1)
@@ -551,16 +554,17 @@ def decode_status(rec: ProofRecord):
     s = scalar_from_canonical(rec.s)
     if s is None:
         return ST_BAD_SCALAR, None, None
-    if pt_is_identity(r1) or pt_is_identity(r2):
+    if commitment_checks and (pt_is_identity(r1) or pt_is_identity(r2)):
         return ST_IDENTITY, None, None      # gadgets.rs:474-478
-    if s == 0:
+    if commitment_checks and s == 0:
         return ST_ZERO_S, None, None        # gadgets.rs:480-482
     return ST_OK, (y1, y2, r1, r2), s
 
 
-def verify_one(rec: ProofRecord, g_bytes: bytes = G_BYTES, h_bytes: bytes = H_BYTES) -> int:
+def verify_one(rec: ProofRecord, g_bytes: bytes = G_BYTES, h_bytes: bytes = H_BYTES,
+               commitment_checks: bool = True) -> int:
     """`BatchVerifier::verify_one` (batch.rs:185-231) preceded by decode_status."""
-    st, pts, s = decode_status(rec)
+    st, pts, s = decode_status(rec, commitment_checks)
     if st != ST_OK:
         return st
     y1, y2, r1, r2 = pts
@@ -574,12 +578,13 @@ def verify_one(rec: ProofRecord, g_bytes: bytes = G_BYTES, h_bytes: bytes = H_BY
     return ST_OK if (pt_eq(lhs1, rhs1) and pt_eq(lhs2, rhs2)) else ST_EQ_FAIL
 
 
-def verify_response(rec: ProofRecord, c_bytes: bytes, g_bytes: bytes = G_BYTES, h_bytes: bytes = H_BYTES) -> int:
+def verify_response(rec: ProofRecord, c_bytes: bytes, g_bytes: bytes = G_BYTES, h_bytes: bytes = H_BYTES,
+                    commitment_checks: bool = True) -> int:
     """`Verifier::verify_response` (verifier/mod.rs:144-171) with a caller-supplied challenge,
     preceded by decode_status (the Proof / Statement were decoded before the call).  The
     challenge arrives as 32 bytes here: non-canonical bytes (scalar_from_bytes would fail,
     ristretto.rs:94-112) give ST_BAD_SCALAR, after the entry's own decode-level checks."""
-    st, pts, s = decode_status(rec)
+    st, pts, s = decode_status(rec, commitment_checks)
     if st != ST_OK:
         return st
     c = scalar_from_canonical(c_bytes)
@@ -633,7 +638,7 @@ def reference_verify(recs: Sequence[ProofRecord], alphas: Optional[Sequence[int]
 # ----------------------------------------------------------------------------
 
 def rlc_partial(recs: Sequence[ProofRecord], seed: bytes, base_index: int = 0,
-                g_bytes: bytes = G_BYTES, h_bytes: bytes = H_BYTES) -> Point:
+                g_bytes: bytes = G_BYTES, h_bytes: bytes = H_BYTES, commitment_checks: bool = True) -> Point:
     """Sum over valid-decoding entries i of
 
         [a_i s_i] G - [a_i] R1_i - [a_i c_i] Y1_i  +  [b_i s_i] H - [b_i] R2_i - [b_i c_i] Y2_i
@@ -647,7 +652,7 @@ def rlc_partial(recs: Sequence[ProofRecord], seed: bytes, base_index: int = 0,
     acc = IDENTITY
     sg = sh = 0
     for j, rec in enumerate(recs):
-        st, pts, s = decode_status(rec)
+        st, pts, s = decode_status(rec, commitment_checks)
         if st != ST_OK:
             continue
         y1, y2, r1, r2 = pts

@@ -46,6 +46,7 @@ pub const CPZ_PARSE_IDENTITY: u8 = 19;
 pub const CPZ_PARSE_ZERO_S: u8 = 20;
 
 pub const CPZ_NUM_STAGES: usize = 16;
+pub const CPZ_ABI_VERSION: c_int = 3;
 
 /// Opaque verifier context (one GPU, its stream, cached generator tables, buffers).
 #[repr(C)]
@@ -54,9 +55,11 @@ pub struct cpz_ctx {
 }
 
 extern "C" {
+    pub fn cpz_abi_version() -> c_int;
     pub fn cpz_device_count() -> c_int;
     pub fn cpz_ctx_create(device_ordinal: c_int, out: *mut *mut cpz_ctx) -> c_int;
     pub fn cpz_ctx_destroy(ctx: *mut cpz_ctx);
+    pub fn cpz_ctx_set_commitment_checks(ctx: *mut cpz_ctx, enable: c_int) -> c_int;
     pub fn cpz_last_error() -> *const c_char;
     pub fn cpz_default_generators(g: *mut u8, h: *mut u8);
     pub fn cpz_verify_each(ctx: *mut cpz_ctx, g: *const u8, h: *const u8, n: usize, y1: *const u8, y2: *const u8,
@@ -121,4 +124,6 @@ extern "C" {
                                   status_out: *mut u8) -> c_int;
     pub fn cpz_ctx_set_timing(ctx: *mut cpz_ctx, enable: c_int) -> c_int;
     pub fn cpz_ctx_stage_times(ctx: *mut cpz_ctx, ms_out: *mut f64, launches_out: *mut c_int) -> c_int;
+    pub fn cpz_ctx_stage_times_n(ctx: *mut cpz_ctx, nstages: c_int, ms_out: *mut f64, launches_out: *mut c_int)
+                                 -> c_int;
 }

@@ -166,11 +166,30 @@ pub fn device_count() -> usize {
 }
 
 impl Gpu {
+    /// A context on GPU `device`.  Refuses a library built against another `cpz.h`
+    /// (`cpz_abi_version`), so no entry point is called with wrongly sized buffers.
     pub fn new(device: usize) -> Result<Gpu, GpuError> {
+        // SAFETY: no arguments.
+        let abi = unsafe { sys::cpz_abi_version() };
+        if abi != sys::CPZ_ABI_VERSION {
+            return Err(GpuError {
+                code: sys::CPZ_EINVAL,
+                message: format!("libcpz ABI {} but these bindings follow {}", abi, sys::CPZ_ABI_VERSION),
+            });
+        }
         let mut ctx = ptr::null_mut();
         // SAFETY: out-pointer to a local.
         check(unsafe { sys::cpz_ctx_create(device as c_int, &mut ctx) })?;
         Ok(Gpu { ctx })
+    }
+
+    /// Commitment checks (`cpz_ctx_set_commitment_checks`): on (the default) reports identity
+    /// commitments and zero s as `Proof::from_bytes` would (gadgets.rs:474-482); off lets the
+    /// two equations alone decide, as `verify_one` (batch.rs:185-231) does for a `Proof`
+    /// built with `Proof::new` -- what a `BatchVerifier` holds.
+    pub fn set_commitment_checks(&self, enable: bool) -> Result<(), GpuError> {
+        // SAFETY: ctx is live; the C side locks it.
+        check(unsafe { sys::cpz_ctx_set_commitment_checks(self.ctx, enable as c_int) })
     }
 
     /// Per-entry statuses of `BatchVerifier::verify` (batch.rs:171-231) for any n.

@@ -181,6 +181,32 @@ int main() {
     Proof again;
     CHECK(pv.prove_with_transcript(k, std::nullopt, &again, nullptr).is_ok() && again.s == pr.s && again.r1 == pr.r1);
   }
+  {  // a Proof built directly with nonce k = 0 (Proof::new: r1 = r2 = identity, s = c x): the
+     // reference's verify_one accepts it; the mirrors run with commitment checks off.  The
+     // bulk ABI's default (from_bytes semantics) reports it as status 4; an undecodable
+     // statement is refused at add time (batch.rs:158).
+    Bytes32 x{}, k{};
+    for (int i = 0; i < 31; i++) x[i] = (uint8_t)(11 * i + 5);
+    Prover pv(dev, params, x);
+    Proof pr;
+    Statement st;
+    CHECK(pv.prove_with_transcript(k, std::nullopt, &pr, &st).is_ok());
+    Bytes32 zero{};
+    CHECK(pr.r1 == zero && pr.r2 == zero);
+    BatchVerifier b(dev);
+    CHECK(b.add(params, st, pr).is_ok());
+    CHECK(b.add(params, base.st[2], base.pr[2]).is_ok());
+    auto r = b.verify();
+    CHECK(r.size() == 2 && r[0].is_ok() && r[1].is_ok());
+    CHECK(Verifier(dev, params, st).verify(pr).is_ok());
+    uint8_t s4 = 0;
+    CHECK(cpz_verify_each(dev.get(), params.g.data(), params.h.data(), 1, st.y1.data(), st.y2.data(), pr.r1.data(),
+                          pr.r2.data(), pr.s.data(), nullptr, nullptr, nullptr, &s4) == CPZ_OK && s4 == CPZ_STATUS_IDENTITY);
+    Statement bad = st;
+    bad.y1.fill(0xff);
+    Result ra = b.add(params, bad, pr);
+    CHECK(ra.is_err() && ra.kind == ErrorKind::InvalidGroupElement && b.len() == 2);
+  }
   if (failures) {
     std::fprintf(stderr, "%d failures\n", failures);
     return 1;

@@ -41,8 +41,37 @@ def test_parameters_validation():
     assert cp.Parameters.with_generators(g, h) == cp.Parameters()
 
 
+class _DecodeStub:
+    """Stands in for the device's bulk decode at add time (statement.validate, batch.rs:158):
+    bookkeeping only -- nothing here verifies anything."""
+
+    def __init__(self, ok=True):
+        self.ok, self.calls = ok, 0
+
+    def decode_points(self, pts):
+        import numpy as np
+        self.calls += 1
+        return np.full(len(pts), 1 if self.ok else 0, np.uint8), None
+
+
+def test_add_validates_the_statement():
+    """batch.rs:158: add_with_context runs statement.validate(); an undecodable statement is
+    refused at add time (InvalidGroupElement), before anything is queued; without a device
+    the validation fails loudly."""
+    b = cp.BatchVerifier(_DecodeStub(ok=False))
+    with pytest.raises(cp.InvalidGroupElement):
+        b.add(cp.Parameters(), cp.Statement(R1, R2), cp.Proof(R1, R2, S))
+    assert b.is_empty()
+    import chaum_pedersen._native as nat
+    if nat.load().cpz_device_count() == 0:
+        with pytest.raises(cp.CpzError):
+            cp.BatchVerifier().add(cp.Parameters(), cp.Statement(bytes(31) + b"\x05", R2), cp.Proof(R1, R2, S))
+    assert cp.BatchVerifier.with_capacity(10).capacity == 10
+    assert cp.BatchVerifier.with_capacity(10 ** 6).capacity == cp.MAX_BATCH_SIZE   # batch.rs:113-118
+
+
 def test_batch_bookkeeping_without_device():
-    b = cp.BatchVerifier.new()
+    b = cp.BatchVerifier(_DecodeStub())
     assert b.len() == 0 and b.is_empty() and b.remaining_capacity() == cp.MAX_BATCH_SIZE == 1000
     with pytest.raises(cp.InvalidParams):
         b.verify()                                  # empty batch (batch.rs:172-176)

@@ -141,7 +141,7 @@ def test_decode_points_rfc9496(gpu, golden):
 
 def test_register_handler_checks(gpu):
     """service.rs:61-97: sizes, element_from_bytes of y1 / y2, identity statements refused."""
-    from chaum_pedersen.service import InvalidArgument, MemoryState, register
+    from chaum_pedersen.service import AlreadyExists, InvalidArgument, MemoryState, register
     st = MemoryState()
     rec = O.prove(O.bench_scalar(b"x", 1), 3)
     register(st, "alice", rec.y1, rec.y2, gpu)
@@ -152,13 +152,17 @@ def test_register_handler_checks(gpu):
              ("bob", rec.y1, bytes.fromhex("01" + "00" * 31),
               "Invalid y2: Invalid group element: Bytes do not represent a valid Ristretto point"),
              ("bob", bytes(32), rec.y2, "Statement contains identity elements"),
-             ("bad id!", rec.y1, rec.y2, "User ID contains invalid characters"),
-             ("alice", rec.y1, rec.y2, "Registration failed: Invalid group parameters: User 'alice' already registered")]
+             ("bad id!", rec.y1, rec.y2, "User ID contains invalid characters")]
     for uid, y1, y2, msg in cases:
         with pytest.raises(InvalidArgument) as e:
             register(st, uid, y1, y2, gpu)
         assert str(e.value) == msg
     assert st.get_user("bob") is None
+    # a taken id is Status::already_exists, not invalid_argument (service.rs:108-112)
+    with pytest.raises(AlreadyExists) as e:
+        register(st, "alice", rec.y1, rec.y2, gpu)
+    assert str(e.value) == "Registration failed: Invalid group parameters: User 'alice' already registered"
+    assert e.value.code == "ALREADY_EXISTS"
 
 
 def test_calls_ordered_across_streams(gpu, golden):
@@ -207,3 +211,81 @@ def test_security_tests_mirror(gpu):
             cp.Proof.from_bytes(blob, gpu)
     p = cp.Proof(out["r1"][0].tobytes(), out["r2"][0].tobytes(), out["s"][0].tobytes())
     assert 32 < len(p.to_bytes()) < 1024 and cp.Proof.from_bytes(p.to_bytes(), gpu).to_bytes() == p.to_bytes()
+
+
+def _cons_rows(recs):
+    return [np.frombuffer(b"".join(getattr(r, k) for r in recs), np.uint8).reshape(-1, 32)
+            for k in ("y1", "y2", "r1", "r2", "s")]
+
+
+def test_commitment_checks_off_equals_verify_one_on_constructed_proofs(gpu):
+    """Proofs built with Proof::new(Commitment::new(..), Response::new(..)) (gadgets.rs:252, 278,
+    317) skip from_bytes' identity / zero-s checks, and the reference's verify_one
+    (batch.rs:185-231) judges them by the equations alone.  With commitment checks off
+    (cpz_ctx_set_commitment_checks) the GPU does the same -- per proof, through the RLC
+    batch check and its fallback, with caller challenges, and through the mirrors:
+      nonce k = 0            -> r1 = r2 = identity, s = c x: valid (default mode: status 4)
+      x = 0, k = 0           -> identity statement and commitment, s = 0: valid (default: 4)
+      valid proof with s = 0 -> equation failure (default: 5)."""
+    x = O.bench_scalar(b"x", 4242)
+    k0 = O.prove(x, 0)
+    assert k0.r1 == bytes(32) and k0.r2 == bytes(32)
+    zz = O.prove(0, 0)
+    assert zz.s == bytes(32) and zz.y1 == bytes(32)
+    s0 = O.prove(x, 99)
+    s0.s = bytes(32)
+    ok = O.prove(x, 7)
+    recs = [ok, k0, zz, s0]
+    rows = _cons_rows(recs)
+    default = [O.verify_one(r) for r in recs]
+    eq_only = [O.verify_one(r, commitment_checks=False) for r in recs]
+    assert default == [0, 4, 4, 5] and eq_only == [0, 0, 0, 1]
+    assert list(gpu.verify_each(*rows)) == default
+    with gpu.commitment_checks(False):
+        assert list(gpu.verify_each(*rows)) == eq_only
+        _, bok, st = gpu.verify_batch(*rows, seed=bytes(range(32)))
+        assert not bok and list(st) == eq_only
+        # the RLC weights the identity-commitment entries (they are valid): the partial is the
+        # oracle's with the same checks off, i.e. the s = 0 entry's alone
+        part, _, _ = gpu.verify_batch(*rows, seed=bytes(range(32)), statuses=False)
+        want = O.rlc_partial(recs, bytes(range(32)), commitment_checks=False)
+        assert part == O.ristretto_encode(want)
+        assert part == O.ristretto_encode(O.rlc_partial([s0], bytes(range(32)), base_index=3,
+                                                        commitment_checks=False))
+        _, bok, st = gpu.verify_batch(*[r[:3] for r in rows], seed=bytes(range(32)))
+        assert bok and not st.any()
+        c = gpu.challenges(*rows[:4])
+        assert list(gpu.verify_response(*rows, c)) == eq_only
+    # back to the default mode
+    assert list(gpu.verify_each(*rows)) == default
+    _, bok, st = gpu.verify_batch(*rows, seed=bytes(range(32)))
+    assert not bok and list(st) == default
+    # the mirrors hold Proof values (Proof::new): equations only, as the reference
+    b = cp.BatchVerifier(gpu)
+    params = cp.Parameters()
+    for r in recs:
+        b.add(params, cp.Statement(r.y1, r.y2), cp.Proof(r.r1, r.r2, r.s))
+    res = b.verify()
+    assert [v.status for v in res] == eq_only
+    cp.Verifier(params, cp.Statement(k0.y1, k0.y2), gpu).verify(cp.Proof(k0.r1, k0.r2, k0.s))
+    cp.Verifier(params, cp.Statement(zz.y1, zz.y2), gpu).verify(cp.Proof(zz.r1, zz.r2, zz.s))
+    with pytest.raises(cp.InvalidParams):
+        cp.Verifier(params, cp.Statement(s0.y1, s0.y2), gpu).verify(cp.Proof(s0.r1, s0.r2, s0.s))
+    # but Proof.from_bytes (the wire) still rejects them, with the reference's messages
+    with pytest.raises(cp.InvalidParams, match="Commitment contains identity element"):
+        cp.Proof.from_bytes(cp.Proof(k0.r1, k0.r2, k0.s).to_bytes(), gpu)
+    with pytest.raises(cp.InvalidParams, match="Response scalar is zero"):
+        cp.Proof.from_bytes(cp.Proof(s0.r1, s0.r2, s0.s).to_bytes(), gpu)
+
+
+def test_add_time_statement_validation_and_capacity(gpu, golden):
+    """batch.rs:158 (statement.validate() in add_with_context) and batch.rs:113-118."""
+    b = cp.BatchVerifier.with_capacity(5000, gpu)
+    assert b.capacity == cp.MAX_BATCH_SIZE
+    rec = O.prove(O.bench_scalar(b"x", 1), 3)
+    bad = bytes.fromhex(golden["rfc9496_bad"][0])
+    with pytest.raises(cp.InvalidGroupElement):
+        b.add(cp.Parameters(), cp.Statement(bad, rec.y2), cp.Proof(rec.r1, rec.r2, rec.s))
+    assert b.is_empty()
+    b.add(cp.Parameters(), cp.Statement(rec.y1, rec.y2), cp.Proof(rec.r1, rec.r2, rec.s))
+    assert b.len() == 1 and b.verify()[0].is_ok()

@@ -85,3 +85,86 @@ def test_two_ranks_hip_partials_gather_and_combine(gpu):
     assert total0 == total1 == whole and not id0 and not id1
     assert not ok0 and not ok1                           # each shard holds a forgery
     assert sorted(bad0 + bad1) == FORGED
+
+
+def _dense_worker(rank, world, port, q):
+    """Rank 0's shard is 2^21 proofs with 1 % forged (its fallback's density probe skips the
+    MSM and reports the no-partial marker 32 x 0xff); rank 1's shard is clean."""
+    sys.path.insert(0, os.path.join(ROOT, "chaum-pedersen-zkp_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import hashlib
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import chaum_pedersen as cp
+    from chaum_pedersen.shard import all_gather_partials, shard_range
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        gpu = cp.Gpu(0)
+        n = 1 << 22
+        lo, hi = shard_range(n, world, rank)
+        d = {k: torch.empty((hi - lo, 32), dtype=torch.uint8, device="cuda:0") for k in ("y1", "y2", "r1", "r2", "s")}
+        gpu.prove_synthetic_device(hi - lo, hashlib.sha256(b"dense-x").digest(), hashlib.sha256(b"dense-k").digest(),
+                                   d["y1"], d["y2"], d["r1"], d["r2"], d["s"], first_index=lo)
+        forged = []
+        if rank == 0:
+            forged = np.sort(np.random.default_rng(5).choice(hi - lo, (hi - lo) // 100, replace=False))
+            dst = torch.from_numpy(forged.astype(np.int64)).cuda()
+            src = torch.from_numpy(((forged + 7) % (hi - lo)).astype(np.int64)).cuda()
+            d["y1"].index_copy_(0, dst, d["y1"].index_select(0, src).clone())
+        st = torch.empty(hi - lo, dtype=torch.uint8, device="cuda:0")
+        partial, ok = gpu.verify_batch_device(d["y1"], d["y2"], d["r1"], d["r2"], d["s"], st, bytes(range(32)),
+                                              first_index=lo, fallback=True)
+        parts = all_gather_partials(partial)
+        total, ident = gpu.combine_partials(parts)
+        bad = torch.nonzero(st).flatten().cpu().numpy()
+        q.put((rank, parts, total, ident, ok, bool(np.array_equal(bad, np.asarray(forged, dtype=bad.dtype)))))
+        gpu.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_dense_shard_marker_combines(gpu):
+    """A dense shard's no-partial marker through the torch.distributed flow
+    (all_gather_partials -> combine_partials): the combine reports the marker and "not
+    identity" instead of failing on an undecodable partial, on every rank; each rank's
+    statuses are exact."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dense_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    (_, parts0, total0, id0, ok0, exact0), (_, parts1, total1, id1, ok1, exact1) = res
+    marker = b"\xff" * 32
+    assert parts0 == parts1 and parts0[0] == marker and parts0[1] == bytes(32)
+    assert total0 == total1 == marker and not id0 and not id1
+    assert not ok0 and ok1 and exact0 and exact1
+
+
+def test_bench_rlc_four_rank_rehearsal():
+    """bench.py's multi-rank RLC path (configs[3]'s flow: per-rank shard partials keyed by the
+    global index, all-gather, combine) as a world-4 gloo rehearsal on the box's one GPU: the
+    combined total of a valid set is the identity, and the line reports no rate."""
+    import json
+    import subprocess
+    port = _free_port()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "4", "--mode", "rlc", "--n-total", str(1 << 20), "--same-device", "--backend", "gloo",
+           "--steps", "1", "--warmup", "1", "--extras", "0", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=360, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["value"] is None and d["ms_per_step"] is None and d["n_gpus"] == 4
+    assert d["rehearsal"]["combined_total_identity"] is True
+    assert d["rehearsal"]["combined_total"] == "00" * 32

@@ -244,3 +244,55 @@ def test_multi_context_shards(gpu):
     finally:
         for g in gpus:
             g.close()
+
+
+def test_multi_context_c4_shape_eight_contexts(gpu):
+    """The single-process multi-GPU entry points at configs[3]'s shape: 8 contexts (here on the
+    one GPU of the box; a node gives each its own device) over 2^24 proofs with 0.1 % forged.
+    Every per-shard partial (weights keyed by the global index) and the combined total equal
+    the C oracle's partial of that shard's / the batch's forged entries alone; both the
+    per-proof and the batch-check entry points return exactly the forged set.  Each shard is
+    dense enough that its fallback verifies it per proof: its partial is then the no-partial
+    marker and the total is the marker too (cpz_combine_partials)."""
+    import chaum_pedersen as cp
+    import coracle as C
+    n, nf, k = 1 << 24, 16_777, 8
+    seed = hashlib.sha256(b"cpz-weights-v1").digest()
+    syn = gpu.prove_synthetic(n, hashlib.sha256(b"c4-x").digest(), hashlib.sha256(b"c4-k").digest())
+    rows = [np.ascontiguousarray(syn[q]) for q in ("y1", "y2", "r1", "r2", "s")]
+    del syn
+    idx = np.sort(np.random.default_rng(88).choice(n, size=nf, replace=False))
+    for j, i in enumerate(idx):
+        if j % 2:
+            rows[0][i] = rows[0][(i + 7) % n]
+        else:
+            v = (int.from_bytes(rows[4][i].tobytes(), "little") + 1) % O.L
+            rows[4][i] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)
+    gpus = [cp.Gpu(0) for _ in range(k)]
+    try:
+        st = cp.verify_each_multi(gpus, *rows)
+        assert np.array_equal(np.nonzero(st)[0], idx) and set(st[idx].tolist()) == {1}
+        parts, total, ok, st_b = cp.verify_batch_multi(gpus, *rows, seed=seed)
+        assert not ok and np.array_equal(st_b, st)
+        # partials proper: the same shards without the fallback (statuses=False)
+        per = n // k
+        host = {q: rows[j][idx] for j, q in enumerate(("y1", "y2", "r1", "r2", "s"))}
+        want_parts = []
+        for s in range(k):
+            lo, hi = s * per, (s + 1) * per
+            p, okp, _ = gpus[s].verify_batch(*(r[lo:hi] for r in rows), seed=seed, first_index=lo, statuses=False)
+            m = (idx >= lo) & (idx < hi)
+            want, live = C.rlc_partial({q: host[q][m] for q in host}, idx[m], seed, threads=16)
+            assert live == int(m.sum()) and p == want and not okp, s
+            want_parts.append(p)
+        tot, ident = gpu.combine_partials(want_parts)
+        want, _ = C.rlc_partial(host, idx, seed, threads=16)
+        assert not ident and tot == want
+        # with the fallback, a shard whose density probe sees >= 2 of its ~2 K forgeries skips
+        # its MSM (marker); any other shard reports its partial -- and the total follows
+        marker = b"\xff" * 32
+        assert all(p in (marker, w) for p, w in zip(parts, want_parts)), parts
+        assert total == (marker if marker in parts else want)
+    finally:
+        for g in gpus:
+            g.close()

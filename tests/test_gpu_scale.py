@@ -215,3 +215,32 @@ def test_fallback_probe_sparse_and_dense(gpu):
     # without a fallback the partial is always computed
     p, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED)
     assert not ok and p != b"\xff" * 32 and p != bytes(32)
+
+
+def test_spans_forged_only_in_a_later_span(gpu):
+    """A 2^23-proof batch is checked as four MSMs of 2^21-proof spans (rlc_range), each
+    span's P added on the device.  Forgeries ONLY in span 2: the batch partial must be the
+    oracle's partial of those entries (an identity partial here would accept a forged batch),
+    the batch must fail, and the fallback must return exactly the forged set.  Also checked
+    for the same span as a batch of its own (first_index = its global start) and for spans
+    0..1 alone (valid: identity, batch ok)."""
+    torch = pytest.importorskip("torch")
+    n, span = 1 << 23, 1 << 21
+    t = _synthetic_device(gpu, torch, n)
+    rng = np.random.default_rng(232)
+    idx = np.sort(rng.choice(np.arange(2 * span, 3 * span), 40, replace=False))
+    host = _forge(t, torch, idx)
+    want = _oracle_partial(host, idx)
+    assert want != bytes(32)
+    st = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    p, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED)
+    assert not ok and p == want
+    p, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED, fallback=True)
+    assert not ok and p == want
+    got = st.cpu().numpy()
+    assert np.array_equal(np.nonzero(got)[0], idx) and set(got[idx].tolist()) == {1}
+    lo, hi = 2 * span, 3 * span
+    p, ok = gpu.verify_batch_device(*(t[k][lo:hi] for k in KEYS), st[lo:hi], WSEED, first_index=lo)
+    assert not ok and p == want
+    p, ok = gpu.verify_batch_device(*(t[k][:lo] for k in KEYS), st[:lo], WSEED)
+    assert ok and p == bytes(32)

@@ -93,7 +93,7 @@ def test_build_script_compiles_the_library_units():
 
 
 def test_reference_patch_is_safe_code():
-    for rel in ("rust/reference-patch/batch_gpu.rs",):
+    for rel in ("rust/reference-patch/gpu.rs", "rust/reference-patch/dispatch.rs"):
         src = open(os.path.join(ROOT, rel)).read()
         code = "\n".join(l.split("//")[0] for l in src.splitlines())
         assert "unsafe" not in code, rel
@@ -104,3 +104,55 @@ def test_reference_patch_is_safe_code():
         if "unsafe {" in l and "impl" not in l:
             ctx = "\n".join(lines[max(0, i - 3):i + 1])
             assert "SAFETY" in ctx, (i, l)
+
+
+REF_BATCH = "/root/reference/src/verifier/batch.rs"
+VERIFY_SIG = "pub fn verify<R: CryptoRngCore>(&self, rng: &mut R) -> Result<Vec<Result<()>>>"
+
+
+def _code(rel):
+    src = open(os.path.join(ROOT, rel)).read()
+    return "\n".join(l.split("//")[0] for l in src.splitlines())
+
+
+def test_patch_serves_verify_with_the_reference_signature():
+    """The drop-in is `verify` itself (batch.rs:171), not a new method: callers need no edit.
+    Its signature is the reference's (read from the reference when it is present), and it
+    dispatches to the GPU under the feature and to the renamed CPU body otherwise."""
+    d = _code("rust/reference-patch/dispatch.rs")
+    assert " ".join(d.split()).count(VERIFY_SIG) == 1
+    if os.path.exists(REF_BATCH):
+        ref = " ".join(open(REF_BATCH).read().split())
+        assert VERIFY_SIG in ref
+    assert '#[cfg(feature = "gpu")]' in d and "super::gpu::verify(self, rng)" in d
+    assert '#[cfg(not(feature = "gpu"))]' in d and "self.verify_cpu(rng)" in d
+    g = _code("rust/reference-patch/gpu.rs")
+    assert "verify_gpu" not in g and "verify_gpu" not in d
+
+
+def test_patch_draws_the_seed_from_rng_and_uses_the_batch_check():
+    g = _code("rust/reference-patch/gpu.rs")
+    assert "rng.fill_bytes(&mut s)" in g                  # weights keyed by rng (batch.rs:240)
+    assert "gpu.verify_batch(" in g and "gpu.verify_each(" in g
+    assert "entries.len() == 1" in g                     # n == 1 -> verify_one, rng untouched
+    assert "set_commitment_checks(false)" in g           # Proof::new entries: equations only
+
+
+def test_patch_compresses_generators_once_per_group():
+    """g and h are compressed in compress_generators only, which runs when a new Parameters
+    group is created -- never inside the per-entry row building."""
+    g = _code("rust/reference-patch/gpu.rs")
+    lines = g.splitlines()
+    start = next(i for i, l in enumerate(lines) if l.startswith("fn compress_generators"))
+    end = next(i for i in range(start, len(lines)) if lines[i].startswith("}"))
+    for i, l in enumerate(lines):
+        if "generator_g()" in l or "generator_h()" in l:
+            inside = start <= i <= end
+            grouping = "e.params.generator_g(), e.params.generator_h()" in l   # Element refs, no compression
+            assert inside or grouping, (i, l)
+            assert "element_to_bytes" not in l or inside, (i, l)
+    calls = [l for l in lines if "compress_generators(" in l and not l.startswith("fn ")]
+    assert len(calls) == 1 and "None =>" in calls[0]
+    rows = lines[next(i for i, l in enumerate(lines) if l.startswith("fn entry_rows")):]
+    rows = rows[:next(i for i, l in enumerate(rows) if l.startswith("}"))]
+    assert not any("generator" in l for l in rows)

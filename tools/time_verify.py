@@ -14,7 +14,8 @@ def main():
     import chaum_pedersen as cp
     n, steps = 1 << 20, int(os.environ.get("STEPS", "10"))
     dev = torch.device("cuda", 0)
-    gpu = cp.Gpu(0)
+    # a timing-only build (csrc/timing_only.h) opens its context through the timing entry
+    gpu = cp.Gpu(0, timing_only=hasattr(cp._native.load(), "cpz_ctx_create_timing_only"))
     t = {k: torch.empty((n, 32), dtype=torch.uint8, device=dev) for k in ("y1", "y2", "r1", "r2", "s")}
     status = torch.empty(n, dtype=torch.uint8, device=dev)
     gpu.prove_synthetic_device(n, bytes(32), bytes(range(32)), t["y1"], t["y2"], t["r1"], t["r2"], t["s"])

@@ -7,8 +7,14 @@
 // Each wave runs 16 independent accumulation chains of one instruction; lane 0 stamps
 // s_memtime / s_memrealtime around the loop and writes them to a buffer of its own (never
 // an output).  W blocks of 256 threads per CU = W waves per SIMD.
-//   cycles/instr (per SIMD) = median over waves of dt / (iters * 16) / W
-//   clock (GHz)             = median of dt / dreal * 0.1
+//   clock (GHz)             = median over waves of dt / dreal * 0.1
+//   cycles/instr (per SIMD) = SIMD cycles of the launch / wave instructions per SIMD
+//                           = (event ms * clock) / (W * iters * 16)
+// The launch's SIMD cycles come from the event time and the measured clock, so the figure
+// holds whether or not all W waves of a SIMD were resident at once.  (Round 2 divided each
+// wave's own stamp span by W, which assumes they were: at 4 and 8 waves/SIMD it reported
+// 3.96 and 2.90 cycles while the launch's throughput implied ~4.5.)  The per-wave form is
+// kept as wave_stamp_cycles for comparison.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -78,7 +84,7 @@ __global__ void __launch_bounds__(256) kclock(int iters, uint64_t* sink, uint64_
 
 template <int OP>
 static int run(int cus, int waves_per_simd, int iters, uint64_t* sink, uint64_t* stamps, hipEvent_t e0, hipEvent_t e1,
-               double* cyc, double* ghz, double* gops) {
+               double* cyc, double* wave_cyc, double* ghz, double* gops) {
   const int grid = cus * waves_per_simd;
   hipLaunchKernelGGL(kclock<OP>, dim3(grid), dim3(256), 0, 0, iters / 4, sink, stamps, 1u);  // warm
   CHECK(hipDeviceSynchronize());
@@ -98,8 +104,9 @@ static int run(int cus, int waves_per_simd, int iters, uint64_t* sink, uint64_t*
   }
   std::nth_element(c.begin(), c.begin() + nw / 2, c.end());
   std::nth_element(f.begin(), f.begin() + nw / 2, f.end());
-  *cyc = c[nw / 2];
+  *wave_cyc = c[nw / 2];
   *ghz = f[nw / 2];
+  *cyc = (double)ms * 1e-3 * (*ghz * 1e9) / ((double)waves_per_simd * iters * kChains);
   *gops = (double)grid * 256.0 * iters * kChains / (ms * 1e-3) / 1e9;
   return 0;
 }
@@ -120,20 +127,20 @@ int main() {
   bool first = true;
   for (int op = 0; op < NOPS; op++) {
     for (int w : {1, 2, 4, 8}) {
-      double cyc = 0, ghz = 0, gops = 0;
+      double cyc = 0, wcyc = 0, ghz = 0, gops = 0;
       int rc = 0;
       switch (op) {
-        case MAD_I64_I32: rc = run<MAD_I64_I32>(cus, w, iters, sink, stamps, e0, e1, &cyc, &ghz, &gops); break;
-        case ADD_U32: rc = run<ADD_U32>(cus, w, iters, sink, stamps, e0, e1, &cyc, &ghz, &gops); break;
-        case AND_B32: rc = run<AND_B32>(cus, w, iters, sink, stamps, e0, e1, &cyc, &ghz, &gops); break;
-        case MUL_LO_U32: rc = run<MUL_LO_U32>(cus, w, iters, sink, stamps, e0, e1, &cyc, &ghz, &gops); break;
-        case LSHL_ADD_U64: rc = run<LSHL_ADD_U64>(cus, w, iters, sink, stamps, e0, e1, &cyc, &ghz, &gops); break;
-        case ASHR_I64: rc = run<ASHR_I64>(cus, w, iters, sink, stamps, e0, e1, &cyc, &ghz, &gops); break;
+        case MAD_I64_I32: rc = run<MAD_I64_I32>(cus, w, iters, sink, stamps, e0, e1, &cyc, &wcyc, &ghz, &gops); break;
+        case ADD_U32: rc = run<ADD_U32>(cus, w, iters, sink, stamps, e0, e1, &cyc, &wcyc, &ghz, &gops); break;
+        case AND_B32: rc = run<AND_B32>(cus, w, iters, sink, stamps, e0, e1, &cyc, &wcyc, &ghz, &gops); break;
+        case MUL_LO_U32: rc = run<MUL_LO_U32>(cus, w, iters, sink, stamps, e0, e1, &cyc, &wcyc, &ghz, &gops); break;
+        case LSHL_ADD_U64: rc = run<LSHL_ADD_U64>(cus, w, iters, sink, stamps, e0, e1, &cyc, &wcyc, &ghz, &gops); break;
+        case ASHR_I64: rc = run<ASHR_I64>(cus, w, iters, sink, stamps, e0, e1, &cyc, &wcyc, &ghz, &gops); break;
       }
       if (rc) return rc;
-      printf("%s {\"op\": \"%s\", \"waves_per_simd\": %d, \"cycles_per_instr\": %.3f, \"clock_ghz\": %.3f, "
-             "\"gops\": %.1f, \"gops_at_2p4ghz\": %.1f}\n",
-             first ? " " : ",", kNames[op], w, cyc, ghz, gops, 4.0 * cus * 64.0 / cyc * 2.4);
+      printf("%s {\"op\": \"%s\", \"waves_per_simd\": %d, \"cycles_per_instr\": %.3f, \"wave_stamp_cycles\": %.3f, "
+             "\"clock_ghz\": %.3f, \"lanes_per_simd_cycle\": %.3f, \"gops\": %.1f, \"gops_at_2p4ghz\": %.1f}\n",
+             first ? " " : ",", kNames[op], w, cyc, wcyc, ghz, 64.0 / cyc, gops, 4.0 * cus * 64.0 / cyc * 2.4);
       first = false;
     }
   }
