@@ -297,6 +297,7 @@ def main():
         torch.cuda.synchronize(dev)
         c_el = time.perf_counter() - c0
         c_st = gpu.stage_times()
+        c_fb = gpu.fallback_stats()
         got = st5.cpu().numpy()
         exact = (not ok) and np.array_equal(np.nonzero(got)[0], idx) and set(got[idx].tolist()) == {1}
         if not exact:
@@ -313,14 +314,18 @@ def main():
             raise SystemExit("bench: C5 per-proof statuses differ from the fallback's")
         ms = {k: v[0] for k, v in c_st.items()}
         c5 = {"workload": "configs[4]: %d proofs, %d forged (half s+1, half wrong y1), RLC batch check + fallback "
-                          "(density probe beside the challenges; a dense batch is verified per proof, nothing prepared) -> exact invalid set" % (n5, nf),
+                          "(density probe beside the challenges; at this density the partitioned check: every "
+                          "256-proof block's RLC partial, per-proof verification of the failing blocks only) -> "
+                          "exact invalid set" % (n5, nf),
               "proofs": n5, "forged": nf, "ms": c_el * 1e3, "proofs_per_s": n5 / c_el, "exact_set": True,
               "phase_ms": {"challenge": ms.get("challenge", 0.0), "rlc_prepare": ms.get("rlc_prepare", 0.0),
                            "rlc_msm": ms.get("rlc_msm", 0.0), "fallback_per_proof": ms.get("fallback", 0.0)},
+              "fallback": c_fb,
               "per_proof_only_ms": p_el * 1e3,
-              "note": "per_proof_only_ms: cpz_verify_each of the same batch (same statuses); at this density "
-                      "the probe (4096 sampled proofs, run beside the challenges) finds the batch cannot pass, so "
-                      "nothing is prepared and no MSM runs"}
+              "ratio_to_per_proof": c_el / p_el,
+              "partial": partial.hex(),
+              "note": "per_proof_only_ms: cpz_verify_each of the same batch (same statuses); rlc_msm is the "
+                      "partitioned MSM (k_part_*), fallback_per_proof the per-proof pass over the failing blocks"}
         del t5, st5
         torch.cuda.empty_cache()
 

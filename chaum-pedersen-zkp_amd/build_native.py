@@ -55,7 +55,7 @@ def _run(cmd):
 def build_libcpz(force: bool = False, verbose: bool = False, out: str = LIBCPZ, defines=()) -> str:
     """Build the product library.  `out` / `defines` build a tuning variant (e.g.
     CPZ_VERIFY_WAVES=3) elsewhere, for side-by-side measurement with CPZ_LIB=<out>."""
-    units = ["kernels.hip", "rlc.hip", "runtime.hip"]
+    units = ["kernels.hip", "rlc.hip", "part.hip", "runtime.hip"]
     srcs = [os.path.join(CSRC, u) for u in units] + _headers()
     if not force and not defines and not _newer(out, srcs):
         return out

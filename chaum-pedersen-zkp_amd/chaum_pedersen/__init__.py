@@ -338,6 +338,14 @@ class Gpu:
         _native.check(self._lib.cpz_ctx_stage_times_n(self._h, _native.NUM_STAGES, ms, cnt))
         return {self.STAGES[k]: (ms[k], cnt[k]) for k in range(_native.NUM_STAGES) if cnt[k]}
 
+    def fallback_stats(self) -> dict:
+        """What the last verify_batch call's fallback did (cpz_ctx_fallback_stats)."""
+        out = (ctypes.c_uint64 * _native.FALLBACK_STATS)()
+        _native.check(self._lib.cpz_ctx_fallback_stats(self._h, out))
+        return {"path": _native.FALLBACK_PATHS.get(int(out[0]), str(out[0])), "probe_invalid": int(out[1]),
+                "blocks_checked": int(out[2]), "blocks_failing": int(out[3]), "per_proof": int(out[4]),
+                "bisection_msms": int(out[5])}
+
     # -- commitment checks (cpz_ctx_set_commitment_checks) ------------------------------------
     def set_commitment_checks(self, enable: bool) -> None:
         """On (default): statuses 4 / 5 for identity commitments and zero s, the rejections of

@@ -33,9 +33,11 @@ EXPORTED = (
     "cpz_verify_batch", "cpz_verify_batch_device", "cpz_combine_partials", "cpz_msm",
     "cpz_parse_proofs", "cpz_parse_proofs_device", "cpz_verify_each_multi", "cpz_verify_batch_multi",
     "cpz_verify_response", "cpz_verify_response_device", "cpz_prove", "cpz_prove_device", "cpz_decode_points",
-    "cpz_abi_version", "cpz_ctx_set_commitment_checks", "cpz_ctx_stage_times_n",
+    "cpz_abi_version", "cpz_ctx_set_commitment_checks", "cpz_ctx_stage_times_n", "cpz_ctx_fallback_stats",
 )
 NUM_STAGES = 16
+FALLBACK_STATS = 6
+FALLBACK_PATHS = {0: "none", 1: "bisection", 2: "partitioned", 3: "per_proof"}
 ABI_VERSION = 3     # CPZ_ABI_VERSION of the cpz.h these declarations follow
 
 
@@ -112,6 +114,8 @@ def _declare(lib):
     lib.cpz_ctx_stage_times_n.restype = ctypes.c_int
     lib.cpz_ctx_stage_times_n.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_int)]
+    lib.cpz_ctx_fallback_stats.restype = ctypes.c_int
+    lib.cpz_ctx_fallback_stats.argtypes = [_p, ctypes.POINTER(ctypes.c_uint64)]
     lib.cpz_ctx_create_timing_only.restype = ctypes.c_int
     lib.cpz_ctx_create_timing_only.argtypes = [ctypes.c_int, ctypes.POINTER(_p)]
     lib.cpz_prove_synthetic_device.restype = ctypes.c_int

@@ -92,6 +92,9 @@ struct VerifyArgs {
                                     // instead of reading c / status from k_challenge
   int eq_only = 0;                  // commitment checks off: identity r1 / r2 and zero s are not
                                     // reported, the equations alone decide (verify_proof)
+  const uint32_t* blocks = nullptr; // k_verify_prepared: workgroup g verifies the kVerifyBlock
+                                    // proofs of block blocks[g] (the partitioned check's failing
+                                    // blocks); n bounds the global proof index
 };
 
 struct ProveArgs {

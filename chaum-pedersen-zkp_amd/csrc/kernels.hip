@@ -367,9 +367,10 @@ __device__ __forceinline__ void verify_one_row(const VerifyArgs& a, int64_t i, c
 // statuses come from the RLC prepare of the same batch, so only the equations are checked.
 __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_prepared(VerifyArgs a) {
   const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
-  const int64_t i = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;  // one proof per thread
+  const int64_t l = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;  // this launch's thread: its slab slot
+  const int64_t i = a.blocks ? (int64_t)a.blocks[blockIdx.x] * kVerifyBlock + threadIdx.x : l;  // one proof per thread
   if (i >= a.n) return;
-  const SlabTable tab{a.scratch, (uint32_t)i * (uint32_t)(kCachedEntries * sizeof(ge_cached))};
+  const SlabTable tab{a.scratch, (uint32_t)l * (uint32_t)(kCachedEntries * sizeof(ge_cached))};
   __shared__ uint32_t dig[16 * kVerifyBlock];
   {
     if (a.status[i] != kStOk) return;  // decode-level rejection: already final

@@ -1,0 +1,339 @@
+// Partitioned batch check on gfx950: the random-linear-combination partial of every block of
+// 256 proofs, so that a failing batch goes to per-proof verification only where a block
+// fails -- the fallback of verify_batch (batch.rs:262-268) / verify_individually
+// (batch.rs:314-318) at forgery densities where bisection cannot prune (configs[4]: 0.1 %
+// forged leaves ~77 % of 256-proof blocks clean, but every range of a few thousand proofs
+// dirty).
+//
+// Block b's partial is the corrected batch equation over its own proofs (rlc.hip header):
+//   P_b = sum_{i in b} [a_i s_i] g - [a_i] r1_i - [a_i c_i] y1_i + [b_i s_i] h - [b_i] r2_i - [b_i c_i] y2_i
+// with the same 128-bit weights, so sum_b P_b is the batch's partial, and P_b is the identity
+// iff every proof of b satisfies both equations (except with probability 2^-128 per forged
+// proof).  It is one Pippenger MSM per block over 1026 points (the block's 4 x 256 prepared
+// points and g, h with the block's weight sums): signed radix-2^8 digits (each radix-2^16
+// digit d of the prepare split as d = lo + 2^8 hi, lo in [-128, 128), hi in [-128, 128]),
+// 32 windows of 128 buckets.
+//   k_part_sort     1 workgroup / block: LDS counting sort of the block's entries by (window,
+//                   bucket) -> a list of 16-bit point ids and per-window bucket offsets.
+//   k_part_acc      1 wave / block; lane (p, h) owns buckets 32h+1 .. 32h+32 of windows p and
+//                   p + 16 and walks their entries from the lowest bucket up with the running-sum
+//                   reduction: run += entry point, and at each bucket boundary acc += run, so
+//                   run = sum_d B_d and acc = sum_d (32h + 33 - d) B_d without storing a bucket.
+//                   Both kinds of step are the same extended + cached addition on selected
+//                   operands, so lanes at different buckets never diverge.
+//   k_part_combine  1 quad / block (16 blocks per wave): T_v = sum_d d B_d from the four lanes'
+//                   (acc, run), P_b = sum_v 2^(8 v) T_v by Horner, quad-cooperative; P_b and its
+//                   identity flag.
+//   k_part_sum1/2   sum_b P_b -> the batch partial (encoded only when it is not the identity).
+#include <hip/hip_runtime.h>
+
+#include "rlc.h"
+#include "rlc_dev.h"
+#include "verify.h"
+
+namespace cpz {
+
+// d = lo + 2^8 hi with lo in [-128, 128) and hi in [-128, 128] for d in [-2^15, 2^15).
+__device__ __forceinline__ void split8(int d, int& lo, int& hi) {
+  lo = ((d + 128) & 255) - 128;
+  hi = (d - lo) >> 8;
+}
+
+__device__ __forceinline__ int digit16(const uint2& g, int q) {
+  const uint32_t w = q < 2 ? g.x : g.y;
+  return (int)(int16_t)(uint16_t)(w >> (16 * (q & 1)));
+}
+
+// ---------------------------------------------------------------------------------------
+// k_part_sort: thread t holds proof t's four points (prepared order -r1, -y1, -r2, -y2),
+// threads 0 / 1 also g / h with the block's weight sums (ids 1024 / 1025).
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_part_sort(PartArgs a) {
+  __shared__ uint32_t cur[kPartWindows][kPartBuckets];
+  __shared__ uint32_t wtot[kPartWindows];
+  __shared__ uint32_t wbase[kPartWindows + 1];
+  const int64_t b = blockIdx.x, gb = a.blk0 + b;
+  const int t = threadIdx.x;
+  for (int i = t; i < kPartWindows * kPartBuckets; i += 256) (&cur[0][0])[i] = 0;
+  const int64_t pi = kPartProofs * gb + t;
+  const int64_t j0 = 4 * pi;
+  const bool in = pi < a.n;  // past the batch's end (last block): no entries
+  int16_t ex[kRlcWindows];
+  if (t < 2) {
+    const sc s = a.block_sums[2 * gb + t];
+    recode16(ex, s.w);
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int w = 0; w < kRlcWindows; w++) {
+    const uint2 g = in ? *reinterpret_cast<const uint2*>(a.digits + w * a.dstride + j0) : make_uint2(0u, 0u);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      int lo, hi;
+      split8(digit16(g, q), lo, hi);
+      if (lo) atomicAdd(&cur[2 * w][(lo < 0 ? -lo : lo) - 1], 1u);
+      if (hi) atomicAdd(&cur[2 * w + 1][(hi < 0 ? -hi : hi) - 1], 1u);
+    }
+    if (t < 2) {
+      int lo, hi;
+      split8(ex[w], lo, hi);
+      if (lo) atomicAdd(&cur[2 * w][(lo < 0 ? -lo : lo) - 1], 1u);
+      if (hi) atomicAdd(&cur[2 * w + 1][(hi < 0 ? -hi : hi) - 1], 1u);
+    }
+  }
+  __syncthreads();
+  // exclusive scan of each window's 128 counts: wave wv takes windows wv, wv + 4, ...; lane l
+  // buckets 2l and 2l + 1
+  {
+    const int lane = t & 63, wv = t >> 6;
+    for (int v = wv; v < kPartWindows; v += 4) {
+      const uint32_t c0 = cur[v][2 * lane], c1 = cur[v][2 * lane + 1], s = c0 + c1;
+      uint32_t x = s;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+      }
+      cur[v][2 * lane] = x - s;
+      cur[v][2 * lane + 1] = x - s + c0;
+      if (lane == 63) wtot[v] = x;
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    uint32_t r = 0;
+    for (int v = 0; v < kPartWindows; v++) {
+      wbase[v] = r;
+      r += wtot[v];
+    }
+    wbase[kPartWindows] = r;
+  }
+  __syncthreads();
+  uint16_t* offs = a.offs + b * kPartOffs;
+  for (int i = t; i < kPartOffs; i += 256) {
+    const int v = i / (kPartBuckets + 1), k = i % (kPartBuckets + 1);
+    offs[i] = (uint16_t)(k < kPartBuckets ? wbase[v] + cur[v][k] : wbase[v + 1]);
+  }
+  __syncthreads();
+  for (int i = t; i < kPartWindows * kPartBuckets; i += 256) (&cur[0][0])[i] += wbase[i / kPartBuckets];
+  __syncthreads();
+  uint16_t* list = a.lists + b * kPartListCap;
+#pragma unroll 1
+  for (int w = 0; w < kRlcWindows; w++) {
+    const uint2 g = in ? *reinterpret_cast<const uint2*>(a.digits + w * a.dstride + j0) : make_uint2(0u, 0u);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      int lo, hi;
+      split8(digit16(g, q), lo, hi);
+      const uint16_t id = (uint16_t)(4 * t + q);
+      if (lo) list[atomicAdd(&cur[2 * w][(lo < 0 ? -lo : lo) - 1], 1u)] = id | (lo < 0 ? 0x8000 : 0);
+      if (hi) list[atomicAdd(&cur[2 * w + 1][(hi < 0 ? -hi : hi) - 1], 1u)] = id | (hi < 0 ? 0x8000 : 0);
+    }
+    if (t < 2) {
+      int lo, hi;
+      split8(ex[w], lo, hi);
+      const uint16_t id = (uint16_t)(4 * kPartProofs + t);
+      if (lo) list[atomicAdd(&cur[2 * w][(lo < 0 ? -lo : lo) - 1], 1u)] = id | (lo < 0 ? 0x8000 : 0);
+      if (hi) list[atomicAdd(&cur[2 * w + 1][(hi < 0 ? -hi : hi) - 1], 1u)] = id | (hi < 0 ? 0x8000 : 0);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_part_acc
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ ge_p3 p3_select(const ge_p3& x, const ge_p3& y, bool c) {  // c ? y : x
+  ge_p3 r;
+  r.X = fe_select(x.X, y.X, c);
+  r.Y = fe_select(x.Y, y.Y, c);
+  r.Z = fe_select(x.Z, y.Z, c);
+  r.T = fe_select(x.T, y.T, c);
+  return r;
+}
+
+// One step of the running-sum walk: entry (run += q) or bucket boundary (acc += run), as one
+// extended + cached addition on selected operands (9 M either way).
+__device__ __forceinline__ void part_step(ge_p3& run, ge_p3& acc, bool entry, const ge_niels& q) {
+  ge_cached c;
+  const fe t2d = fe_mul(run.T, FE_D2());
+  c.YpX = fe_select(fe_add(run.Y, run.X), q.ypx, entry);
+  c.YmX = fe_select(fe_sub(run.Y, run.X), q.ymx, entry);
+  c.Z = fe_select(run.Z, fe_one(), entry);
+  c.T2d = fe_select(t2d, q.xy2d, entry);
+  const ge_p3 r = p1p1_to_p3(ge_add_cached(p3_select(acc, run, entry), c));
+  run = p3_select(run, r, entry);
+  acc = p3_select(r, acc, entry);
+}
+
+// The next entry's Niels point is brought into the wave's LDS slot by direct-to-LDS loads
+// (gfx950 global_load_lds_dwordx4: lane l's 16-byte vector v lands at slot[v][l]) while the
+// current step's arithmetic runs, so the prefetch costs no VGPRs (the kernel sits at the
+// 256-VGPR budget of 2 waves per SIMD).  Nothing is stored inside the walk, so the vmcnt
+// wait at the top of a step waits for that prefetch (and the id prefetch) only.
+__device__ __forceinline__ void part_stage(uint4 (*slot)[64], const PartArgs& a, const ge_niels* P, uint32_t id) {
+  const uint32_t j = id & 0x7fffu;
+  const ge_niels* src = j < 4u * kPartProofs ? P + j : a.tab + (j == 4u * kPartProofs ? 0 : kNielsEntriesRlc);
+  const uint4* g = reinterpret_cast<const uint4*>(src);
+#pragma unroll
+  for (int v = 0; v < 8; v++) __builtin_amdgcn_global_load_lds(g + v, &slot[v][0], 16, 0, 0);
+}
+
+// Lane (p, h) walks its quarter of window v's buckets UPWARD (its entries are one contiguous
+// run of the sorted list): run += entry, and at each bucket boundary acc += run, so at the
+// end S = run = sum_d B_d and A = acc = sum_d (32h + 33 - d) B_d; k_part_combine forms
+// sum_d (d - 32h) B_d = 33 S - A.
+__global__ void __launch_bounds__(256, 2) k_part_acc(PartArgs a) {
+  __shared__ uint4 stage[4][8][64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wv;
+  if (b >= a.nblk) return;  // whole waves
+  const int64_t gb = a.blk0 + b;
+  const int p = lane >> 2, h = lane & 3;
+  const uint16_t* list = a.lists + b * kPartListCap;
+  const ge_niels* P = a.pts + (int64_t)4 * kPartProofs * gb;
+  ge_p3* ws = a.wsum + b * kPartWsum;
+  uint4 (*slot)[64] = stage[wv];
+#pragma unroll 1
+  for (int pass = 0; pass < 2; pass++) {
+    const int v = p + 16 * pass;
+    const uint16_t* o = a.offs + b * kPartOffs + v * (kPartBuckets + 1);
+    const int klo = 32 * h;
+    int k = klo;
+    uint32_t e = o[k], eend = o[k + 1];
+    const uint32_t elast = o[klo + 32];
+    uint32_t cid = e < elast ? list[e] : 0u;
+    uint32_t nid = e + 1 < elast ? list[e + 1] : 0u;
+    if (e < eend) part_stage(slot, a, P, cid);
+    ge_p3 run = ge_identity(), acc = ge_identity();
+#pragma unroll 1
+    for (;;) {
+      const bool entry = e < eend;
+      const bool last = !entry && k == klo + 31;
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this step's point (and ids) arrived
+      ge_niels q;
+      uint4* qv = reinterpret_cast<uint4*>(&q);
+#pragma unroll
+      for (int u = 0; u < 8; u++) qv[u] = slot[u][lane];
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): read before the slot is refilled
+      q = ge_niels_cneg(q, (cid >> 15) != 0);
+      // the next step's position; its point (if it is an entry) staged now
+      uint32_t e2 = e, eend2 = eend;
+      int k2 = k;
+      uint32_t cid2 = cid, nid2 = nid;
+      if (entry) {
+        e2 = e + 1;
+        cid2 = nid;
+        nid2 = e + 2 < elast ? list[e + 2] : 0u;
+      } else if (!last) {
+        k2 = k + 1;
+        eend2 = o[k2 + 1];
+      }
+      if (!last && e2 < eend2) part_stage(slot, a, P, cid2);
+      part_step(run, acc, entry, q);
+      if (last) break;
+      e = e2;
+      eend = eend2;
+      k = k2;
+      cid = cid2;
+      nid = nid2;
+    }
+    store_p3(ws + (v * kPartQuarters + h) * 2, acc);      // A_h = sum (32h + 33 - d) B_d
+    store_p3(ws + (v * kPartQuarters + h) * 2 + 1, run);  // S_h = sum B_d
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// k_part_combine: quad j of the wave owns block 16 x blockIdx + j.
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_part_combine(PartArgs a) {
+  const int j = threadIdx.x >> 2, q = threadIdx.x & 3;
+  const int64_t b = (int64_t)blockIdx.x * 16 + j;
+  const bool live = b < a.nblk;
+  const ge_p3* ws = a.wsum + (live ? b : a.nblk - 1) * kPartWsum;  // dead quads: any block, dropped
+  ge_p3 P = ge_identity();
+#pragma unroll 1
+  for (int v = kPartWindows - 1; v >= 0; v--) {
+    // T_v = sum_d d B_d = sum_h (33 + 32 h) S_h - A_h = 32 (Stot + Sw) + Stot - Atot with
+    // Stot = sum_h S_h, Sw = S_1 + 2 S_2 + 3 S_3 = U + V + X (U = S_3, V = S_2 + U, X = S_1 + V)
+    const ge_p3* w = ws + v * kPartQuarters * 2;
+    const ge_p3 U = load_p3(w + 7);
+    const ge_p3 V = ge_add_quad(load_p3(w + 5), U, q);
+    const ge_p3 X = ge_add_quad(load_p3(w + 3), V, q);
+    const ge_p3 Stot = ge_add_quad(X, load_p3(w + 1), q);
+    const ge_p3 Sw = ge_add_quad(ge_add_quad(U, V, q), X, q);
+    ge_p3 At = ge_add_quad(load_p3(w + 0), load_p3(w + 2), q);
+    At = ge_add_quad(At, load_p3(w + 4), q);
+    At = ge_add_quad(At, load_p3(w + 6), q);
+    ge_p3 T = p3_dbl_n_quad(ge_add_quad(Stot, Sw, q), 5, q);
+    T = ge_add_quad(T, Stot, q);
+    T = ge_add_quad(T, ge_neg(At), q);
+    if (v == kPartWindows - 1) P = T;
+    else P = ge_add_quad(p3_dbl_n_quad(P, 8, q), T, q);
+  }
+  if (live && q == 0) {
+    store_p3(a.part + a.blk0 + b, P);
+    a.fail[a.blk0 + b] = ristretto_is_identity(P) ? 0 : 1;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// sum_b P_b: quads add 64 consecutive entries each, then one wave adds those.
+// ---------------------------------------------------------------------------------------
+constexpr int kPartSumRun = 64;
+
+__global__ void __launch_bounds__(64) k_part_sum1(const ge_p3* part, int64_t n, ge_p3* tmp) {
+  const int j = threadIdx.x >> 2, q = threadIdx.x & 3;
+  const int64_t g = (int64_t)blockIdx.x * 16 + j;
+  const int64_t lo = g * kPartSumRun;
+  ge_p3 acc = ge_identity();
+#pragma unroll 1
+  for (int k = 0; k < kPartSumRun; k++)
+    if (lo + k < n) acc = ge_add_quad(acc, load_p3(part + lo + k), q);  // uniform per quad
+  if (q == 0 && lo < n) store_p3(tmp + g, acc);
+}
+
+__global__ void __launch_bounds__(64) k_part_sum2(const ge_p3* tmp, int64_t m, uint32_t* partial_out,
+                                                  int* identity_out) {
+  __shared__ ge_p3 lds[16];
+  const int j = threadIdx.x >> 2, q = threadIdx.x & 3;
+  ge_p3 acc = ge_identity();
+#pragma unroll 1
+  for (int64_t k = j; k < m; k += 16) acc = ge_add_quad(acc, load_p3(tmp + k), q);
+  if (q == 0) lds[j] = acc;
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    ge_p3 s = lds[0];
+#pragma unroll 1
+    for (int k = 1; k < 16; k++) s = ge_add_quad(s, lds[k], q);
+    if (q == 0) {
+      const bool id = ristretto_is_identity(s);
+      uint32_t enc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (!id) ristretto_encode(enc, s);
+      for (int k = 0; k < 8; k++) partial_out[k] = enc[k];
+      identity_out[0] = id ? 1 : 0;
+    }
+  }
+}
+
+hipError_t launch_part_msm(const PartArgs& a, hipStream_t st) {
+  if (a.nblk <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_part_sort, dim3((unsigned)a.nblk), dim3(256), 0, st, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_part_acc, dim3((unsigned)((a.nblk + 3) / 4)), dim3(256), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_part_combine, dim3((unsigned)((a.nblk + 15) / 16)), dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_part_sum(const ge_p3* part, int64_t nblk, ge_p3* tmp, uint32_t* partial_out, int* identity_out,
+                           hipStream_t st) {
+  const int64_t m = (nblk + kPartSumRun - 1) / kPartSumRun;
+  hipLaunchKernelGGL(k_part_sum1, dim3((unsigned)((m + 15) / 16)), dim3(64), 0, st, part, nblk, tmp);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_part_sum2, dim3(1), dim3(64), 0, st, tmp, m, partial_out, identity_out);
+  return hipGetLastError();
+}
+
+}  // namespace cpz

@@ -93,6 +93,42 @@ struct RlcPipe {
   hipEvent_t done = nullptr;        // the side stream's work done
 };
 
+// ---- partitioned batch check (part.hip) --------------------------------------------------
+// The batch's prepared points cut into blocks of kPartProofs proofs (the weight blocks); one
+// Pippenger MSM per block with signed 8-bit windows (the 16-bit digits of the prepare split in
+// two), giving every block's partial P_b = sum over its proofs of the RLC terms.  A block with
+// P_b the identity holds no forgery (w.o.p.); the others go to per-proof verification.
+constexpr int kPartProofs = kRlcPrepBlock;           // 256 proofs per block
+constexpr int kPartPoints = 4 * kPartProofs + 2;      // + g, h with the block's weight sums
+constexpr int kPartWindows = 2 * kRlcWindows;         // 32 signed radix-2^8 windows
+constexpr int kPartBuckets = 128;                     // |digit| in [1, 128]
+constexpr int kPartQuarters = 4;                      // lanes per window pair (32 buckets each)
+constexpr int kPartListCap = kPartWindows * kPartPoints;  // sorted entries per block, at most
+constexpr int kPartOffs = kPartWindows * (kPartBuckets + 1);
+constexpr int kPartWsum = kPartWindows * kPartQuarters * 2;  // (W, S) per window and quarter
+
+struct PartArgs {
+  int64_t nblk;                  // blocks of this launch: [blk0, blk0 + nblk) of the prepared set
+  int64_t blk0;
+  int64_t n;                     // proofs of the prepared set (the last block may be partial)
+  const ge_niels* pts;           // prepared negated Niels points, 4 per proof
+  const int16_t* digits;         // [16][dstride] signed radix-2^16 digits
+  int64_t dstride;
+  const sc* block_sums;          // [blocks][2]: sum a s, sum b s per block
+  const ge_niels* tab;           // g at tab[0], h at tab[kNielsEntriesRlc]
+  uint16_t* lists;               // [nblk][kPartListCap] point ids (bit 15: negate) sorted by (window, bucket)
+  uint16_t* offs;                // [nblk][kPartOffs] bucket starts per window (+ window end)
+  ge_p3* wsum;                   // [nblk][kPartWsum]
+  ge_p3* part;                   // [blocks] P_b (indexed by the global block)
+  uint8_t* fail;                 // [blocks] 1 iff P_b is not the identity
+};
+
+hipError_t launch_part_msm(const PartArgs& a, hipStream_t st);
+// out = sum of part[0 .. nblk) (encoded, identity flag), through the scratch `tmp` of
+// ceil(nblk / 16) ge_p3
+hipError_t launch_part_sum(const ge_p3* part, int64_t nblk, ge_p3* tmp, uint32_t* partial_out, int* identity_out,
+                           hipStream_t st);
+
 hipError_t launch_rlc_prepare(const RlcPrepArgs& a, hipStream_t st);
 // Sort geometry for `npts` MSM points: sets a.groups / a.chunk.
 void rlc_sort_geometry(RlcMsmArgs& a, int64_t npts);

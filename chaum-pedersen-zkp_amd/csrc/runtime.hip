@@ -156,6 +156,11 @@ struct cpz_ctx {
   RlcPrepared rl_prep;
   RlcMsmSet rl_msm;
   DevBuf rl_flags, rl_parts;
+  // partitioned batch check (part.hip): sorted lists / offsets / window sums of one chunk of
+  // blocks, every block's partial and fail flag, the sum's scratch, the failing-block list
+  DevBuf pt_lists, pt_offs, pt_wsum, pt_part, pt_fail, pt_tmp, pt_blocks;
+  // what the last batch call's fallback did (cpz_ctx_fallback_stats)
+  uint64_t fb_stats[CPZ_FALLBACK_STATS] = {};
   // commitment checks (statuses 4 and 5: the Proof::from_bytes rejections); off = equations only
   bool eq_only = false;
   // pipelined MSM tails (cpz::RlcPipe): a high-priority side stream and its events
@@ -759,6 +764,7 @@ constexpr int kProbeChunks = 16;
 int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const void* y2, const void* r1, const void* r2,
                  const void* s, uint8_t* status, hipStream_t st, int depth, bool allow_probe = true) {
   auto per_proof = [&](int64_t a, int64_t b) -> int {
+    ctx->fb_stats[4] += (uint64_t)(b - a);
     cpz::VerifyArgs va;
     va.n = b - a;
     va.y1 = static_cast<const uint32_t*>(y1) + 8 * a;
@@ -823,6 +829,7 @@ int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const voi
     int ident = 0;
     int rc = rlc_range(ctx, cuts[k], cuts[k + 1], st, part, &ident);
     if (rc) return rc;
+    ctx->fb_stats[5] += 1;
     fail[k] = !ident;
     nfail += fail[k] ? 1 : 0;
   }
@@ -867,16 +874,139 @@ int launch_probe(cpz_ctx* ctx, size_t n, const void* const rows[5], int64_t star
   return kProbeChunks;
 }
 
+// Per-proof verification (k_verify_prepared) of the listed blocks of kVerifyBlock proofs of the
+// prepared batch: launches of at most half the occupancy grid, round-robin over the verify
+// streams and their scratch slabs (as launch_verify_chunks).
+int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* status, const uint32_t* d_blocks,
+                           int64_t nb, hipStream_t st) {
+  static_assert(cpz::kVerifyBlock == cpz::kPartProofs, "a listed block is one verify workgroup");
+  if (nb <= 0) return CPZ_OK;
+  const int full = (occupancy_grid(ctx) + CPZ_VERIFY_CHUNK_DIV - 1) / CPZ_VERIFY_CHUNK_DIV;
+  const size_t slab = (size_t)full * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached);
+  CPZ_HIP(ctx->scratch.ensure((size_t)CPZ_VERIFY_STREAMS * slab));
+  const int64_t chunks = (nb + full - 1) / full;
+  const int nst = (int)std::min<int64_t>(CPZ_VERIFY_STREAMS, chunks);
+  if (nst > 1) {
+    if (!ctx->aux_start) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_start, hipEventDisableTiming));
+    CPZ_HIP(hipEventRecord(ctx->aux_start, st));
+    for (int k = 0; k < nst - 1; k++) {
+      if (!ctx->aux_stream[k]) CPZ_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[k], hipStreamNonBlocking));
+      if (!ctx->aux_done[k]) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_done[k], hipEventDisableTiming));
+      CPZ_HIP(hipStreamWaitEvent(ctx->aux_stream[k], ctx->aux_start, 0));
+    }
+  }
+  cpz::VerifyArgs va;
+  va.n = n;
+  va.s = static_cast<const uint32_t*>(s);
+  va.c = static_cast<const uint32_t*>(ctx->c.p);
+  va.status = status;
+  va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
+  va.pre = static_cast<const cpz::ge_niels*>(ctx->rl_prep.pts.p);
+  va.eq_only = ctx->eq_only ? 1 : 0;
+  for (int64_t c = 0; c < chunks; c++) {
+    const int64_t g0 = c * full;
+    const int g = (int)std::min<int64_t>(full, nb - g0);
+    cpz::VerifyArgs v = va;
+    v.blocks = d_blocks + g0;
+    const int k = (int)(c % nst);
+    v.scratch = static_cast<char*>(ctx->scratch.p) + (size_t)k * slab;
+    hipStream_t sc = k == 0 ? st : ctx->aux_stream[k - 1];
+    StageTimer t(ctx, 1, sc);
+    CPZ_HIP(cpz::launch_verify_each(v, g, sc));
+  }
+  if (nst > 1) {
+    for (int k = 0; k < nst - 1; k++) {
+      CPZ_HIP(hipEventRecord(ctx->aux_done[k], ctx->aux_stream[k]));
+      CPZ_HIP(hipStreamWaitEvent(st, ctx->aux_done[k], 0));
+    }
+  }
+  return CPZ_OK;
+}
+
+// Blocks per launch of the partitioned MSM (bounds its list / window-sum buffers: ~72 KB of
+// lists and offsets and 40 KB of window sums per block).
+constexpr int64_t kPartChunkBlocks = 8192;
+// Density probe outcomes (invalid entries among the kProbeChunks x 256 sampled) for which the
+// partitioned check pays: its MSM costs ~0.3 of per-proof verification per proof, and a block
+// of 256 is clean with probability (1 - rho)^256; above ~12 sampled (rho > ~0.3 %) more than
+// half the blocks fail and plain per-proof verification is cheaper.
+constexpr int kPartMaxProbeBad = 12;
+
+// The partitioned fallback over the prepared batch: every block's partial (k_part_*), the
+// batch partial as their sum, and per-proof verification of the failing blocks only.
+int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, uint8_t partial[32], int* identity,
+                  hipStream_t st) {
+  const int64_t nblk = (n + cpz::kPartProofs - 1) / cpz::kPartProofs;
+  const int64_t chunk = std::min<int64_t>(nblk, kPartChunkBlocks);
+  CPZ_HIP(ctx->pt_lists.ensure((size_t)chunk * cpz::kPartListCap * sizeof(uint16_t)));
+  CPZ_HIP(ctx->pt_offs.ensure((size_t)chunk * cpz::kPartOffs * sizeof(uint16_t)));
+  CPZ_HIP(ctx->pt_wsum.ensure((size_t)chunk * cpz::kPartWsum * sizeof(cpz::ge_p3)));
+  CPZ_HIP(ctx->pt_part.ensure((size_t)nblk * sizeof(cpz::ge_p3)));
+  CPZ_HIP(ctx->pt_fail.ensure((size_t)nblk));
+  CPZ_HIP(ctx->pt_tmp.ensure((size_t)((nblk + 63) / 64 + 16) * sizeof(cpz::ge_p3)));
+  CPZ_HIP(ctx->pt_blocks.ensure((size_t)nblk * sizeof(uint32_t)));
+  if (int rc = rlc_reserve_msm(ctx->rl_msm, 1)) return rc;  // its partial / flag words
+  {
+    StageTimer t(ctx, 3, st);
+    cpz::PartArgs pa;
+    pa.n = n;
+    pa.pts = static_cast<const cpz::ge_niels*>(ctx->rl_prep.pts.p);
+    pa.digits = static_cast<const int16_t*>(ctx->rl_prep.dig.p);
+    pa.dstride = rlc_dstride(ctx->rl_prep.cap);
+    pa.block_sums = static_cast<const cpz::sc*>(ctx->rl_prep.bsum.p);
+    pa.tab = static_cast<const cpz::ge_niels*>(ctx->tab.p);
+    pa.lists = static_cast<uint16_t*>(ctx->pt_lists.p);
+    pa.offs = static_cast<uint16_t*>(ctx->pt_offs.p);
+    pa.wsum = static_cast<cpz::ge_p3*>(ctx->pt_wsum.p);
+    pa.part = static_cast<cpz::ge_p3*>(ctx->pt_part.p);
+    pa.fail = static_cast<uint8_t*>(ctx->pt_fail.p);
+    for (int64_t b0 = 0; b0 < nblk; b0 += chunk) {
+      pa.blk0 = b0;
+      pa.nblk = std::min<int64_t>(chunk, nblk - b0);
+      CPZ_HIP(cpz::launch_part_msm(pa, st));
+    }
+    CPZ_HIP(cpz::launch_part_sum(pa.part, nblk, static_cast<cpz::ge_p3*>(ctx->pt_tmp.p),
+                                 static_cast<uint32_t*>(ctx->rl_msm.partial.p), static_cast<int*>(ctx->rl_msm.flags.p),
+                                 st));
+  }
+  std::vector<uint8_t> dirty((size_t)nblk);
+  int flags[1];
+  CPZ_HIP(hipMemcpyAsync(dirty.data(), ctx->pt_fail.p, (size_t)nblk, hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipMemcpyAsync(partial, ctx->rl_msm.partial.p, 32, hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipMemcpyAsync(flags, ctx->rl_msm.flags.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipStreamSynchronize(st));
+  *identity = flags[0];
+  std::vector<uint32_t> blocks;
+  for (int64_t b = 0; b < nblk; b++)
+    if (dirty[(size_t)b]) blocks.push_back((uint32_t)b);
+  ctx->fb_stats[1] = (uint64_t)nblk;
+  ctx->fb_stats[2] = blocks.size();
+  ctx->fb_stats[3] = std::min<uint64_t>((uint64_t)blocks.size() * cpz::kPartProofs, (uint64_t)n);
+  if (blocks.empty()) return CPZ_OK;
+  CPZ_HIP(hipMemcpyAsync(ctx->pt_blocks.p, blocks.data(), blocks.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  StageTimer span(ctx, 4, st);  // wall time of the per-proof pass; launches timed as verify_each
+  int rc = verify_prepared_blocks(ctx, n, s, d_status, static_cast<const uint32_t*>(ctx->pt_blocks.p),
+                                  (int64_t)blocks.size(), st);
+  if (rc) return rc;
+  CPZ_HIP(hipStreamSynchronize(st));  // `blocks` is pageable host memory read by the copy above
+  return CPZ_OK;
+}
+
 int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
                       const void* s, const void* cb, const uint64_t* co, const uint8_t* cp, uint8_t* d_status,
                       const uint8_t seed[32], uint64_t first_index, uint8_t partial_out[32], int* batch_ok,
                       int fallback, uint8_t* host_status, hipStream_t st) {
   // A fallback-enabled check of a large batch without contexts first samples its density,
   // beside the batch's challenges (the probe's ~0.5 ms of per-proof latency hides under
-  // them).  A dense batch (>= 2 invalid entries among the kProbeChunks x 256 sampled)
-  // cannot pass and bisection cannot prune it: nothing is prepared, every entry is verified
-  // per proof (k_verify_each on the challenges just computed), and partial_out is 32 x 0xff
-  // ("no partial": not an encoding) -- the cost of the per-proof path plus the probe.
+  // them).  Two or more invalid entries among the kProbeChunks x 256 sampled: the batch
+  // cannot pass and bisection cannot prune it (every range of a few thousand proofs fails).
+  //   * up to kPartMaxProbeBad sampled (density up to ~0.3 %, configs[4]'s 0.1 %): the
+  //     partitioned check -- prepare, every 256-proof block's partial in one pass, per-proof
+  //     verification of the failing blocks only; partial_out is the batch's partial.
+  //   * denser: nothing is prepared, every entry is verified per proof (k_verify_each on the
+  //     challenges just computed), and partial_out is 32 x 0xff ("no partial": not an
+  //     encoding) -- the cost of the per-proof path plus the probe.
+  for (auto& v : ctx->fb_stats) v = 0;
   int64_t starts[kProbeChunks];
   const bool probe = fallback && co == nullptr && (int64_t)n >= kProbeMin;
   if (probe) {
@@ -895,7 +1025,25 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
     CPZ_HIP(hipStreamSynchronize(ctx->probe_stream));
     int bad = 0;
     for (uint8_t v : pst) bad += (v == cpz::kStatusEqFail) ? 1 : 0;
-    if (bad >= 2) {
+    ctx->fb_stats[1] = (uint64_t)bad;
+    if (bad >= 2 && bad <= kPartMaxProbeBad) {
+      ctx->fb_stats[0] = CPZ_FALLBACK_PARTITIONED;
+      if ((rc = rlc_prepare_points(ctx, n, y1, y2, r1, r2, s, d_status, seed, first_index, st))) return rc;
+      uint8_t part[32];
+      int ident = 0;
+      if ((rc = part_fallback(ctx, (int64_t)n, s, d_status, part, &ident, st))) return rc;
+      ctx->fb_stats[4] = ctx->fb_stats[3];
+      if (partial_out) std::memcpy(partial_out, part, 32);
+      if (batch_ok) *batch_ok = 0;  // the probe saw invalid entries
+      if (host_status) {
+        CPZ_HIP(hipMemcpyAsync(host_status, d_status, n, hipMemcpyDeviceToHost, st));
+        CPZ_HIP(hipStreamSynchronize(st));
+      }
+      return CPZ_OK;
+    }
+    if (bad > kPartMaxProbeBad) {
+      ctx->fb_stats[0] = CPZ_FALLBACK_PER_PROOF;
+      ctx->fb_stats[4] = (uint64_t)n;
       if (partial_out) std::memset(partial_out, 0xff, 32);
       if (batch_ok) *batch_ok = 0;
       cpz::VerifyArgs va;
@@ -935,6 +1083,7 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
   const bool all_live = any_bad == 0;
   if (batch_ok) *batch_ok = (ident && all_live) ? 1 : 0;
   if (!ident && fallback) {
+    ctx->fb_stats[0] = CPZ_FALLBACK_BISECTION;
     rc = rlc_fallback(ctx, 0, (int64_t)n, y1, y2, r1, r2, s, d_status, st, 0, !probe);
     if (rc) return rc;
     CPZ_HIP(hipStreamSynchronize(st));  // statuses complete on return (documented)
@@ -1015,6 +1164,13 @@ int cpz_ctx_create_timing_only(int device_ordinal, cpz_ctx** out) { return ctx_c
 #endif
 
 int cpz_abi_version(void) { return CPZ_ABI_VERSION; }
+
+int cpz_ctx_fallback_stats(cpz_ctx* ctx, uint64_t out[CPZ_FALLBACK_STATS]) {
+  if (!ctx || !out) return fail(CPZ_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  std::memcpy(out, ctx->fb_stats, sizeof(ctx->fb_stats));
+  return CPZ_OK;
+}
 
 int cpz_ctx_set_commitment_checks(cpz_ctx* ctx, int enable) {
   if (!ctx) return fail(CPZ_EINVAL, "null context");
@@ -1358,6 +1514,9 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   for (DevBuf* b : {&ctx->pz_blob, &ctx->pz_off, &ctx->pz_rows, &ctx->pz_code, &ctx->pz_aux}) b->release();
   ctx->rl_prep.release();
   ctx->rl_msm.release();
+  for (DevBuf* b : {&ctx->pt_lists, &ctx->pt_offs, &ctx->pt_wsum, &ctx->pt_part, &ctx->pt_fail, &ctx->pt_tmp,
+                    &ctx->pt_blocks})
+    b->release();
   ctx->rl_flags.release();
   ctx->rl_parts.release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -170,9 +170,12 @@ int cpz_prove_synthetic_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t 
  *                With a fallback, a batch of >= 2^20 entries without contexts is first
  *                sampled (4096 entries verified per proof, beside the batch's challenges):
  *                if two or more sampled entries are invalid the batch cannot pass and
- *                bisection could not prune it, so nothing is prepared, every entry is
- *                verified per proof, batch_ok = 0 and partial_out is 32 bytes of 0xff (not
- *                an encoding: "no partial computed").
+ *                bisection could not prune it.  Up to 12 sampled invalid entries (density
+ *                up to ~0.3 %): the partitioned check -- every 256-proof block's own RLC
+ *                partial, per-proof verification of the failing blocks only; partial_out
+ *                is the batch's partial as usual.  More: nothing is prepared, every entry
+ *                is verified per proof, batch_ok = 0 and partial_out is 32 bytes of 0xff
+ *                (not an encoding: "no partial computed").
  * The _device form takes device-resident inputs and always needs d_status_out (decode-level
  * statuses, or exact ones when fallback != 0); it synchronises `stream`. */
 int cpz_verify_batch(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
@@ -186,6 +189,23 @@ int cpz_verify_batch_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[3
                             const uint8_t *d_ctx_present, const uint8_t seed[32], uint64_t first_index,
                             uint8_t partial_out[32], int *batch_ok, void *d_status_out, int fallback,
                             void *stream);
+
+/* What the last cpz_verify_batch[_device] call on the context did to locate invalid entries
+ * (fallback != 0), for tests and benchmarks:
+ *   out[0]  path: CPZ_FALLBACK_NONE (the batch passed, or no fallback), _BISECTION (sub-range
+ *           RLC partials, per-proof leaves), _PARTITIONED (every 256-proof block's partial,
+ *           per-proof verification of the failing blocks), _PER_PROOF (dense: everything)
+ *   out[1]  invalid entries the density probe saw (0 without a probe)
+ *   out[2]  blocks whose partial the partitioned check computed
+ *   out[3]  blocks whose partial was not the identity
+ *   out[4]  entries the fallback verified per proof
+ *   out[5]  sub-range MSMs the bisection ran */
+#define CPZ_FALLBACK_STATS 6
+#define CPZ_FALLBACK_NONE 0
+#define CPZ_FALLBACK_BISECTION 1
+#define CPZ_FALLBACK_PARTITIONED 2
+#define CPZ_FALLBACK_PER_PROOF 3
+int cpz_ctx_fallback_stats(cpz_ctx *ctx, uint64_t out[CPZ_FALLBACK_STATS]);
 
 /* Bulk Ristretto255::element_from_bytes (ristretto.rs:120-138) on the device: ok_out[i] = 1 iff
  * the 32-byte encoding points[i] decodes (RFC 9496), and, when reencoded_out is not NULL, the

@@ -12,7 +12,7 @@ use std::env;
 use std::path::PathBuf;
 use std::process::Command;
 
-const UNITS: [&str; 3] = ["kernels.hip", "rlc.hip", "runtime.hip"];
+const UNITS: [&str; 4] = ["kernels.hip", "rlc.hip", "part.hip", "runtime.hip"];
 
 fn main() {
     println!("cargo:rerun-if-env-changed=CPZ_LIB_DIR");

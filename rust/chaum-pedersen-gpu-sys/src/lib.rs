@@ -47,6 +47,11 @@ pub const CPZ_PARSE_ZERO_S: u8 = 20;
 
 pub const CPZ_NUM_STAGES: usize = 16;
 pub const CPZ_ABI_VERSION: c_int = 3;
+pub const CPZ_FALLBACK_STATS: usize = 6;
+pub const CPZ_FALLBACK_NONE: u64 = 0;
+pub const CPZ_FALLBACK_BISECTION: u64 = 1;
+pub const CPZ_FALLBACK_PARTITIONED: u64 = 2;
+pub const CPZ_FALLBACK_PER_PROOF: u64 = 3;
 
 /// Opaque verifier context (one GPU, its stream, cached generator tables, buffers).
 #[repr(C)]
@@ -60,6 +65,7 @@ extern "C" {
     pub fn cpz_ctx_create(device_ordinal: c_int, out: *mut *mut cpz_ctx) -> c_int;
     pub fn cpz_ctx_destroy(ctx: *mut cpz_ctx);
     pub fn cpz_ctx_set_commitment_checks(ctx: *mut cpz_ctx, enable: c_int) -> c_int;
+    pub fn cpz_ctx_fallback_stats(ctx: *mut cpz_ctx, out: *mut u64) -> c_int;
     pub fn cpz_last_error() -> *const c_char;
     pub fn cpz_default_generators(g: *mut u8, h: *mut u8);
     pub fn cpz_verify_each(ctx: *mut cpz_ctx, g: *const u8, h: *const u8, n: usize, y1: *const u8, y2: *const u8,

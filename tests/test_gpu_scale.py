@@ -244,3 +244,38 @@ def test_spans_forged_only_in_a_later_span(gpu):
     assert not ok and p == want
     p, ok = gpu.verify_batch_device(*(t[k][:lo] for k in KEYS), st[:lo], WSEED)
     assert ok and p == bytes(32)
+
+
+def _blocks_with(idx, n):
+    return np.unique(np.asarray(idx) // 256)
+
+
+@pytest.mark.parametrize("n", [1 << 22, (1 << 20) + 77])
+def test_partitioned_fallback_at_c5_density(gpu, n):
+    """configs[4]'s density (0.1 % forged, half s + 1, half wrong y1) through the batch check
+    with its fallback: the density probe sees a few invalid samples, so the fallback is the
+    partitioned check -- every 256-proof block's RLC partial, then per-proof verification of
+    the failing blocks ONLY.  Checked: the exact forged set (statuses 1 there, 0 elsewhere);
+    the batch partial equals the C oracle's partial of the forged entries alone; the path
+    taken; the failing blocks are exactly the blocks holding a forgery; and no entry of a
+    clean block is verified per proof (per_proof == the failing blocks' proofs).  The ragged
+    size puts a forgery in the partial last block."""
+    torch = pytest.importorskip("torch")
+    t = _synthetic_device(gpu, torch, n)
+    rng = np.random.default_rng(4242 + n)
+    idx = np.sort(rng.choice(n - 1, size=max(8, n // 1000) - 1, replace=False))
+    idx = np.union1d(idx, [n - 1])
+    host = _forge(t, torch, idx)
+    st = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    p, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED, fallback=True)
+    stats = gpu.fallback_stats()
+    got = st.cpu().numpy()
+    assert not ok
+    assert np.array_equal(np.nonzero(got)[0], idx) and set(got[idx].tolist()) == {1}
+    assert stats["path"] == "partitioned", stats
+    dirty = _blocks_with(idx, n)
+    nblk = (n + 255) // 256
+    assert stats["blocks_checked"] == nblk and stats["blocks_failing"] == dirty.size, (stats, dirty.size)
+    want_pp = sum(min(256, n - 256 * int(b)) for b in dirty)
+    assert stats["per_proof"] == want_pp
+    assert p == _oracle_partial(host, idx)
