@@ -59,6 +59,31 @@ def _profile(name):
     return (_load_json(os.path.join("profiles", cands[-1])) or {}) if cands else {}
 
 
+def mad_peak_at_kernel_clock(oc):
+    """The v_mad_i64_i32 issue ceiling at the clock k_verify_each itself runs at: the best
+    measured lane rate per SIMD cycle (tools/ubench/clock_rates.hip, profiles/rNN_clock_rates.json:
+    event-timed launch cycles at the measured shader clock) x 1024 SIMDs x the kernel's own
+    shader clock (in-kernel s_memtime / s_memrealtime probe of a timing-only build,
+    profiles/rNN_verify_clock_probe.json).  None when either file is missing."""
+    pdir = os.path.join(ROOT, "profiles")
+    cr_f = sorted(f for f in os.listdir(pdir) if f.endswith("_clock_rates.json"))
+    pr_f = sorted(f for f in os.listdir(pdir) if f.endswith("_verify_clock_probe.json"))
+    if not cr_f or not pr_f:
+        return None
+    cr = _load_json(os.path.join("profiles", cr_f[-1])) or {}
+    pr = _load_json(os.path.join("profiles", pr_f[-1])) or {}
+    rows = [r for r in cr.get("rows", []) if r.get("op") == "v_mad_i64_i32"]
+    clk = (pr.get("shader_clock_ghz") or {}).get("mean")
+    if not rows or not clk:
+        return None
+    simds = 4 * cr.get("cus", 256)
+    best = max(rows, key=lambda r: r.get("gops", 0.0))
+    lanes = best.get("lanes_per_simd_cycle") or best["gops"] * 1e9 / (simds * best["clock_ghz"] * 1e9)
+    return {"peak": lanes * simds * clk * 1e9, "lanes_per_simd_cycle": lanes, "clock_ghz": clk,
+            "best_waves_per_simd": best.get("waves_per_simd"), "ubench_clock_ghz": best.get("clock_ghz"),
+            "sources": ["profiles/" + cr_f[-1], "profiles/" + pr_f[-1]]}
+
+
 def cpu_threads(requested: int) -> dict:
     """Threads for the CPU baseline: the CPUs this process may run on (sched_getaffinity),
     capped by OMP_NUM_THREADS when the environment sets it (the GPU box's CPU share)."""
@@ -387,13 +412,23 @@ def main():
     pmc = _profile("verify_each_pmc")
     if args.mode == "each":
         achieved = (mads * n / span_s) / 1e12 if span_s else None
+        kc = mad_peak_at_kernel_clock(oc)
+        peak_k = kc["peak"] if kc else peak_mad
         roofline = {
             "kernel": "k_verify_each",
             "bound": "valu-int",
             "achieved": achieved,
-            "peak": peak_mad / 1e12,
+            "peak": peak_k / 1e12,
             "unit": "Tmad/s",
-            "frac": (achieved / (peak_mad / 1e12)) if achieved else None,
+            "frac": (achieved / (peak_k / 1e12)) if achieved else None,
+            "peak_clock_ghz": kc["clock_ghz"] if kc else None,
+            "peak_basis": ("v_mad_i64_i32 issue rate %.2f lanes / SIMD cycle (best of the clock_rates sweep, %s "
+                           "waves/SIMD) x 1024 SIMDs x the kernel's own shader clock %.3f GHz (in-kernel probe)"
+                           % (kc["lanes_per_simd_cycle"], kc["best_waves_per_simd"], kc["clock_ghz"])) if kc else
+                          "v_mad_i64_i32 rate measured by the clock_rates sweep",
+            "peak_sources": kc["sources"] if kc else None,
+            "peak_at_ubench_clock": peak_mad / 1e12,
+            "frac_vs_peak_at_ubench_clock": (achieved / (peak_mad / 1e12)) if achieved else None,
             "traffic": pmc.get("hbm_bytes_per_launch"),
             "traffic_per_proof": pmc.get("hbm_bytes_per_proof"),
             "traffic_source": pmc.get("source"),

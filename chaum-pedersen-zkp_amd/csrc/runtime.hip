@@ -979,9 +979,9 @@ int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, uin
   std::vector<uint32_t> blocks;
   for (int64_t b = 0; b < nblk; b++)
     if (dirty[(size_t)b]) blocks.push_back((uint32_t)b);
-  ctx->fb_stats[1] = (uint64_t)nblk;
-  ctx->fb_stats[2] = blocks.size();
-  ctx->fb_stats[3] = std::min<uint64_t>((uint64_t)blocks.size() * cpz::kPartProofs, (uint64_t)n);
+  ctx->fb_stats[2] = (uint64_t)nblk;
+  ctx->fb_stats[3] = blocks.size();
+  for (uint32_t b : blocks) ctx->fb_stats[4] += (uint64_t)std::min<int64_t>(cpz::kPartProofs, n - (int64_t)b * cpz::kPartProofs);
   if (blocks.empty()) return CPZ_OK;
   CPZ_HIP(hipMemcpyAsync(ctx->pt_blocks.p, blocks.data(), blocks.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   StageTimer span(ctx, 4, st);  // wall time of the per-proof pass; launches timed as verify_each
@@ -1032,7 +1032,6 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
       uint8_t part[32];
       int ident = 0;
       if ((rc = part_fallback(ctx, (int64_t)n, s, d_status, part, &ident, st))) return rc;
-      ctx->fb_stats[4] = ctx->fb_stats[3];
       if (partial_out) std::memcpy(partial_out, part, 32);
       if (batch_ok) *batch_ok = 0;  // the probe saw invalid entries
       if (host_status) {

@@ -5,12 +5,17 @@
 set -o pipefail
 export PYTHONDONTWRITEBYTECODE=1
 mkdir -p gpurun_out
-steps=${STEPS:-"tests smoke clock probe bench"}
+steps=${STEPS:-"quick tests smoke clock probe sq bench"}
 for s in $steps; do
   case $s in
     tests) echo "== pytest -m gpu ${TESTS:-tests}"
       timeout -k 10 1100 python -u -m pytest ${TESTS:-tests} -x -v -m gpu --timeout 400 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?
       grep -E "PASSED|FAILED|ERROR" gpurun_out/gpu_tests.log | tail -80; tail -5 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc ;;
+    quick) echo "== quick: ${QUICK:-tests/test_gpu_scale.py::test_partitioned_fallback_at_c5_density}"
+      timeout -k 10 600 python -u -m pytest ${QUICK:-tests/test_gpu_scale.py::test_partitioned_fallback_at_c5_density} -x -v --timeout 300 --timeout-method thread > gpurun_out/quick.log 2>&1; rc=$?
+      grep -E "PASSED|FAILED|ERROR|assert|Error" gpurun_out/quick.log | tail -30; [ $rc -eq 0 ] || exit $rc ;;
+    sq) echo "== sq_radix"
+      timeout -k 10 120 tools/ubench/sq_radix > gpurun_out/sq_radix.json 2> gpurun_out/sq_radix.err; rc=$?; cat gpurun_out/sq_radix.json; [ $rc -eq 0 ] || exit $rc ;;
     smoke) echo "== smoke"
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; tail -3 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc ;;
     clock) echo "== clock_rates"

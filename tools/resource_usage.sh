@@ -4,7 +4,7 @@
 # Extra -D flags (a tuning variant) can be passed as arguments.
 set -euo pipefail
 cd "$(dirname "$0")/../chaum-pedersen-zkp_amd/csrc"
-for u in kernels.hip rlc.hip; do
+for u in kernels.hip rlc.hip part.hip; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I . -I ../../include "$@" \
     --cuda-device-only -c "$u" -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 |
     grep -E "remark: (Function Name|    (TotalSGPRs|VGPRs|AGPRs|ScratchSize|Occupancy|SGPRs Spill|VGPRs Spill|LDS Size))" || true
