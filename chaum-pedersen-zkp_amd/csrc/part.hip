@@ -15,10 +15,12 @@
 // 32 windows of 128 buckets.
 //   k_part_sort     1 workgroup / block: LDS counting sort of the block's entries by (window,
 //                   bucket) -> a list of 16-bit point ids and per-window bucket offsets.
-//   k_part_acc      1 wave / block; lane (p, h) owns buckets 32h+1 .. 32h+32 of windows p and
-//                   p + 16 and walks their entries from the lowest bucket up with the running-sum
-//                   reduction: run += entry point, and at each bucket boundary acc += run, so
-//                   run = sum_d B_d and acc = sum_d (32h + 33 - d) B_d without storing a bucket.
+//   k_part_acc      1 wave / block; lane (p, h) owns buckets Wh+1 .. Wh+W of windows p and
+//                   p + 16 (W = 32; W = 8 in the top window, whose digits are <= 32: see
+//                   kPartTopBuckets) and walks their entries from the lowest bucket up with the
+//                   running-sum reduction: run += entry point, and at each bucket boundary
+//                   acc += run, so run = sum_d B_d and acc = sum_d (Wh + W + 1 - d) B_d without
+//                   storing a bucket.
 //                   Both kinds of step are the same extended + cached addition on selected
 //                   operands, so lanes at different buckets never diverge.
 //   k_part_combine  1 quad / block (16 blocks per wave): T_v = sum_d d B_d from the four lanes'
@@ -39,6 +41,14 @@ __device__ __forceinline__ void split8(int d, int& lo, int& hi) {
   hi = (d - lo) >> 8;
 }
 
+// Buckets per lane of window v's walk: 32 (a quarter of the 128), except in the top window.
+// Its 8-bit digits are the high halves of radix-2^16 digit 15 of scalars < 2^253 (weights,
+// a c, b c and the block sums are reduced mod l), which lies in [0, 2^13]: so they are in
+// [0, 32], all in the first quarter -- a fixed 32-bucket split left one lane walking the whole
+// window (512 entries) while the other 63 walked ~160, and doubled the kernel's time.  With 8
+// buckets per lane the window's four lanes share them.
+__device__ __forceinline__ int part_width(int v) { return v == kPartWindows - 1 ? kPartTopBuckets / kPartQuarters : 32; }
+
 __device__ __forceinline__ int digit16(const uint2& g, int q) {
   const uint32_t w = q < 2 ? g.x : g.y;
   return (int)(int16_t)(uint16_t)(w >> (16 * (q & 1)));
@@ -52,9 +62,11 @@ __global__ void __launch_bounds__(256) k_part_sort(PartArgs a) {
   __shared__ uint32_t cur[kPartWindows][kPartBuckets];
   __shared__ uint32_t wtot[kPartWindows];
   __shared__ uint32_t wbase[kPartWindows + 1];
+  __shared__ uint32_t top_over;
   const int64_t b = blockIdx.x, gb = a.blk0 + b;
   const int t = threadIdx.x;
   for (int i = t; i < kPartWindows * kPartBuckets; i += 256) (&cur[0][0])[i] = 0;
+  if (t == 0) top_over = 0;
   const int64_t pi = kPartProofs * gb + t;
   const int64_t j0 = 4 * pi;
   const bool in = pi < a.n;  // past the batch's end (last block): no entries
@@ -82,6 +94,13 @@ __global__ void __launch_bounds__(256) k_part_sort(PartArgs a) {
     }
   }
   __syncthreads();
+  // The top window's walk covers buckets 1 .. kPartTopBuckets only (k_part_acc).  Its digits
+  // never exceed that (kPartTopBuckets); should one ever do, the block is marked failing
+  // here, so that it is verified per proof instead of being judged on a partial that would
+  // miss the entry (k_part_combine ORs its identity test into this flag).
+  if (t >= kPartTopBuckets && t < kPartBuckets && cur[kPartWindows - 1][t] != 0) top_over = 1;
+  __syncthreads();
+  if (t == 0) a.fail[gb] = top_over ? 1 : 0;
   // exclusive scan of each window's 128 counts: wave wv takes windows wv, wv + 4, ...; lane l
   // buckets 2l and 2l + 1
   {
@@ -151,25 +170,36 @@ __device__ __forceinline__ ge_p3 p3_select(const ge_p3& x, const ge_p3& y, bool 
   return r;
 }
 
-// One step of the running-sum walk: entry (run += q) or bucket boundary (acc += run), as one
-// extended + cached addition on selected operands (9 M either way).
-__device__ __forceinline__ void part_step(ge_p3& run, ge_p3& acc, bool entry, const ge_niels& q) {
-  ge_cached c;
-  const fe t2d = fe_mul(run.T, FE_D2());
-  c.YpX = fe_select(fe_add(run.Y, run.X), q.ypx, entry);
-  c.YmX = fe_select(fe_sub(run.Y, run.X), q.ymx, entry);
-  c.Z = fe_select(run.Z, fe_one(), entry);
-  c.T2d = fe_select(t2d, q.xy2d, entry);
-  const ge_p3 r = p1p1_to_p3(ge_add_cached(p3_select(acc, run, entry), c));
+// One step of the running-sum walk, as one addition on selected operands: entry (run += q,
+// q an affine Niels point) or bucket boundary (acc += run).  run is always the extended
+// operand and acc is kept in cached form, so the only selected input is the cached operand
+// (q with Z = 1, or acc); the result is run's new value or, in cached form, acc's.
+// 9 M either way (4 + p1p1 -> p3 + acc's 2 d T).
+__device__ __forceinline__ ge_cached cached_select(const ge_cached& x, const ge_cached& y, bool c) {  // c ? y : x
+  ge_cached r;
+  r.YpX = fe_select(x.YpX, y.YpX, c);
+  r.YmX = fe_select(x.YmX, y.YmX, c);
+  r.Z = fe_select(x.Z, y.Z, c);
+  r.T2d = fe_select(x.T2d, y.T2d, c);
+  return r;
+}
+
+__device__ __forceinline__ void part_step(ge_p3& run, ge_cached& acc, bool entry, const ge_niels& q) {
+  ge_cached o;
+  o.YpX = fe_select(acc.YpX, q.ypx, entry);
+  o.YmX = fe_select(acc.YmX, q.ymx, entry);
+  o.Z = fe_select(acc.Z, fe_one(), entry);
+  o.T2d = fe_select(acc.T2d, q.xy2d, entry);
+  const ge_p3 r = p1p1_to_p3(ge_add_cached(run, o));
+  acc = cached_select(p3_to_cached(r), acc, entry);
   run = p3_select(run, r, entry);
-  acc = p3_select(r, acc, entry);
 }
 
 // The next entry's Niels point is brought into the wave's LDS slot by direct-to-LDS loads
 // (gfx950 global_load_lds_dwordx4: lane l's 16-byte vector v lands at slot[v][l]) while the
 // current step's arithmetic runs, so the prefetch costs no VGPRs (the kernel sits at the
-// 256-VGPR budget of 2 waves per SIMD).  Nothing is stored inside the walk, so the vmcnt
-// wait at the top of a step waits for that prefetch (and the id prefetch) only.
+// 256-VGPR budget of 2 waves per SIMD).  The vmcnt wait at the top of a step waits for that
+// prefetch and the id prefetch (and, once per lane, the stores of its first window's sums).
 __device__ __forceinline__ void part_stage(uint4 (*slot)[64], const PartArgs& a, const ge_niels* P, uint32_t id) {
   const uint32_t j = id & 0x7fffu;
   const ge_niels* src = j < 4u * kPartProofs ? P + j : a.tab + (j == 4u * kPartProofs ? 0 : kNielsEntriesRlc);
@@ -178,10 +208,12 @@ __device__ __forceinline__ void part_stage(uint4 (*slot)[64], const PartArgs& a,
   for (int v = 0; v < 8; v++) __builtin_amdgcn_global_load_lds(g + v, &slot[v][0], 16, 0, 0);
 }
 
-// Lane (p, h) walks its quarter of window v's buckets UPWARD (its entries are one contiguous
-// run of the sorted list): run += entry, and at each bucket boundary acc += run, so at the
-// end S = run = sum_d B_d and A = acc = sum_d (32h + 33 - d) B_d; k_part_combine forms
-// sum_d (d - 32h) B_d = 33 S - A.
+// Lane (p, h) walks its share of window p's buckets UPWARD (its entries are one contiguous run
+// of the sorted list), then, without waiting for the other lanes, its share of window p + 16:
+// run += entry, and at each bucket boundary acc += run, so at the end of a window's share
+// S = run = sum_d B_d and A = acc = sum_d (Wh + W + 1 - d) B_d (stored in cached form);
+// k_part_combine forms sum_d (d - Wh) B_d = (W + 1) S - A.  (One walk over both windows: two
+// separate walks made every lane wait for the slowest lane of the first window.)
 __global__ void __launch_bounds__(256, 2) k_part_acc(PartArgs a) {
   __shared__ uint4 stage[4][8][64];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -190,55 +222,66 @@ __global__ void __launch_bounds__(256, 2) k_part_acc(PartArgs a) {
   const int64_t gb = a.blk0 + b;
   const int p = lane >> 2, h = lane & 3;
   const uint16_t* list = a.lists + b * kPartListCap;
+  const uint16_t* ob = a.offs + b * kPartOffs;
   const ge_niels* P = a.pts + (int64_t)4 * kPartProofs * gb;
   ge_p3* ws = a.wsum + b * kPartWsum;
   uint4 (*slot)[64] = stage[wv];
+  int v = p, width = part_width(v), klo = width * h, k = klo;
+  const uint16_t* o = ob + v * (kPartBuckets + 1);
+  uint32_t e = o[k], eend = o[k + 1], elast = o[klo + width];
+  uint32_t cid = e < elast ? list[e] : 0u;
+  uint32_t nid = e + 1 < elast ? list[e + 1] : 0u;
+  if (e < eend) part_stage(slot, a, P, cid);
+  ge_p3 run = ge_identity();
+  ge_cached acc = ge_cached_identity();
 #pragma unroll 1
-  for (int pass = 0; pass < 2; pass++) {
-    const int v = p + 16 * pass;
-    const uint16_t* o = a.offs + b * kPartOffs + v * (kPartBuckets + 1);
-    const int klo = 32 * h;
-    int k = klo;
-    uint32_t e = o[k], eend = o[k + 1];
-    const uint32_t elast = o[klo + 32];
-    uint32_t cid = e < elast ? list[e] : 0u;
-    uint32_t nid = e + 1 < elast ? list[e + 1] : 0u;
-    if (e < eend) part_stage(slot, a, P, cid);
-    ge_p3 run = ge_identity(), acc = ge_identity();
-#pragma unroll 1
-    for (;;) {
-      const bool entry = e < eend;
-      const bool last = !entry && k == klo + 31;
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this step's point (and ids) arrived
-      ge_niels q;
-      uint4* qv = reinterpret_cast<uint4*>(&q);
+  for (;;) {
+    const bool entry = e < eend;
+    const bool wend = !entry && k == klo + width - 1;  // last boundary of this window's share
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this step's point (and ids) arrived
+    ge_niels q;
+    uint4* qv = reinterpret_cast<uint4*>(&q);
 #pragma unroll
-      for (int u = 0; u < 8; u++) qv[u] = slot[u][lane];
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): read before the slot is refilled
-      q = ge_niels_cneg(q, (cid >> 15) != 0);
-      // the next step's position; its point (if it is an entry) staged now
-      uint32_t e2 = e, eend2 = eend;
-      int k2 = k;
-      uint32_t cid2 = cid, nid2 = nid;
-      if (entry) {
-        e2 = e + 1;
-        cid2 = nid;
-        nid2 = e + 2 < elast ? list[e + 2] : 0u;
-      } else if (!last) {
-        k2 = k + 1;
-        eend2 = o[k2 + 1];
-      }
-      if (!last && e2 < eend2) part_stage(slot, a, P, cid2);
-      part_step(run, acc, entry, q);
-      if (last) break;
-      e = e2;
-      eend = eend2;
-      k = k2;
-      cid = cid2;
-      nid = nid2;
+    for (int u = 0; u < 8; u++) qv[u] = slot[u][lane];
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): read before the slot is refilled
+    q = ge_niels_cneg(q, (cid >> 15) != 0);
+    // the next step's position; its point (if it is an entry) staged now
+    uint32_t e2 = e, eend2 = eend;
+    int k2 = k;
+    uint32_t cid2 = cid, nid2 = nid;
+    if (entry) {
+      e2 = e + 1;
+      cid2 = nid;
+      nid2 = e + 2 < elast ? list[e + 2] : 0u;
+    } else if (!wend) {
+      k2 = k + 1;
+      eend2 = o[k2 + 1];
     }
-    store_p3(ws + (v * kPartQuarters + h) * 2, acc);      // A_h = sum (32h + 33 - d) B_d
-    store_p3(ws + (v * kPartQuarters + h) * 2 + 1, run);  // S_h = sum B_d
+    if (!wend && e2 < eend2) part_stage(slot, a, P, cid2);
+    part_step(run, acc, entry, q);
+    if (wend) {
+      store_p3(ws + (v * kPartQuarters + h) * 2, *reinterpret_cast<const ge_p3*>(&acc));  // A_h (cached)
+      store_p3(ws + (v * kPartQuarters + h) * 2 + 1, run);                                // S_h
+      if (v >= 16) break;
+      v += 16;
+      width = part_width(v);
+      klo = width * h;
+      k2 = klo;
+      o = ob + v * (kPartBuckets + 1);
+      e2 = o[k2];
+      eend2 = o[k2 + 1];
+      elast = o[klo + width];
+      cid2 = e2 < elast ? list[e2] : 0u;
+      nid2 = e2 + 1 < elast ? list[e2 + 1] : 0u;
+      if (e2 < eend2) part_stage(slot, a, P, cid2);
+      run = ge_identity();
+      acc = ge_cached_identity();
+    }
+    e = e2;
+    eend = eend2;
+    k = k2;
+    cid = cid2;
+    nid = nid2;
   }
 }
 
@@ -253,18 +296,22 @@ __global__ void __launch_bounds__(64) k_part_combine(PartArgs a) {
   ge_p3 P = ge_identity();
 #pragma unroll 1
   for (int v = kPartWindows - 1; v >= 0; v--) {
-    // T_v = sum_d d B_d = sum_h (33 + 32 h) S_h - A_h = 32 (Stot + Sw) + Stot - Atot with
-    // Stot = sum_h S_h, Sw = S_1 + 2 S_2 + 3 S_3 = U + V + X (U = S_3, V = S_2 + U, X = S_1 + V)
+    // T_v = sum_d d B_d = sum_h (W + 1 + W h) S_h - A_h = W (Stot + Sw) + Stot - Atot with
+    // Stot = sum_h S_h, Sw = S_1 + 2 S_2 + 3 S_3 = U + V + X (U = S_3, V = S_2 + U, X = S_1 + V),
+    // W = part_width(v) a power of two
     const ge_p3* w = ws + v * kPartQuarters * 2;
     const ge_p3 U = load_p3(w + 7);
     const ge_p3 V = ge_add_quad(load_p3(w + 5), U, q);
     const ge_p3 X = ge_add_quad(load_p3(w + 3), V, q);
     const ge_p3 Stot = ge_add_quad(X, load_p3(w + 1), q);
     const ge_p3 Sw = ge_add_quad(ge_add_quad(U, V, q), X, q);
-    ge_p3 At = ge_add_quad(load_p3(w + 0), load_p3(w + 2), q);
-    At = ge_add_quad(At, load_p3(w + 4), q);
-    At = ge_add_quad(At, load_p3(w + 6), q);
-    ge_p3 T = p3_dbl_n_quad(ge_add_quad(Stot, Sw, q), 5, q);
+    ge_p3 At = ge_identity();  // the A_h are stored in cached form
+#pragma unroll 1
+    for (int hh = 0; hh < kPartQuarters; hh++) {
+      const ge_p3 c = load_p3(w + 2 * hh);
+      At = ge_add_quad(At, *reinterpret_cast<const ge_cached*>(&c), q);
+    }
+    ge_p3 T = p3_dbl_n_quad(ge_add_quad(Stot, Sw, q), __builtin_ctz(part_width(v)), q);
     T = ge_add_quad(T, Stot, q);
     T = ge_add_quad(T, ge_neg(At), q);
     if (v == kPartWindows - 1) P = T;
@@ -272,7 +319,7 @@ __global__ void __launch_bounds__(64) k_part_combine(PartArgs a) {
   }
   if (live && q == 0) {
     store_p3(a.part + a.blk0 + b, P);
-    a.fail[a.blk0 + b] = ristretto_is_identity(P) ? 0 : 1;
+    a.fail[a.blk0 + b] = (a.fail[a.blk0 + b] || !ristretto_is_identity(P)) ? 1 : 0;  // k_part_sort's flag
   }
 }
 

@@ -103,6 +103,7 @@ constexpr int kPartPoints = 4 * kPartProofs + 2;      // + g, h with the block's
 constexpr int kPartWindows = 2 * kRlcWindows;         // 32 signed radix-2^8 windows
 constexpr int kPartBuckets = 128;                     // |digit| in [1, 128]
 constexpr int kPartQuarters = 4;                      // lanes per window pair (32 buckets each)
+constexpr int kPartTopBuckets = 32;                   // |digit| bound of the top window (part.hip)
 constexpr int kPartListCap = kPartWindows * kPartPoints;  // sorted entries per block, at most
 constexpr int kPartOffs = kPartWindows * (kPartBuckets + 1);
 constexpr int kPartWsum = kPartWindows * kPartQuarters * 2;  // (W, S) per window and quarter
@@ -120,7 +121,8 @@ struct PartArgs {
   uint16_t* offs;                // [nblk][kPartOffs] bucket starts per window (+ window end)
   ge_p3* wsum;                   // [nblk][kPartWsum]
   ge_p3* part;                   // [blocks] P_b (indexed by the global block)
-  uint8_t* fail;                 // [blocks] 1 iff P_b is not the identity
+  uint8_t* fail;                 // [blocks] 1 iff P_b is not the identity (or a top-window digit
+                                 // exceeded kPartTopBuckets: the block is verified per proof)
 };
 
 hipError_t launch_part_msm(const PartArgs& a, hipStream_t st);
