@@ -15,14 +15,14 @@
 // 32 windows of 128 buckets.
 //   k_part_sort     1 workgroup / block: LDS counting sort of the block's entries by (window,
 //                   bucket) -> a list of 16-bit point ids and per-window bucket offsets.
-//   k_part_acc      1 wave / block; lane (p, h) owns buckets Wh+1 .. Wh+W of windows p and
-//                   p + 16 (W = 32; W = 8 in the top window, whose digits are <= 32: see
-//                   kPartTopBuckets) and walks their entries from the lowest bucket up with the
-//                   running-sum reduction: run += entry point, and at each bucket boundary
-//                   acc += run, so run = sum_d B_d and acc = sum_d (Wh + W + 1 - d) B_d without
-//                   storing a bucket.
-//                   Both kinds of step are the same extended + cached addition on selected
-//                   operands, so lanes at different buckets never diverge.
+//   k_part_acc      1 wave / block; a lane walks two units -- (window v, share h): buckets
+//                   Wh+1 .. Wh+W, W = 32, or 4 in the top window, whose digits are <= 16 (see
+//                   part_width) -- one of windows 0..15 and one of 16..31, paired by size in
+//                   k_part_sort, each from its lowest bucket up with the running-sum
+//                   reduction: run += entry point, and at each bucket boundary acc += run, so
+//                   run = sum_d B_d and acc = sum_d (Wh + W + 1 - d) B_d without storing a
+//                   bucket.  Both kinds of step are the same extended + cached addition on
+//                   selected operands, so lanes at different buckets never diverge.
 //   k_part_combine  1 quad / block (16 blocks per wave): T_v = sum_d d B_d from the four lanes'
 //                   (acc, run), P_b = sum_v 2^(8 v) T_v by Horner, quad-cooperative; P_b and its
 //                   identity flag.
@@ -42,11 +42,13 @@ __device__ __forceinline__ void split8(int d, int& lo, int& hi) {
 }
 
 // Buckets per lane of window v's walk: 32 (a quarter of the 128), except in the top window.
-// Its 8-bit digits are the high halves of radix-2^16 digit 15 of scalars < 2^253 (weights,
-// a c, b c and the block sums are reduced mod l), which lies in [0, 2^13]: so they are in
-// [0, 32], all in the first quarter -- a fixed 32-bucket split left one lane walking the whole
-// window (512 entries) while the other 63 walked ~160, and doubled the kernel's time.  With 8
-// buckets per lane the window's four lanes share them.
+// Its 8-bit digits are the high halves of radix-2^16 digit 15 of scalars < l < 2^252 + 2^125
+// (a c, b c and the block sums are reduced mod l; the weights have no digit 15): digit 15 is
+// s >> 240 <= 4096 plus the carry out of digit 14, so it lies in [0, 4097] and its high half
+// in [0, 16] -- all in the first quarter.  A fixed 32-bucket split left one lane walking the
+// whole window (512 entries) while the other 63 walked ~160 and doubled the kernel's time; 8
+// per lane still left two lanes with ~250 (C5 134 ms for the partials); 4 per lane spreads
+// the window over all four.
 __device__ __forceinline__ int part_width(int v) { return v == kPartWindows - 1 ? kPartTopBuckets / kPartQuarters : 32; }
 
 __device__ __forceinline__ int digit16(const uint2& g, int q) {
@@ -133,6 +135,35 @@ __global__ void __launch_bounds__(256) k_part_sort(PartArgs a) {
     const int v = i / (kPartBuckets + 1), k = i % (kPartBuckets + 1);
     offs[i] = (uint16_t)(k < kPartBuckets ? wbase[v] + cur[v][k] : wbase[v + 1]);
   }
+  // Walk units: (window v, lane share h), 128 per block, 64 in windows 0..15 (the r- and
+  // y-points' low digits: ~288 steps each) and 64 in windows 16..31 (y only: ~160).  Lane r of
+  // k_part_acc walks the r-th largest low unit and then the r-th smallest high unit, so every
+  // lane's total is close to the mean (~445 steps): pairing a fixed p with p + 16 made the
+  // wave wait for its largest binomial sum (~485 in a simulation of the digit distribution).
+  {
+    __shared__ uint32_t usz[2 * kPartUnits];
+    __shared__ uint8_t asg[2][kPartUnits];
+    if (t < 2 * kPartUnits) {
+      const int v = t >> 2, h = t & 3, w = part_width(v);
+      const uint32_t e0 = cur[v][w * h];
+      const uint32_t e1 = w * (h + 1) < kPartBuckets ? cur[v][w * (h + 1)] : wtot[v];
+      usz[t] = e1 - e0 + w;
+    }
+    __syncthreads();
+    if (t < 2 * kPartUnits) {
+      const bool low = t < kPartUnits;
+      const int base = low ? 0 : kPartUnits;
+      const uint32_t me = usz[t];
+      int rank = 0;
+      for (int u = base; u < base + kPartUnits; u++) {  // low: descending, high: ascending
+        const uint32_t o = usz[u];
+        rank += low ? (o > me || (o == me && u < t)) : (o < me || (o == me && u < t));
+      }
+      asg[low ? 0 : 1][rank] = (uint8_t)t;
+    }
+    __syncthreads();
+    if (t < kPartUnits) a.assign[b * kPartUnits + t] = (uint16_t)(asg[0][t] | (asg[1][t] << 8));
+  }
   __syncthreads();
   for (int i = t; i < kPartWindows * kPartBuckets; i += 256) (&cur[0][0])[i] += wbase[i / kPartBuckets];
   __syncthreads();
@@ -170,30 +201,12 @@ __device__ __forceinline__ ge_p3 p3_select(const ge_p3& x, const ge_p3& y, bool 
   return r;
 }
 
-// One step of the running-sum walk, as one addition on selected operands: entry (run += q,
-// q an affine Niels point) or bucket boundary (acc += run).  run is always the extended
-// operand and acc is kept in cached form, so the only selected input is the cached operand
-// (q with Z = 1, or acc); the result is run's new value or, in cached form, acc's.
-// 9 M either way (4 + p1p1 -> p3 + acc's 2 d T).
-__device__ __forceinline__ ge_cached cached_select(const ge_cached& x, const ge_cached& y, bool c) {  // c ? y : x
-  ge_cached r;
-  r.YpX = fe_select(x.YpX, y.YpX, c);
-  r.YmX = fe_select(x.YmX, y.YmX, c);
-  r.Z = fe_select(x.Z, y.Z, c);
-  r.T2d = fe_select(x.T2d, y.T2d, c);
-  return r;
-}
-
-__device__ __forceinline__ void part_step(ge_p3& run, ge_cached& acc, bool entry, const ge_niels& q) {
-  ge_cached o;
-  o.YpX = fe_select(acc.YpX, q.ypx, entry);
-  o.YmX = fe_select(acc.YmX, q.ymx, entry);
-  o.Z = fe_select(acc.Z, fe_one(), entry);
-  o.T2d = fe_select(acc.T2d, q.xy2d, entry);
-  const ge_p3 r = p1p1_to_p3(ge_add_cached(run, o));
-  acc = cached_select(p3_to_cached(r), acc, entry);
-  run = p3_select(run, r, entry);
-}
+// One step of the running-sum walk is one addition: entry (run += q, q an affine Niels point)
+// or bucket boundary (acc += run).  run is always the extended operand; the cached operand is
+// read from the lane's stage slot (q, Z = 1) or its acc slot, a per-lane LDS index, and a
+// boundary writes acc back (cached form) under its lane mask: 9 M either way (4 + p1p1 -> p3 +
+// acc's 2 d T), with no operand or result selects but run's.  (acc in registers, selected by
+// v_cndmask: 233 -> 241 ms for C5, msm 109 -> 118 ms, A/B.)
 
 // The next entry's Niels point is brought into the wave's LDS slot by direct-to-LDS loads
 // (gfx950 global_load_lds_dwordx4: lane l's 16-byte vector v lands at slot[v][l]) while the
@@ -208,32 +221,82 @@ __device__ __forceinline__ void part_stage(uint4 (*slot)[64], const PartArgs& a,
   for (int v = 0; v < 8; v++) __builtin_amdgcn_global_load_lds(g + v, &slot[v][0], 16, 0, 0);
 }
 
-// Lane (p, h) walks its share of window p's buckets UPWARD (its entries are one contiguous run
-// of the sorted list), then, without waiting for the other lanes, its share of window p + 16:
+// A lane walks one unit (window v, share h) of windows 0..15 and one of windows 16..31, as
+// k_part_sort paired them (a.assign), each UPWARD through its buckets (its entries are one
+// contiguous run of the sorted list), the second without waiting for the other lanes:
 // run += entry, and at each bucket boundary acc += run, so at the end of a window's share
 // S = run = sum_d B_d and A = acc = sum_d (Wh + W + 1 - d) B_d (stored in cached form);
 // k_part_combine forms sum_d (d - Wh) B_d = (W + 1) S - A.  (One walk over both windows: two
-// separate walks made every lane wait for the slowest lane of the first window.)
+// separate walks made every lane wait for the slowest lane of the first window.)  76 KB of
+// LDS per block of 4 waves: per wave the staged point and acc (below).
+//
+// acc's slots in LDS, written and read limb by limb (no local array is address-taken, so
+// nothing goes to scratch): an = (Y+X, Y-X, 2dT) in the staged points' 8-vector layout, az = Z.
+#define CPZ_LIMB(f, i) ((uint32_t)(f).v[i])
+__device__ __forceinline__ uint32_t limb30(const ge_cached& c, int i) {  // word i of (Y+X, Y-X, 2dT, 0, 0)
+  return i < 10 ? CPZ_LIMB(c.YpX, i) : i < 20 ? CPZ_LIMB(c.YmX, i - 10) : i < 30 ? CPZ_LIMB(c.T2d, i - 20) : 0u;
+}
+__device__ __forceinline__ void acc_store(uint4 (*an)[64], uint4 (*az)[64], int lane, const ge_cached& c) {
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    an[k][lane] = make_uint4(limb30(c, 4 * k), limb30(c, 4 * k + 1), limb30(c, 4 * k + 2), limb30(c, 4 * k + 3));
+  az[0][lane] = make_uint4(CPZ_LIMB(c.Z, 0), CPZ_LIMB(c.Z, 1), CPZ_LIMB(c.Z, 2), CPZ_LIMB(c.Z, 3));
+  az[1][lane] = make_uint4(CPZ_LIMB(c.Z, 4), CPZ_LIMB(c.Z, 5), CPZ_LIMB(c.Z, 6), CPZ_LIMB(c.Z, 7));
+  az[2][lane] = make_uint4(CPZ_LIMB(c.Z, 8), CPZ_LIMB(c.Z, 9), 0u, 0u);
+}
+#undef CPZ_LIMB
+__device__ __forceinline__ fe acc_load_z(uint4 (*az)[64], int lane) {
+  const uint4 a = az[0][lane], b = az[1][lane], c = az[2][lane];
+  fe r;
+  r.v[0] = (int32_t)a.x; r.v[1] = (int32_t)a.y; r.v[2] = (int32_t)a.z; r.v[3] = (int32_t)a.w;
+  r.v[4] = (int32_t)b.x; r.v[5] = (int32_t)b.y; r.v[6] = (int32_t)b.z; r.v[7] = (int32_t)b.w;
+  r.v[8] = (int32_t)c.x; r.v[9] = (int32_t)c.y;
+  return r;
+}
+
 __global__ void __launch_bounds__(256, 2) k_part_acc(PartArgs a) {
-  __shared__ uint4 stage[4][8][64];
+  __shared__ uint4 lds[4][19][64];  // per wave: staged point (0..7), acc (8..15), acc's Z (16..18)
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + wv;
   if (b >= a.nblk) return;  // whole waves
   const int64_t gb = a.blk0 + b;
-  const int p = lane >> 2, h = lane & 3;
+  const uint32_t units = a.assign[b * kPartUnits + lane];  // (low unit, high unit), k_part_sort
+  int v = (units & 0xff) >> 2, h = units & 3;
   const uint16_t* list = a.lists + b * kPartListCap;
   const uint16_t* ob = a.offs + b * kPartOffs;
   const ge_niels* P = a.pts + (int64_t)4 * kPartProofs * gb;
   ge_p3* ws = a.wsum + b * kPartWsum;
-  uint4 (*slot)[64] = stage[wv];
-  int v = p, width = part_width(v), klo = width * h, k = klo;
+  uint4 (*slot)[64] = lds[wv];
+  int width = part_width(v), klo = width * h, k = klo;
   const uint16_t* o = ob + v * (kPartBuckets + 1);
   uint32_t e = o[k], eend = o[k + 1], elast = o[klo + width];
   uint32_t cid = e < elast ? list[e] : 0u;
   uint32_t nid = e + 1 < elast ? list[e + 1] : 0u;
   if (e < eend) part_stage(slot, a, P, cid);
   ge_p3 run = ge_identity();
-  ge_cached acc = ge_cached_identity();
+  uint4 (*an)[64] = lds[wv] + 8;   // acc's Y+X, Y-X, 2dT (the staged points' layout)
+  uint4 (*az)[64] = lds[wv] + 16;  // acc's Z
+  auto acc_get = [&]() -> ge_cached {
+    uint32_t w[32];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint4 x = an[u][lane];
+      w[4 * u] = x.x;
+      w[4 * u + 1] = x.y;
+      w[4 * u + 2] = x.z;
+      w[4 * u + 3] = x.w;
+    }
+    ge_cached c;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+      c.YpX.v[i] = (int32_t)w[i];
+      c.YmX.v[i] = (int32_t)w[10 + i];
+      c.T2d.v[i] = (int32_t)w[20 + i];
+    }
+    c.Z = acc_load_z(az, lane);
+    return c;
+  };
+  acc_store(an, az, lane, ge_cached_identity());
 #pragma unroll 1
   for (;;) {
     const bool entry = e < eend;
@@ -241,10 +304,14 @@ __global__ void __launch_bounds__(256, 2) k_part_acc(PartArgs a) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this step's point (and ids) arrived
     ge_niels q;
     uint4* qv = reinterpret_cast<uint4*>(&q);
+    // the cached operand: the staged point (vectors 0..7 of the wave's LDS) or acc (8..15),
+    // a per-lane index
+    const int src = entry ? 0 : 8;
 #pragma unroll
-    for (int u = 0; u < 8; u++) qv[u] = slot[u][lane];
+    for (int u = 0; u < 8; u++) qv[u] = lds[wv][src + u][lane];
+    const fe zq = acc_load_z(az, lane);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): read before the slot is refilled
-    q = ge_niels_cneg(q, (cid >> 15) != 0);
+    q = ge_niels_cneg(q, entry && (cid >> 15) != 0);
     // the next step's position; its point (if it is an entry) staged now
     uint32_t e2 = e, eend2 = eend;
     int k2 = k;
@@ -258,12 +325,23 @@ __global__ void __launch_bounds__(256, 2) k_part_acc(PartArgs a) {
       eend2 = o[k2 + 1];
     }
     if (!wend && e2 < eend2) part_stage(slot, a, P, cid2);
-    part_step(run, acc, entry, q);
+    {
+      ge_cached oc;
+      oc.YpX = q.ypx;
+      oc.YmX = q.ymx;
+      oc.T2d = q.xy2d;
+      oc.Z = fe_select(zq, fe_one(), entry);
+      const ge_p3 r = p1p1_to_p3(ge_add_cached(run, oc));
+      if (!entry) acc_store(an, az, lane, p3_to_cached(r));
+      run = p3_select(run, r, entry);
+    }
     if (wend) {
+      const ge_cached acc = acc_get();
       store_p3(ws + (v * kPartQuarters + h) * 2, *reinterpret_cast<const ge_p3*>(&acc));  // A_h (cached)
       store_p3(ws + (v * kPartQuarters + h) * 2 + 1, run);                                // S_h
       if (v >= 16) break;
-      v += 16;
+      v = (units >> 8) >> 2;
+      h = (units >> 8) & 3;
       width = part_width(v);
       klo = width * h;
       k2 = klo;
@@ -275,7 +353,7 @@ __global__ void __launch_bounds__(256, 2) k_part_acc(PartArgs a) {
       nid2 = e2 + 1 < elast ? list[e2 + 1] : 0u;
       if (e2 < eend2) part_stage(slot, a, P, cid2);
       run = ge_identity();
-      acc = ge_cached_identity();
+      acc_store(an, az, lane, ge_cached_identity());
     }
     e = e2;
     eend = eend2;

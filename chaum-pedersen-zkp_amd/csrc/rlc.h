@@ -103,10 +103,11 @@ constexpr int kPartPoints = 4 * kPartProofs + 2;      // + g, h with the block's
 constexpr int kPartWindows = 2 * kRlcWindows;         // 32 signed radix-2^8 windows
 constexpr int kPartBuckets = 128;                     // |digit| in [1, 128]
 constexpr int kPartQuarters = 4;                      // lanes per window pair (32 buckets each)
-constexpr int kPartTopBuckets = 32;                   // |digit| bound of the top window (part.hip)
+constexpr int kPartTopBuckets = 16;                   // |digit| bound of the top window (part.hip)
 constexpr int kPartListCap = kPartWindows * kPartPoints;  // sorted entries per block, at most
 constexpr int kPartOffs = kPartWindows * (kPartBuckets + 1);
 constexpr int kPartWsum = kPartWindows * kPartQuarters * 2;  // (W, S) per window and quarter
+constexpr int kPartUnits = kPartWindows * kPartQuarters / 2;  // walk units per half (64 = lanes)
 
 struct PartArgs {
   int64_t nblk;                  // blocks of this launch: [blk0, blk0 + nblk) of the prepared set
@@ -120,6 +121,7 @@ struct PartArgs {
   uint16_t* lists;               // [nblk][kPartListCap] point ids (bit 15: negate) sorted by (window, bucket)
   uint16_t* offs;                // [nblk][kPartOffs] bucket starts per window (+ window end)
   ge_p3* wsum;                   // [nblk][kPartWsum]
+  uint16_t* assign;              // [nblk][kPartUnits] lane -> (unit of windows 0..15, unit of 16..31)
   ge_p3* part;                   // [blocks] P_b (indexed by the global block)
   uint8_t* fail;                 // [blocks] 1 iff P_b is not the identity (or a top-window digit
                                  // exceeded kPartTopBuckets: the block is verified per proof)

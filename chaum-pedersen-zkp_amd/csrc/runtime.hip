@@ -158,7 +158,7 @@ struct cpz_ctx {
   DevBuf rl_flags, rl_parts;
   // partitioned batch check (part.hip): sorted lists / offsets / window sums of one chunk of
   // blocks, every block's partial and fail flag, the sum's scratch, the failing-block list
-  DevBuf pt_lists, pt_offs, pt_wsum, pt_part, pt_fail, pt_tmp, pt_blocks;
+  DevBuf pt_lists, pt_offs, pt_wsum, pt_part, pt_fail, pt_tmp, pt_blocks, pt_assign;
   // what the last batch call's fallback did (cpz_ctx_fallback_stats)
   uint64_t fb_stats[CPZ_FALLBACK_STATS] = {};
   // commitment checks (statuses 4 and 5: the Proof::from_bytes rejections); off = equations only
@@ -939,6 +939,7 @@ int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, uin
   const int64_t nblk = (n + cpz::kPartProofs - 1) / cpz::kPartProofs;
   const int64_t chunk = std::min<int64_t>(nblk, kPartChunkBlocks);
   CPZ_HIP(ctx->pt_lists.ensure((size_t)chunk * cpz::kPartListCap * sizeof(uint16_t)));
+  CPZ_HIP(ctx->pt_assign.ensure((size_t)chunk * cpz::kPartUnits * sizeof(uint16_t)));
   CPZ_HIP(ctx->pt_offs.ensure((size_t)chunk * cpz::kPartOffs * sizeof(uint16_t)));
   CPZ_HIP(ctx->pt_wsum.ensure((size_t)chunk * cpz::kPartWsum * sizeof(cpz::ge_p3)));
   CPZ_HIP(ctx->pt_part.ensure((size_t)nblk * sizeof(cpz::ge_p3)));
@@ -956,6 +957,7 @@ int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, uin
     pa.block_sums = static_cast<const cpz::sc*>(ctx->rl_prep.bsum.p);
     pa.tab = static_cast<const cpz::ge_niels*>(ctx->tab.p);
     pa.lists = static_cast<uint16_t*>(ctx->pt_lists.p);
+    pa.assign = static_cast<uint16_t*>(ctx->pt_assign.p);
     pa.offs = static_cast<uint16_t*>(ctx->pt_offs.p);
     pa.wsum = static_cast<cpz::ge_p3*>(ctx->pt_wsum.p);
     pa.part = static_cast<cpz::ge_p3*>(ctx->pt_part.p);
@@ -1514,7 +1516,7 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->rl_prep.release();
   ctx->rl_msm.release();
   for (DevBuf* b : {&ctx->pt_lists, &ctx->pt_offs, &ctx->pt_wsum, &ctx->pt_part, &ctx->pt_fail, &ctx->pt_tmp,
-                    &ctx->pt_blocks})
+                    &ctx->pt_blocks, &ctx->pt_assign})
     b->release();
   ctx->rl_flags.release();
   ctx->rl_parts.release();
