@@ -69,28 +69,13 @@ struct RlcMsmArgs {
   ge_p3* seg_s;                  // [16][2^15 / kRlcSegLen]
   ge_p3* seg_w;                  // [16][2^15 / kRlcSegLen]
   ge_p3* win;                    // [16]
-  ge_p3* acc;                    // 1: the window groups' running combination (pipelined tails)
   uint32_t* partial_out;         // 8 words
   int* identity_out;             // 1
-  int w0 = 0, w1 = kRlcWindows;  // windows of this launch (bucket / fix / segment / window / final)
   // A batch verified as several MSMs over consecutive proof spans: the final of each span
   // adds its P into *total (the first span stores it), and only the last span encodes --
   // the sum -- into partial_out / identity_out.  total == nullptr: a single MSM.
   ge_p3* total = nullptr;
   int total_first = 1, total_last = 1;
-};
-
-// Pipelined tails: the windows are cut into `groups` groups (a power of two <= 16); the
-// buckets of the top group are accumulated first, and while the next group's buckets run on
-// the launch stream, the finished group's fix-up, reductions and its share of the 2^(16 w)
-// combination run on `side` (each group's combination needs the one above it: the doubling
-// chain of the top windows starts before the low windows' buckets are done).  groups <= 1
-// or side == nullptr: everything on the launch stream.
-struct RlcPipe {
-  int groups = 1;
-  hipStream_t side = nullptr;
-  hipEvent_t ev[kRlcWindows] = {};  // bucket group g done (launch stream)
-  hipEvent_t done = nullptr;        // the side stream's work done
 };
 
 // ---- partitioned batch check (part.hip) --------------------------------------------------
@@ -141,7 +126,7 @@ void rlc_sort_geometry(RlcMsmArgs& a, int64_t npts);
 // | final).
 constexpr int kRlcMsmMarks = 6;
 hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0, int64_t b1, const ge_niels* tab,
-                          hipStream_t st, hipEvent_t* marks = nullptr, const RlcPipe* pipe = nullptr);
+                          hipStream_t st, hipEvent_t* marks = nullptr);
 hipError_t launch_msm_load(int64_t n, const uint32_t* pts_enc, const uint32_t* scalars, ge_niels* pts,
                            int16_t* digits, int64_t dstride, int* bad, hipStream_t st);
 hipError_t launch_rlc_combine(const uint32_t* parts, int k, uint32_t* out, int* flags, hipStream_t st);

@@ -523,7 +523,7 @@ __device__ __forceinline__ void stage_point(uint4 (*slot)[64], const ge_niels* s
 
 __global__ void __launch_bounds__(256, 4) k_rlc_bucket(RlcMsmArgs a) {
   __shared__ uint4 stage[4][8][64];
-  const int w = a.w0 + blockIdx.y;
+  const int w = blockIdx.y;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
@@ -580,7 +580,7 @@ __global__ void __launch_bounds__(256, 4) k_rlc_bucket(RlcMsmArgs a) {
 #else
 // (141 VGPRs, 3 waves/SIMD; forcing 4 waves -- 128 VGPRs with spills -- measured 7 % slower)
 __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
-  const int w = a.w0 + blockIdx.y;
+  const int w = blockIdx.y;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
   const uint32_t total = off[kRlcBuckets];
@@ -642,8 +642,8 @@ __device__ __forceinline__ ge_cached load_cached(const ge_cached* src) {
 __global__ void __launch_bounds__(256, CPZ_RLC_FIX_WAVES) k_rlc_bucket_fix(RlcMsmArgs a) {
   __builtin_amdgcn_s_setprio(3);  // issue ahead of bucket waves sharing the SIMD (pipelined tails)
   const int64_t tl = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (tl >= (int64_t)(a.w1 - a.w0) * kRlcBuckets) return;
-  const int64_t t = tl + (int64_t)a.w0 * kRlcBuckets;
+  if (tl >= (int64_t)kRlcWindows * kRlcBuckets) return;
+  const int64_t t = tl;
   const int w = (int)(t / kRlcBuckets);
   const int b = (int)(t % kRlcBuckets);
   const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
@@ -669,8 +669,8 @@ __global__ void __launch_bounds__(256, 2) k_rlc_segment(RlcMsmArgs a) {
   const int64_t tl = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 2;
   const int q = threadIdx.x & 3;
   constexpr int nseg = kRlcBuckets / kRlcSegLen;
-  if (tl >= (int64_t)(a.w1 - a.w0) * nseg) return;  // whole quads
-  const int64_t t = tl + (int64_t)a.w0 * nseg;
+  if (tl >= (int64_t)kRlcWindows * nseg) return;  // whole quads
+  const int64_t t = tl;
   const int w = (int)(t / nseg);
   const int sg = (int)(t % nseg);
   const ge_cached* B =
@@ -701,7 +701,7 @@ constexpr int kRlcWinQuads = CPZ_RLC_WIN_QUADS;  // 512 threads: 256 VGPRs witho
 __global__ void __launch_bounds__(4 * kRlcWinQuads) k_rlc_window(RlcMsmArgs a) {
   __shared__ ge_p3 lds[kRlcWinQuads], lds_m[kRlcWinQuads], lds_w[kRlcWinQuads];
   __builtin_amdgcn_s_setprio(3);
-  const int w = a.w0 + blockIdx.x;
+  const int w = blockIdx.x;
   const int u = threadIdx.x >> 2, q = threadIdx.x & 3;
   constexpr int nseg = kRlcBuckets / kRlcSegLen;
   constexpr int P = nseg / kRlcWinQuads;
@@ -762,56 +762,42 @@ __global__ void __launch_bounds__(4 * kRlcWinQuads) k_rlc_window(RlcMsmArgs a) {
   }
 }
 
-// P_g = sum_{w in [w0, w1)} 2^(16 (w - w0)) T_w by a tree: quad j of wave 0 owns window
-// w0 + j; at level `span` the active quads double their upper partner 16 span times and add
-// it to their own (16 (nw - 1) doublings deep).  Unless this is the top group, quad 0 of
-// wave 1 meanwhile shifts the groups above, acc, by 2^(16 nw); the sum is the new acc, or,
-// for the bottom group, the batch's partial P = sum_w 2^(16 w) T_w, encoded with its
-// identity flag.  (One group: the whole tree, 240 doublings deep.)
-__global__ void __launch_bounds__(128) k_rlc_final(RlcMsmArgs a, int first, int last) {
-  __shared__ ge_p3 lds[kRlcWindows + 1];
+// P = sum_w 2^(16 w) T_w by a tree on one wave: quad j owns window j; at level `span` the
+// active quads double their upper partner 16 span times and add it to their own (240
+// doublings deep), then the partial is encoded with its identity flag -- or, for one span of
+// a multi-span batch, added into the batch's running total (RlcMsmArgs::total).
+__global__ void __launch_bounds__(64) k_rlc_final(RlcMsmArgs a) {
+  __shared__ ge_p3 lds[kRlcWindows];
   __builtin_amdgcn_s_setprio(3);
-  const int nw = a.w1 - a.w0;
   const int j = threadIdx.x >> 2, q = threadIdx.x & 3;
-  if (threadIdx.x < 64) {
-    if (q == 0 && j < nw) lds[j] = load_p3(a.win + a.w0 + j);
+  if (q == 0) lds[j] = load_p3(a.win + j);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  for (int span = 1; span < kRlcWindows; span <<= 1) {  // one wave: LDS traffic stays in program order
+    if ((j % (2 * span)) == 0) {
+      const ge_p3 lo = ge_add_quad(lds[j], p3_dbl_n_quad(lds[j + span], 16 * span, q), q);
+      if (q == 0) lds[j] = lo;
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    for (int span = 1; span < nw; span <<= 1) {  // one wave: LDS traffic stays in program order
-      const bool active = j < nw && (j % (2 * span)) == 0;
-      if (active) {
-        const ge_p3 lo = ge_add_quad(lds[j], p3_dbl_n_quad(lds[j + span], 16 * span, q), q);
-        if (q == 0) lds[j] = lo;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
-  } else if (threadIdx.x < 68 && !first) {
-    const ge_p3 sh = p3_dbl_n_quad(load_p3(a.acc), 16 * nw, q);
-    if (q == 0) lds[kRlcWindows] = sh;
   }
-  __syncthreads();
-  if (threadIdx.x < 4) {
-    ge_p3 P = lds[0];
-    if (!first) P = ge_add_quad(P, lds[kRlcWindows], q);
-    if (last && a.total) {  // one span of a multi-span batch
-      if (!a.total_first) P = ge_add_quad(load_p3(a.total), P, q);
-      if (!a.total_last) {
-        if (q == 0) store_p3(a.total, P);
-        return;
-      }
+  if (threadIdx.x >= 4) return;
+  ge_p3 P = lds[0];
+  if (a.total) {  // one span of a multi-span batch
+    if (!a.total_first) P = ge_add_quad(load_p3(a.total), P, q);
+    if (!a.total_last) {
+      if (q == 0) store_p3(a.total, P);
+      return;
     }
-    if (!last) {
-      if (q == 0) store_p3(a.acc, P);
-    } else if (q == 0) {
-      // The identity (every valid batch) encodes to 32 zero bytes: only a failing batch pays
-      // for the encoding's inverse square root, one lane's ~30 K instructions (~0.1 ms).
-      const bool id = ristretto_is_identity(P);
-      uint32_t enc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (!id) ristretto_encode(enc, P);
-      for (int k = 0; k < 8; k++) a.partial_out[k] = enc[k];
-      a.identity_out[0] = id ? 1 : 0;
-    }
+  }
+  if (q == 0) {
+    // The identity (every valid batch) encodes to 32 zero bytes: only a failing batch pays
+    // for the encoding's inverse square root, one lane's ~30 K instructions (~0.1 ms).
+    const bool id = ristretto_is_identity(P);
+    uint32_t enc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (!id) ristretto_encode(enc, P);
+    for (int k = 0; k < 8; k++) a.partial_out[k] = enc[k];
+    a.identity_out[0] = id ? 1 : 0;
   }
 }
 
@@ -870,11 +856,9 @@ void rlc_sort_geometry(RlcMsmArgs& a, int64_t npts) {
 }
 
 hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0, int64_t b1, const ge_niels* tab,
-                          hipStream_t st, hipEvent_t* marks, const RlcPipe* pipe) {
+                          hipStream_t st, hipEvent_t* marks) {
   hipError_t e;
-  auto mark = [&](int k, hipStream_t s = nullptr) -> hipError_t {
-    return marks ? hipEventRecord(marks[k], s ? s : st) : hipSuccess;
-  };
+  auto mark = [&](int k) -> hipError_t { return marks ? hipEventRecord(marks[k], st) : hipSuccess; };
   if ((e = mark(0)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_rlc_extra, dim3(1), dim3(256), 0, st, a, block_sums, b0, b1, tab);
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -904,49 +888,20 @@ hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0,
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = mark(1)) != hipSuccess) return e;
   const int64_t chunks = (a.istride + kRlcChunk - 1) / kRlcChunk;  // per window, upper bound
-  auto tails = [&](const RlcMsmArgs& g, int first, int last, hipStream_t s) -> hipError_t {
-    const int nw = g.w1 - g.w0;
-    const int64_t nbg = (int64_t)nw * kRlcBuckets;
-    hipLaunchKernelGGL(k_rlc_bucket_fix, dim3((unsigned)((nbg + 255) / 256)), dim3(256), 0, s, g);
-    hipError_t r = hipGetLastError();
-    if (r != hipSuccess) return r;
-    if (last && (r = mark(3, s)) != hipSuccess) return r;
-    const int64_t ns = (int64_t)nw * (kRlcBuckets / kRlcSegLen);
-    hipLaunchKernelGGL(k_rlc_segment, dim3((unsigned)((4 * ns + 255) / 256)), dim3(256), 0, s, g);  // a quad each
-    if ((r = hipGetLastError()) != hipSuccess) return r;
-    hipLaunchKernelGGL(k_rlc_window, dim3(nw), dim3(4 * kRlcWinQuads), 0, s, g);
-    if ((r = hipGetLastError()) != hipSuccess) return r;
-    if (last && (r = mark(4, s)) != hipSuccess) return r;
-    hipLaunchKernelGGL(k_rlc_final, dim3(1), dim3(128), 0, s, g, first, last);
-    return hipGetLastError();
-  };
-  const int groups = pipe && pipe->side && pipe->groups > 1 ? pipe->groups : 1;
-  const int per = kRlcWindows / groups;
-  if (groups == 1) {
-    hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((chunks + 255) / 256), kRlcWindows), dim3(256), 0, st, a);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = mark(2)) != hipSuccess) return e;
-    if ((e = tails(a, 1, 1, st)) != hipSuccess) return e;
-    return mark(5);
-  }
-  for (int g = groups - 1; g >= 0; g--) {  // top windows first
-    RlcMsmArgs ga = a;
-    ga.w0 = g * per;
-    ga.w1 = ga.w0 + per;
-    hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((chunks + 255) / 256), per), dim3(256), 0, st, ga);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = hipEventRecord(pipe->ev[g], st)) != hipSuccess) return e;
-  }
+  hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((chunks + 255) / 256), kRlcWindows), dim3(256), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = mark(2)) != hipSuccess) return e;
-  for (int g = groups - 1; g >= 0; g--) {
-    RlcMsmArgs ga = a;
-    ga.w0 = g * per;
-    ga.w1 = ga.w0 + per;
-    if ((e = hipStreamWaitEvent(pipe->side, pipe->ev[g], 0)) != hipSuccess) return e;
-    if ((e = tails(ga, g == groups - 1, g == 0, pipe->side)) != hipSuccess) return e;
-  }
-  if ((e = hipEventRecord(pipe->done, pipe->side)) != hipSuccess) return e;
-  if ((e = hipStreamWaitEvent(st, pipe->done, 0)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rlc_bucket_fix, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = mark(3)) != hipSuccess) return e;
+  const int64_t ns = (int64_t)kRlcWindows * (kRlcBuckets / kRlcSegLen);
+  hipLaunchKernelGGL(k_rlc_segment, dim3((unsigned)((4 * ns + 255) / 256)), dim3(256), 0, st, a);  // a quad each
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rlc_window, dim3(kRlcWindows), dim3(4 * kRlcWinQuads), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = mark(4)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rlc_final, dim3(1), dim3(64), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   return mark(5);
 }
 

@@ -96,11 +96,11 @@ struct RlcPrepared {
 };
 
 struct RlcMsmSet {
-  DevBuf counts, offsets, bhist, idx, inter, buckets, heads, segs, segw, win, acc, total, partial, flags;
+  DevBuf counts, offsets, bhist, idx, inter, buckets, heads, segs, segw, win, total, partial, flags;
   int64_t cap = 0;
   void release() {
-    for (DevBuf* b : {&counts, &offsets, &bhist, &idx, &inter, &buckets, &heads, &segs, &segw, &win, &acc, &total,
-                      &partial, &flags})
+    for (DevBuf* b : {&counts, &offsets, &bhist, &idx, &inter, &buckets, &heads, &segs, &segw, &win, &total, &partial,
+                      &flags})
       b->release();
     cap = 0;
   }
@@ -163,8 +163,6 @@ struct cpz_ctx {
   uint64_t fb_stats[CPZ_FALLBACK_STATS] = {};
   // commitment checks (statuses 4 and 5: the Proof::from_bytes rejections); off = equations only
   bool eq_only = false;
-  // pipelined MSM tails (cpz::RlcPipe): a high-priority side stream and its events
-  cpz::RlcPipe rl_pipe;
   // Completion of the last call's work on whatever stream it used: the *_device entry points
   // return without synchronising, and their kernels read context buffers (comb, tab, prefix,
   // c, scratch, RLC buffers) that the next call may rewrite on another stream.
@@ -521,27 +519,6 @@ int stage_inputs(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], int count
 }
 
 // ---- RLC batch path --------------------------------------------------------------------
-#ifndef CPZ_RLC_GROUPS
-#define CPZ_RLC_GROUPS 1  // window groups of the pipelined MSM tails (cpz::RlcPipe); 1 = one stream
-#endif
-
-// The side stream (highest priority) and events of the pipelined tails, created once.
-int rlc_pipe(cpz_ctx* ctx, const cpz::RlcPipe** out) {
-  *out = nullptr;
-  if (CPZ_RLC_GROUPS <= 1) return CPZ_OK;
-  cpz::RlcPipe& p = ctx->rl_pipe;
-  if (!p.side) {
-    int least = 0, greatest = 0;
-    CPZ_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    CPZ_HIP(hipStreamCreateWithPriority(&p.side, hipStreamNonBlocking, greatest));
-    for (int g = 0; g < CPZ_RLC_GROUPS; g++) CPZ_HIP(hipEventCreateWithFlags(&p.ev[g], hipEventDisableTiming));
-    CPZ_HIP(hipEventCreateWithFlags(&p.done, hipEventDisableTiming));
-    p.groups = CPZ_RLC_GROUPS;
-  }
-  *out = &p;
-  return CPZ_OK;
-}
-
 // digits row stride: 4 points per proof + g, h, rounded to 8 so that every window row starts
 // 16-byte aligned (k_rlc_hist reads 8 digits per load)
 int64_t rlc_dstride(int64_t cap) { return (4 * cap + 2 + 7) & ~(int64_t)7; }
@@ -577,7 +554,6 @@ int rlc_reserve_msm(RlcMsmSet& S, int64_t span) {
   CPZ_HIP(S.segs.ensure(sizeof(cpz::ge_p3) * nseg));
   CPZ_HIP(S.segw.ensure(sizeof(cpz::ge_p3) * nseg));
   CPZ_HIP(S.win.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows));
-  CPZ_HIP(S.acc.ensure(sizeof(cpz::ge_p3)));
   CPZ_HIP(S.total.ensure(sizeof(cpz::ge_p3)));
   CPZ_HIP(S.partial.ensure(64));
   CPZ_HIP(S.flags.ensure(4 * sizeof(int)));
@@ -629,7 +605,6 @@ int rlc_msm_args(const RlcPrepared& P, RlcMsmSet& S, int64_t lo, int64_t hi, cpz
   m.seg_s = static_cast<cpz::ge_p3*>(S.segs.p);
   m.seg_w = static_cast<cpz::ge_p3*>(S.segw.p);
   m.win = static_cast<cpz::ge_p3*>(S.win.p);
-  m.acc = static_cast<cpz::ge_p3*>(S.acc.p);
   m.partial_out = static_cast<uint32_t*>(S.partial.p);
   m.identity_out = static_cast<int*>(S.flags.p);
   return CPZ_OK;
@@ -666,10 +641,8 @@ int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t part
     if (!timed)
       for (int k = 0; k < got; k++)
         if (marks[k]) ctx->free_events.push_back(marks[k]);
-    const cpz::RlcPipe* pipe;
-    if (int rc = rlc_pipe(ctx, &pipe)) return rc;
     CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_prep.bsum.p), b0, b1,
-                                static_cast<const cpz::ge_niels*>(ctx->tab.p), st, timed ? marks : nullptr, pipe));
+                                static_cast<const cpz::ge_niels*>(ctx->tab.p), st, timed ? marks : nullptr));
     if (timed)
       for (int k = 0; k + 1 < cpz::kRlcMsmMarks; k++) ctx->marks.push_back({8 + k, marks[k], marks[k + 1]});
   }
@@ -1261,10 +1234,8 @@ int cpz_msm(cpz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalar
                                static_cast<const uint32_t*>(ctx->in[1].p), m.pts, m.digits, m.dstride,
                                static_cast<int*>(ctx->rl_flags.p) + 2, ctx->stream));
   // the extra points (g, h at e0) get zero scalars: empty block range
-  const cpz::RlcPipe* pipe;
-  if ((rc = rlc_pipe(ctx, &pipe))) return rc;
   CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_prep.bsum.p), 0, 0,
-                              static_cast<const cpz::ge_niels*>(ctx->tab.p), ctx->stream, nullptr, pipe));
+                              static_cast<const cpz::ge_niels*>(ctx->tab.p), ctx->stream, nullptr));
   int flags[3];
   CPZ_HIP(hipMemcpyAsync(out, ctx->rl_msm.partial.p, 32, hipMemcpyDeviceToHost, ctx->stream));
   CPZ_HIP(hipMemcpyAsync(flags, ctx->rl_flags.p, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
@@ -1505,13 +1476,6 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->copy_stream);
     (void)hipStreamDestroy(ctx->copy_stream);
   }
-  if (ctx->rl_pipe.side) {
-    (void)hipStreamSynchronize(ctx->rl_pipe.side);
-    (void)hipStreamDestroy(ctx->rl_pipe.side);
-  }
-  for (auto& e : ctx->rl_pipe.ev)
-    if (e) (void)hipEventDestroy(e);
-  if (ctx->rl_pipe.done) (void)hipEventDestroy(ctx->rl_pipe.done);
   for (DevBuf* b : {&ctx->pz_blob, &ctx->pz_off, &ctx->pz_rows, &ctx->pz_code, &ctx->pz_aux}) b->release();
   ctx->rl_prep.release();
   ctx->rl_msm.release();
