@@ -68,6 +68,26 @@ struct DevBuf {
   }
 };
 
+// A stream on a hardware queue of its own.  HIP maps plain streams onto at most
+// GPU_MAX_HW_QUEUES (4 by default) queues per process, reusing the least-used one beyond that,
+// and two streams on one queue run one after the other: two torch streams created after the
+// contexts' streams shared a queue (rocprofv3 Queue_Id), so the two batch checks issued on
+// them never overlapped (0.996x one in flight, against 1.07x on the contexts' own streams).
+// A stream with a CU mask always gets a queue of its own; the mask here holds every CU, so
+// the verify streams (whose launches must overlap) stay concurrent whatever other streams
+// the process creates.  Such a stream synchronises with the legacy default stream
+// (hipStreamDefault semantics), which only adds ordering.
+hipError_t stream_own_queue(hipStream_t* s, int cus) {
+  std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+  for (int c = 0; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
+  hipError_t e = hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    e = hipStreamCreateWithFlags(s, hipStreamDefault);
+  }
+  return e;
+}
+
 // Host-buffer pipeline chunk (proofs): 2^17 proofs = 20 MiB of inputs, ~2.8 ms of verify work.
 constexpr size_t kPipeChunk = size_t(1) << 17;
 
@@ -366,7 +386,7 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
     if (!ctx->aux_start) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_start, hipEventDisableTiming));
     CPZ_HIP(hipEventRecord(ctx->aux_start, st));  // the aux streams start after st's prior work
     for (int k = 0; k < nst - 1; k++) {
-      if (!ctx->aux_stream[k]) CPZ_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[k], hipStreamNonBlocking));
+      if (!ctx->aux_stream[k]) CPZ_HIP(stream_own_queue(&ctx->aux_stream[k], ctx->cus));
       if (!ctx->aux_done[k]) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_done[k], hipEventDisableTiming));
       CPZ_HIP(hipStreamWaitEvent(ctx->aux_stream[k], ctx->aux_start, 0));
     }
@@ -823,7 +843,7 @@ int launch_probe(cpz_ctx* ctx, size_t n, const void* const rows[5], int64_t star
   const int64_t blk = cpz::kRlcPrepBlock;
   const size_t m = (size_t)kProbeChunks * blk;
   CPZ_HIP(ctx->probe.ensure(m * (5 * 32 + 32 + 1)));
-  if (!ctx->probe_stream) CPZ_HIP(hipStreamCreateWithFlags(&ctx->probe_stream, hipStreamNonBlocking));
+  if (!ctx->probe_stream) CPZ_HIP(stream_own_queue(&ctx->probe_stream, ctx->cus));
   if (!ctx->probe_done) CPZ_HIP(hipEventCreateWithFlags(&ctx->probe_done, hipEventDisableTiming));
   if (!ctx->aux_start) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_start, hipEventDisableTiming));
   CPZ_HIP(hipEventRecord(ctx->aux_start, st));  // after everything before this call on st
@@ -863,7 +883,7 @@ int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* stat
     if (!ctx->aux_start) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_start, hipEventDisableTiming));
     CPZ_HIP(hipEventRecord(ctx->aux_start, st));
     for (int k = 0; k < nst - 1; k++) {
-      if (!ctx->aux_stream[k]) CPZ_HIP(hipStreamCreateWithFlags(&ctx->aux_stream[k], hipStreamNonBlocking));
+      if (!ctx->aux_stream[k]) CPZ_HIP(stream_own_queue(&ctx->aux_stream[k], ctx->cus));
       if (!ctx->aux_done[k]) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_done[k], hipEventDisableTiming));
       CPZ_HIP(hipStreamWaitEvent(ctx->aux_stream[k], ctx->aux_start, 0));
     }
@@ -1105,7 +1125,7 @@ int ctx_create(int device_ordinal, cpz_ctx** out) {
   // A blocking stream: it orders with the legacy default stream, so work queued by other
   // libraries (e.g. torch's default stream, handle 0, which the C ABI reads as "use the
   // context stream") is ordered with the verifier's kernels in both directions.
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault);
+  if (e == hipSuccess) e = stream_own_queue(&ctx->stream, prop.multiProcessorCount);
   if (e != hipSuccess) {
     delete ctx;
     return fail(CPZ_EHIP, std::string("context setup: ") + hipGetErrorString(e));
@@ -1509,7 +1529,7 @@ int verify_each_pipelined(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], 
   CPZ_HIP(ctx->st.ensure(n));
   CPZ_HIP(ctx->c.ensure(n * 32));  // each chunk's challenges at its own offset
   VerifyRR rr;
-  if (!ctx->copy_stream) CPZ_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+  if (!ctx->copy_stream) CPZ_HIP(stream_own_queue(&ctx->copy_stream, ctx->cus));
   if (!ctx->copy_done) CPZ_HIP(hipEventCreateWithFlags(&ctx->copy_done, hipEventDisableTiming));
   uint8_t* st = static_cast<uint8_t*>(ctx->st.p);
   for (size_t off = 0; off < n; off += kPipeChunk) {

@@ -2,9 +2,10 @@
 
 One in flight: STEPS calls of cpz_verify_batch_device on one context, back to back (what the
 bench's `rlc` line times).  Two in flight: two contexts, each driven by its own host thread on
-its own stream, STEPS calls each -- independent batches, as a verifier service would run them --
-so that one batch's latency-bound tails (bucket fix-up, reductions, the 240-doubling final) and
-memory-bound sort can run beside the other batch's VALU-bound prepare and buckets.  Prints one
+its own stream (the context's own, on its own hardware queue), STEPS calls each -- independent
+batches, as a verifier service would run them -- so that one batch's latency-bound tails (bucket
+fix-up, reductions, the 240-doubling final) and memory-bound sort can run beside the other
+batch's VALU-bound prepare and buckets.  Prints one
 JSON line: proofs/s of each mode over all the batches it checked (every batch must pass)."""
 import json
 import os
@@ -30,13 +31,15 @@ def main():
     gpus[0].prove_synthetic_device(n, bench.SEED_X, bench.SEED_K, t["y1"], t["y2"], t["r1"], t["r2"], t["s"])
     torch.cuda.synchronize(dev)
     rows = [t[k] for k in ("y1", "y2", "r1", "r2", "s")]
-    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    # each context on its own stream (the context's, unless TORCH_STREAMS=1 asks for torch streams)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)] if os.environ.get("TORCH_STREAMS") == "1" else [None, None]
     status = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(2)]
     bad = []
 
     def run(k, count):
         for _ in range(count):
-            _, ok = gpus[k].verify_batch_device(*rows, status[k], bench.WEIGHT_SEED, stream=streams[k].cuda_stream)
+            st = streams[k].cuda_stream if streams[k] is not None else None
+            _, ok = gpus[k].verify_batch_device(*rows, status[k], bench.WEIGHT_SEED, stream=st)
             if not ok:
                 bad.append(k)
 
