@@ -153,6 +153,43 @@ def rlc_roofline(stages, n, steps, oc):
     return out
 
 
+def rlc_two_in_flight(cp, gpu, t, n, steps, device, first_index):
+    """Service-style throughput of the batch check: two contexts on one GPU, each driven by its
+    own host thread on its own stream (each context's stream has a hardware queue of its own),
+    `steps` independent batch checks each.  One batch's latency-bound tails and memory-bound
+    sort then run beside the other's VALU-bound prepare and buckets.  Every batch must pass."""
+    import threading
+
+    import torch
+    gpus = [gpu, cp.Gpu(device)]
+    status = [torch.empty(n, dtype=torch.uint8, device=t["s"].device) for _ in range(2)]
+    bad = []
+
+    def run(k, count):
+        for _ in range(count):
+            _, ok = gpus[k].verify_batch_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status[k], WEIGHT_SEED,
+                                                first_index=first_index, stream=0)
+            if not ok:
+                bad.append(k)
+
+    run(1, 2)  # the second context's tables and buffers
+    torch.cuda.synchronize()
+    th = [threading.Thread(target=run, args=(k, steps)) for k in range(2)]
+    t0 = time.perf_counter()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    gpus[1].close()
+    if bad or any(int((st != 0).sum().item()) for st in status):
+        raise SystemExit("bench: a batch check in flight rejected a valid batch")
+    return {"batches": 2 * steps, "proofs_per_s": 2 * n * steps / el, "ms_per_batch": el * 1e3 / (2 * steps),
+            "how": "two contexts, two host threads, each context on its own stream / hardware queue "
+                   "(tools/rlc_inflight.py); not the line's value"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -296,7 +333,8 @@ def main():
             raise SystemExit("bench: RLC batch check rejected a valid batch")
         rlc_extra = {"workload": "configs[2]: RLC batch check of the same 2^20 proofs (Pippenger, 16-bit windows)",
                      "proofs_per_s": n * args.steps / r_el, "ms_per_step": r_el * 1e3 / args.steps,
-                     "roofline": rlc_roofline(r_st, n, args.steps, oc)}
+                     "roofline": rlc_roofline(r_st, n, args.steps, oc),
+                     "two_in_flight": rlc_two_in_flight(cp, gpu, t, n, args.steps, local_rank, lo)}
 
     c5 = None
     if args.mode == "each" and solo and args.extras and args.c5_n:
