@@ -212,6 +212,9 @@ def main():
     ap.add_argument("--extras", type=int, default=1,
                     help="at N=1 in 'each' mode also measure the RLC check, C5, the prover and the host path")
     ap.add_argument("--rlc-extra", type=int, default=None, help="override --extras for the RLC extra")
+    ap.add_argument("--rlc-inflight", type=int, default=1,
+                    help="add the two-batches-in-flight figure to the RLC extra (0: one batch at a time only, "
+                         "e.g. under a profiler whose per-kernel averages should not mix the two)")
     ap.add_argument("--host-e2e", type=int, default=None, help="override --extras for the host-buffer extra")
     ap.add_argument("--c5-n", type=int, default=1 << 24, help="configs[4] batch size (0.1 %% forged)")
     ap.add_argument("--backend", default="nccl",
@@ -334,7 +337,8 @@ def main():
         rlc_extra = {"workload": "configs[2]: RLC batch check of the same 2^20 proofs (Pippenger, 16-bit windows)",
                      "proofs_per_s": n * args.steps / r_el, "ms_per_step": r_el * 1e3 / args.steps,
                      "roofline": rlc_roofline(r_st, n, args.steps, oc),
-                     "two_in_flight": rlc_two_in_flight(cp, gpu, t, n, args.steps, local_rank, lo)}
+                     "two_in_flight": (rlc_two_in_flight(cp, gpu, t, n, args.steps, local_rank, lo)
+                                       if args.rlc_inflight else None)}
 
     c5 = None
     if args.mode == "each" and solo and args.extras and args.c5_n:

@@ -10,7 +10,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
-ARGS="--steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --extras 0 --rlc-extra 1 ${BENCH_ARGS}"
+ARGS="--steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --extras 0 --rlc-extra 1 --rlc-inflight 0 ${BENCH_ARGS}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_trace -o run -- python3 bench.py $ARGS > $OUT/prof_trace.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_fetch -o run -- python3 bench.py $ARGS > $OUT/prof_fetch.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_write -o run -- python3 bench.py $ARGS > $OUT/prof_write.log 2>&1 &&
