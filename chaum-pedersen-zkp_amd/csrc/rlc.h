@@ -105,14 +105,15 @@ struct PartArgs {
   const ge_niels* tab;           // g at tab[0], h at tab[kNielsEntriesRlc]
   uint16_t* lists;               // [nblk][kPartListCap] point ids (bit 15: negate) sorted by (window, bucket)
   uint16_t* offs;                // [nblk][kPartOffs] bucket starts per window (+ window end)
-  ge_p3* wsum;                   // [nblk][kPartWsum]
+  ge_p3* wsum;                   // [blocks][kPartWsum] (indexed by the global block)
   uint16_t* assign;              // [nblk][kPartUnits] lane -> (unit of windows 0..15, unit of 16..31)
   ge_p3* part;                   // [blocks] P_b (indexed by the global block)
   uint8_t* fail;                 // [blocks] 1 iff P_b is not the identity (or a top-window digit
                                  // exceeded kPartTopBuckets: the block is verified per proof)
 };
 
-hipError_t launch_part_msm(const PartArgs& a, hipStream_t st);
+hipError_t launch_part_msm(const PartArgs& a, hipStream_t st);      // sort + walk of [blk0, blk0 + nblk)
+hipError_t launch_part_combine(const PartArgs& a, hipStream_t st);  // P_b and fail flags of [blk0, blk0 + nblk)
 // out = sum of part[0 .. nblk) (encoded, identity flag), through the scratch `tmp` of
 // ceil(nblk / 16) ge_p3
 hipError_t launch_part_sum(const ge_p3* part, int64_t nblk, ge_p3* tmp, uint32_t* partial_out, int* identity_out,

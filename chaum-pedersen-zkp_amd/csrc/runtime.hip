@@ -916,8 +916,9 @@ int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* stat
   return CPZ_OK;
 }
 
-// Blocks per launch of the partitioned MSM (bounds its list / window-sum buffers: ~72 KB of
-// lists and offsets and 40 KB of window sums per block).
+// Blocks per launch of the partitioned MSM's sort and walk (bounds its list / offset buffers:
+// ~72 KB per block; the window sums, 40 KB per block, are kept for the whole batch so that one
+// combine launch covers every block).
 constexpr int64_t kPartChunkBlocks = 8192;
 // Density probe outcomes (invalid entries among the kProbeChunks x 256 sampled) for which the
 // partitioned check pays: its MSM costs ~0.3 of per-proof verification per proof, and a block
@@ -934,7 +935,7 @@ int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, uin
   CPZ_HIP(ctx->pt_lists.ensure((size_t)chunk * cpz::kPartListCap * sizeof(uint16_t)));
   CPZ_HIP(ctx->pt_assign.ensure((size_t)chunk * cpz::kPartUnits * sizeof(uint16_t)));
   CPZ_HIP(ctx->pt_offs.ensure((size_t)chunk * cpz::kPartOffs * sizeof(uint16_t)));
-  CPZ_HIP(ctx->pt_wsum.ensure((size_t)chunk * cpz::kPartWsum * sizeof(cpz::ge_p3)));
+  CPZ_HIP(ctx->pt_wsum.ensure((size_t)nblk * cpz::kPartWsum * sizeof(cpz::ge_p3)));  // 40 KB per block
   CPZ_HIP(ctx->pt_part.ensure((size_t)nblk * sizeof(cpz::ge_p3)));
   CPZ_HIP(ctx->pt_fail.ensure((size_t)nblk));
   CPZ_HIP(ctx->pt_tmp.ensure((size_t)((nblk + 63) / 64 + 16) * sizeof(cpz::ge_p3)));
@@ -960,6 +961,9 @@ int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, uin
       pa.nblk = std::min<int64_t>(chunk, nblk - b0);
       CPZ_HIP(cpz::launch_part_msm(pa, st));
     }
+    pa.blk0 = 0;
+    pa.nblk = nblk;
+    CPZ_HIP(cpz::launch_part_combine(pa, st));
     CPZ_HIP(cpz::launch_part_sum(pa.part, nblk, static_cast<cpz::ge_p3*>(ctx->pt_tmp.p),
                                  static_cast<uint32_t*>(ctx->rl_msm.partial.p), static_cast<int*>(ctx->rl_msm.flags.p),
                                  st));
