@@ -916,10 +916,11 @@ int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* stat
   return CPZ_OK;
 }
 
-// Blocks per launch of the partitioned MSM's sort and walk (bounds its list / offset buffers:
-// ~72 KB per block; the window sums, 40 KB per block, are kept for the whole batch so that one
-// combine launch covers every block).
-constexpr int64_t kPartChunkBlocks = 8192;
+// Blocks per launch of the partitioned MSM's sort and walk: 2^24 proofs, ~4.8 GB of lists and
+// offsets (~72 KB per block); the window sums, 40 KB per block, are kept for the whole batch so
+// that one combine launch covers every block.  Per 8192 blocks the launch tails cost C5 5 ms
+// (227.9 / 229.5 ms against 223.7 / 223.6 at 65536, 224.6 / 224.9 at 32768; A/B, one call).
+constexpr int64_t kPartChunkBlocks = 65536;
 // Density probe outcomes (invalid entries among the kProbeChunks x 256 sampled) for which the
 // partitioned check pays: its MSM costs ~0.3 of per-proof verification per proof, and a block
 // of 256 is clean with probability (1 - rho)^256; above ~12 sampled (rho > ~0.3 %) more than
