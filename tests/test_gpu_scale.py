@@ -279,3 +279,46 @@ def test_partitioned_fallback_at_c5_density(gpu, n):
     want_pp = sum(min(256, n - 256 * int(b)) for b in dirty)
     assert stats["per_proof"] == want_pp
     assert p == _oracle_partial(host, idx)
+
+
+def test_two_contexts_in_flight_on_one_gpu(gpu):
+    """Two contexts on one GPU, each driven by its own host thread on its own stream (the
+    contexts' streams have hardware queues of their own, so their kernels run concurrently):
+    batch checks of two different batches -- one valid, one with forgeries -- issued back to back
+    from both threads give every call its own batch's result: the valid batch passes with the
+    identity partial, the forged one fails with the oracle's partial of its forged entries and
+    (with the fallback) exactly its forged set.  Guards the per-context buffers and ordering
+    when the two contexts' work overlaps on the device."""
+    import threading
+
+    import chaum_pedersen as cp
+    torch = pytest.importorskip("torch")
+    n = 1 << 18
+    good = _synthetic_device(gpu, torch, n)
+    bad = {k: v.clone() for k, v in good.items()}
+    idx = np.sort(np.random.default_rng(77).choice(n, size=10, replace=False))
+    host = _forge(bad, torch, idx)
+    want = _oracle_partial(host, idx)
+    other = cp.Gpu(0)
+    out = {0: [], 1: []}
+
+    def run(k, g, rows):
+        st = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+        for _ in range(4):
+            p, ok = g.verify_batch_device(*(rows[key] for key in KEYS), st, WSEED, fallback=(k == 1), stream=0)
+            out[k].append((p, ok, st.cpu().numpy().copy()))
+
+    try:
+        th = [threading.Thread(target=run, args=(0, gpu, good)), threading.Thread(target=run, args=(1, other, bad))]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+    finally:
+        other.close()
+    assert len(out[0]) == 4 and len(out[1]) == 4
+    for p, ok, st in out[0]:
+        assert ok and p == bytes(32) and not st.any()
+    for p, ok, st in out[1]:
+        assert not ok and p == want
+        assert np.array_equal(np.nonzero(st)[0], idx) and set(st[idx].tolist()) == {1}
