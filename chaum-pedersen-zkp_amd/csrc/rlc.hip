@@ -640,7 +640,7 @@ __device__ __forceinline__ ge_cached load_cached(const ge_cached* src) {
 #define CPZ_RLC_FIX_WAVES 4
 #endif
 __global__ void __launch_bounds__(256, CPZ_RLC_FIX_WAVES) k_rlc_bucket_fix(RlcMsmArgs a) {
-  __builtin_amdgcn_s_setprio(3);  // issue ahead of bucket waves sharing the SIMD (pipelined tails)
+  __builtin_amdgcn_s_setprio(3);  // tails issue ahead of bucket waves sharing the SIMD (another batch in flight)
   const int64_t tl = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (tl >= (int64_t)kRlcWindows * kRlcBuckets) return;
   const int64_t t = tl;
