@@ -190,6 +190,85 @@ def rlc_two_in_flight(cp, gpu, t, n, steps, device, first_index):
                    "(tools/rlc_inflight.py); not the line's value"}
 
 
+SMALL_SIZES = (1, 2, 5, 10, 20, 50, 100, 1000)
+
+
+def _median_call_ms(fn, budget_s=0.25, min_calls=5, max_calls=200):
+    """Median wall time of synchronous calls of fn (ms), after one untimed call."""
+    fn()
+    times = []
+    stop = time.perf_counter() + budget_s
+    while len(times) < min_calls or (time.perf_counter() < stop and len(times) < max_calls):
+        t0 = time.perf_counter()
+        fn()
+        times.append((time.perf_counter() - t0) * 1e3)
+    times.sort()
+    return times[len(times) // 2], len(times)
+
+
+def small_batch_table(gpu=None, sizes=SMALL_SIZES, stages=False, cpu=True):
+    """The drop-in's own regime: one synchronous BatchVerifier-sized call from pageable host
+    buffers per n (the reference bench's sizes, benches/batch_verification.rs:12-35, plus the
+    cap 1000, batch.rs:48), median wall ms per call, through
+      verify_each   cpz_verify_each (per-proof equations; what gpu.rs runs for n == 1)
+      verify_batch  cpz_verify_batch with statuses (RLC + exact fallback; gpu.rs for n >= 2)
+    beside the C oracle's BatchVerifier::verify on one thread (cpzo_reference_batch_verify: the
+    reference's defective batch equation then per-entry verify_one, oracle/cpz_oracle.c).
+    Valid proofs; a second verify_batch row has one forged entry (its fallback included)."""
+    import numpy as np
+
+    import chaum_pedersen as cp
+    own = gpu is None
+    gpu = gpu or cp.Gpu(0)
+    nmax = max(sizes)
+    rows = gpu.prove_synthetic(nmax, SEED_X, SEED_K)
+    forged = {k: v.copy() for k, v in rows.items()}
+    s0 = (int.from_bytes(forged["s"][0].tobytes(), "little") + 1) % L
+    forged["s"][0] = np.frombuffer(s0.to_bytes(32, "little"), np.uint8)
+    keys = ("y1", "y2", "r1", "r2", "s")
+    out = {"sizes": list(sizes), "unit": "ms per call (median, synchronous, host buffers)", "rows": []}
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import coracle  # CPU baseline only (test infrastructure)
+    for n in sizes:
+        sub = [rows[k][:n] for k in keys]
+        subf = [forged[k][:n] for k in keys]
+        r = {"n": n}
+        r["verify_each_ms"], _ = _median_call_ms(lambda: gpu.verify_each(*sub))
+        st = gpu.verify_each(*sub)
+        assert not st.any(), "small_batch: valid proofs rejected"
+        r["verify_batch_ms"], _ = _median_call_ms(lambda: gpu.verify_batch(*sub, WEIGHT_SEED))
+        _, ok, st = gpu.verify_batch(*sub, WEIGHT_SEED)
+        assert ok and not st.any(), "small_batch: valid batch rejected"
+        if n >= 2:
+            r["verify_batch_one_forged_ms"], _ = _median_call_ms(lambda: gpu.verify_batch(*subf, WEIGHT_SEED))
+            _, ok, st = gpu.verify_batch(*subf, WEIGHT_SEED)
+            assert (not ok) and st[0] == 1 and not st[1:].any(), "small_batch: forged entry not located"
+        if stages:
+            gpu.set_timing(True)
+            gpu.stage_times()
+            gpu.verify_each(*sub)
+            r["verify_each_stages"] = {k: v[0] for k, v in gpu.stage_times().items()}
+            gpu.verify_batch(*sub, WEIGHT_SEED)
+            r["verify_batch_stages"] = {k: v[0] for k, v in gpu.stage_times().items()}
+            gpu.set_timing(False)
+        if cpu:
+            hr = {k: rows[k] for k in keys}
+            r["cpu_batch_verifier_ms"], _ = _median_call_ms(lambda: coracle.reference_batch_verify(hr, 0, n),
+                                                            budget_s=0.5, min_calls=3)
+        best = min(("verify_each", r["verify_each_ms"]), ("verify_batch", r["verify_batch_ms"]), key=lambda x: x[1])
+        r["faster_gpu_entry"] = best[0]
+        if cpu:
+            r["gpu_over_cpu_speedup"] = r["cpu_batch_verifier_ms"] / best[1]
+        out["rows"].append(r)
+    if cpu:
+        out["cpu"] = {"cores": 1, "kind": "port", "what": "cpzo_reference_batch_verify (BatchVerifier::verify "
+                      "semantics: defective equation + per-entry fallback, batch.rs:171-318), one thread"}
+    if own:
+        gpu.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)

@@ -86,10 +86,6 @@ struct VerifyArgs {
   const ge_niels* pre = nullptr; // RLC fallback: the prepared Niels points (-r1, -y1, -r2, -y2 of
                                  // proof i at 4 i ..), reused instead of decoding; entries whose
                                  // decode-level status is non-zero keep it
-  const uint32_t* fused = nullptr;  // non-null: no contexts and the fixed challenge schedule applies;
-                                    // the kernel computes c and the response status itself from these
-                                    // 100 words (prefix ^ k1, then k2: challenge_fixed's constants)
-                                    // instead of reading c / status from k_challenge
   int eq_only = 0;                  // commitment checks off: identity r1 / r2 and zero s are not
                                     // reported, the equations alone decide (verify_proof)
   const uint32_t* blocks = nullptr; // k_verify_prepared: workgroup g verifies the kVerifyBlock
@@ -122,9 +118,6 @@ hipError_t launch_parse_proofs(const ParseArgs& a, hipStream_t st);
 // Fixed-base combs of 2 bases (g, h): bases_scratch holds 2 * kCombWindows ge_p3.
 hipError_t launch_build_comb(const uint32_t* gh_words, ge_p3* bases_scratch, ge_niels* comb, hipStream_t st);
 hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st);
-#if defined(CPZ_VERIFY_DYNAMIC)
-hipError_t launch_verify_each_queue(const VerifyArgs& a, int grid, unsigned* work, hipStream_t st);
-#endif
 int verify_each_blocks_per_cu();  // resident k_verify_each blocks per CU (occupancy API)
 hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st);
 hipError_t launch_prove_response(const ProveArgs& a, hipStream_t st);

@@ -29,15 +29,6 @@
 #define CPZ_HDM inline
 #endif
 
-// Optional scheduling fence between field operations (-DCPZ_SEQ_FENCES): keeps the
-// compiler from interleaving several 20-register column accumulators at once.  Off by
-// default: with the biased single-chain carry the verify kernel fits 256 VGPRs without
-// it, and letting the scheduler interleave independent products measured ~1 % faster.
-#if defined(__HIP_DEVICE_COMPILE__) && defined(CPZ_SEQ_FENCES)
-#define CPZ_SEQ() __builtin_amdgcn_sched_barrier(0)
-#else
-#define CPZ_SEQ() ((void)0)
-#endif
 
 #if defined(CPZ_BOUNDS_CHECK) && !defined(__HIP_DEVICE_COMPILE__)
 #include <stdio.h>
@@ -175,19 +166,15 @@ CPZ_HD int32_t unbias_limb(int64_t H, int k) {
 // reduced limb has to be widened back to 64 bits (the two-chain ref10 order needs that
 // twice and is ~15 % more VALU work here).
 //
-// High-word carry (CPZ_CARRY_HI=1, default): with H = hi 2^32 + lo, column k's high word
+// High-word carry: with H = hi 2^32 + lo, column k's high word
 // moves into column k+1 as ONE v_mad_i64_i32 (hi * 2^(32-w) + H[k+1], the multiplier kept
 // opaque in an SGPR so LLVM does not turn it back into a 64-bit shift + add), and the few
 // bits of lo above the limb (lo >> w < 2^7) join limb k+1 in 32 bits (v_add3 with the
 // unbias).  Per column: 1 MAD + 3 32-bit ops instead of a 64-bit shift, a 64-bit add and 2
 // 32-bit ops; limbs end in [-2^(w-1), 2^(w-1) + 127).  k_verify_each 2.155 -> 2.105 ms per
-// launch (A/B, two alternating runs each, one box).  =0 selects the shift/add chain.
-#ifndef CPZ_CARRY_HI
-#define CPZ_CARRY_HI 1
-#endif
+// launch against the shift/add chain (A/B, two alternating runs each, one box).
 CPZ_HD fe fe_carry_biased(int64_t H[10]) {
   fe r;
-#if CPZ_CARRY_HI
   uint32_t small = 0;
 #pragma unroll
   for (int k = 0; k < 9; k++) {
@@ -204,16 +191,6 @@ CPZ_HD fe fe_carry_biased(int64_t H[10]) {
   // carry out of limb 9 = hi9 2^7 + (lo9 >> 25), times 19 into limb 0 (biased, then centred)
   const int64_t h0 = (int64_t)hi9 * (int64_t)opaque_sgpr(19 << 7) +
                      (int64_t)(uint64_t)(((uint32_t)r.v[0] + (uint32_t)carry_bias(0)) + 19u * (lo9 >> 25));
-#else
-#pragma unroll
-  for (int k = 0; k < 9; k++) {
-    H[k + 1] += H[k] >> ((k & 1) ? 25 : 26);
-    r.v[k] = unbias_limb(H[k], k);
-  }
-  const int64_t c9 = H[9] >> 25;
-  r.v[9] = unbias_limb(H[9], 9);
-  const int64_t h0 = (int64_t)r.v[0] + 19 * c9 + carry_bias(0);
-#endif
   r.v[1] += (int32_t)(h0 >> 26);
   r.v[0] = unbias_limb(h0, 0);
   return r;
@@ -250,7 +227,6 @@ CPZ_HD fe fe_mul(const fe& f, const fe& g) {
     }
   }
   fe r = fe_carry_biased(h);
-  CPZ_SEQ();
   return r;
 }
 
@@ -286,7 +262,6 @@ CPZ_HD fe fe_sq(const fe& f) {
   int64_t h[10];
   fe_sq_wide(h, f, 1);
   fe r = fe_carry_biased(h);
-  CPZ_SEQ();
   return r;
 }
 
@@ -298,7 +273,6 @@ CPZ_HD fe fe_sq2(const fe& f) {
 #pragma unroll
   for (int i = 0; i < 10; i++) h[i] += h[i];
   fe r = fe_carry_biased(h);
-  CPZ_SEQ();
   return r;
 }
 
@@ -323,21 +297,15 @@ CPZ_HD fe fe_carry_floor(int64_t H[10]) {
 
 // Repeated squaring (n >= 1): the intermediate squares use floor carries (above), the
 // last one the centred carry, so the result is an ordinary tight element.
-// Unroll factor of the squaring loop (tuning variant -DCPZ_SQN_UNROLL=k): letting the
-// scheduler overlap one square's carry chain with the next square's products measured
-// slower, not faster (k_verify_each 2.31 ms rolled vs 2.33 ms for k = 2 and 4, A/B).
-#ifndef CPZ_SQN_UNROLL
-#define CPZ_SQN_UNROLL 1
-#endif
-#define CPZ_PRAGMA_(x) _Pragma(#x)
-#define CPZ_PRAGMA(x) CPZ_PRAGMA_(x)
+// The squaring loop stays rolled: letting the scheduler overlap one square's carry chain with
+// the next square's products measured slower (k_verify_each 2.31 ms rolled vs 2.33 ms
+// unrolled by 2 and 4, A/B).
 CPZ_HD fe fe_sqn(fe f, int n) {
-CPZ_PRAGMA(unroll CPZ_SQN_UNROLL)
+#pragma unroll 1
   for (int i = 1; i < n; i++) {
     int64_t h[10];
     fe_sq_wide(h, f, 0);
     f = fe_carry_floor(h);
-    CPZ_SEQ();
   }
   return fe_sq(f);
 }

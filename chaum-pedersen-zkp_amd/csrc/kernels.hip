@@ -329,34 +329,16 @@ __device__ __forceinline__ void verify_one_row(const VerifyArgs& a, int64_t i, c
                                                uint32_t* rows) {
   const uint32_t* src[4] = {a.y1, a.y2, a.r1, a.r2};
   uint32_t sw[8], cw[8];
-  uint8_t st_s;
-  if (a.fused) {
-    // the challenge and the response checks here, from the rows being staged (no k_challenge
-    // launch, no c round trip through HBM)
-    uint32_t w[4][8];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      load_words8(w[q], src[q], i);
+  for (int q = 0; q < 4; q++) {
+    uint32_t w[8];
+    load_words8(w, src[q], i);
 #pragma unroll
-      for (int k = 0; k < 8; k++) rows[(8 * q + k) * kVerifyBlock] = w[q][k];
-    }
-    load_words8(sw, a.s, i);
-    const sc c = challenge_fixed_pk(a.fused, a.fused + 50, w[0], w[1], w[2], w[3]);
-#pragma unroll
-    for (int k = 0; k < 8; k++) cw[k] = c.w[k];
-    st_s = response_status(sw, a.eq_only != 0);
-  } else {
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      uint32_t w[8];
-      load_words8(w, src[q], i);
-#pragma unroll
-      for (int k = 0; k < 8; k++) rows[(8 * q + k) * kVerifyBlock] = w[k];
-    }
-    load_words8(sw, a.s, i);
-    load_words8(cw, a.c, i);
-    st_s = a.status[i];
+    for (int k = 0; k < 8; k++) rows[(8 * q + k) * kVerifyBlock] = w[k];
   }
+  load_words8(sw, a.s, i);
+  load_words8(cw, a.c, i);
+  const uint8_t st_s = a.status[i];
   const DigitRef y1{rows, kVerifyBlock}, y2{rows + 8 * kVerifyBlock, kVerifyBlock},
       r1{rows + 16 * kVerifyBlock, kVerifyBlock}, r2{rows + 24 * kVerifyBlock, kVerifyBlock};
   a.status[i] = verify_proof(y1, y2, r1, r2, sw, cw, st_s, comb_g, comb_h, tab, dig, kVerifyBlock, nullptr,
@@ -423,36 +405,6 @@ __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each(
   }
 #endif
 }
-
-#if defined(CPZ_VERIFY_DYNAMIC)
-// Work-queue variant (A/B only): one launch of the resident grid; each wave takes the next 64
-// proofs from a global counter until the batch is exhausted (every wave leaves once the
-// counter passes n), so no launch boundary inside a batch leaves SIMDs half occupied.
-__global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_each_queue(VerifyArgs a, unsigned* work) {
-  const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
-  const int64_t gtid = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;
-  const SlabTable tab{a.scratch, (uint32_t)gtid * (uint32_t)(kCachedEntries * sizeof(ge_cached))};
-  __shared__ uint32_t dig[16 * kVerifyBlock];
-  __shared__ uint32_t rows[32 * kVerifyBlock];
-  const int lane = threadIdx.x & 63;
-  for (;;) {
-    unsigned base = 0;
-    if (lane == 0) base = atomicAdd(work, 64u);
-    base = (unsigned)__shfl((int)base, 0, 64);
-    if ((int64_t)base >= a.n) break;
-    const int64_t i = (int64_t)base + lane;
-    if (i < a.n) verify_one_row(a, i, comb_g, comb_h, tab, dig + threadIdx.x, rows + threadIdx.x);
-  }
-}
-
-hipError_t launch_verify_each_queue(const VerifyArgs& a, int grid, unsigned* work, hipStream_t st) {
-  if (a.n <= 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned), st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_verify_each_queue, dim3(grid), dim3(kVerifyBlock), 0, st, a, work);
-  return hipGetLastError();
-}
-#endif
 
 // ---------------------------------------------------------------------------------------
 // Synthetic prover (input generator): x_i, k_i = wide(ChaCha20(seed_x / seed_k, block i)).

@@ -23,12 +23,9 @@ constexpr int kRlcSortGroups = 64;      // max blocks per window in the counting
 constexpr int64_t kRlcSortChunk = CPZ_RLC_SORT_CHUNK;  // target points per sort block
 constexpr int kNielsEntriesRlc = kTableB;
 constexpr int kRlcChunk = 64;            // sorted entries per bucket-accumulation thread
-#ifndef CPZ_RLC_INTER32
-#define CPZ_RLC_INTER32 1  // 32-bit coarse-sort entries (rlc.hip, k_rlc_coarse / k_rlc_fine)
-#endif
 // Points of one MSM (its flat positions t, incl. the two extras): the 32-bit entries hold t
 // in 24 bits and all-ones is their empty marker.
-constexpr int64_t kRlcMaxMsmPoints = CPZ_RLC_INTER32 ? (1ll << 24) - 1 : (1ll << 31);
+constexpr int64_t kRlcMaxMsmPoints = (1ll << 24) - 1;
 
 struct RlcPrepArgs {
   int64_t n;
@@ -61,7 +58,7 @@ struct RlcMsmArgs {
   int groups;                    // sort blocks per window
   int64_t chunk;                 // points per sort block
   uint32_t* idx;                 // [16][istride]
-  uint64_t* inter;               // [16][istride] coarse-sorted entries (32-bit with CPZ_RLC_INTER32)
+  uint32_t* inter;               // [16][istride] coarse-sorted entries (32-bit)
   int64_t istride;
   ge_p3* buckets;                // [16][2^15]
   ge_p3* heads;                  // [16][hstride] partials of buckets begun in an earlier chunk

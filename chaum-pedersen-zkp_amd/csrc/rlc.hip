@@ -283,9 +283,9 @@ __global__ void __launch_bounds__(1024) k_rlc_scan(RlcMsmArgs a) {
 //                 it spans < 1 MB, so its writes still merge in L2.
 // A coarse bin's region of `inter` is the same range of positions its buckets occupy in
 // idx, so both passes share the offsets from k_rlc_scan.
-// Coarse-sorted entries are 32 bits (CPZ_RLC_INTER32, rlc.h): fine bucket (7 bits) << 25 |
-// sign << 24 | flat position t of the point in this MSM (t < kRlcMaxMsmPoints); k_rlc_fine maps
-// t back to the point id.  (64-bit entries with the id itself: CPZ_RLC_INTER32=0.)
+// Coarse-sorted entries are 32 bits: fine bucket (7 bits) << 25 | sign << 24 | flat position t
+// of the point in this MSM (t < kRlcMaxMsmPoints); k_rlc_fine maps t back to the point id.
+// (64-bit entries holding the id itself measured 0.61 against 0.53 ms per 2^20 proofs.)
 constexpr int kRlcCoarse = 256;
 constexpr int kRlcFinePerCoarse = kRlcBuckets / kRlcCoarse;  // 128
 constexpr int kRlcTile = 8192;
@@ -326,11 +326,7 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_coarse(RlcMsmArgs a) {
   const int64_t c0 = (int64_t)g * a.chunk;
   const int64_t c1 = c0 + a.chunk < total ? c0 + a.chunk : total;
   const int16_t* dig = a.digits + (int64_t)w * a.dstride;
-#if CPZ_RLC_INTER32
-  uint32_t* inter = reinterpret_cast<uint32_t*>(a.inter) + (int64_t)w * a.istride;
-#else
-  uint64_t* inter = a.inter + (int64_t)w * a.istride;
-#endif
+  uint32_t* inter = a.inter + (int64_t)w * a.istride;
   constexpr int per_thread = kRlcTile / kRlcSortBlock;  // 8
   // A thread's 8 points of a tile are consecutive, so their digits are one 16-byte load where
   // the range is aligned (p0 is a multiple of 8 on every RLC path; the two extras at the end
@@ -360,19 +356,12 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_coarse(RlcMsmArgs a) {
       const int64_t t = tb + k;
       ent[k] = ~0ull;
       if (t < c1) {
-        const int64_t j = msm_point(a, t);
         const int d = dv[k];
         if (d != 0) {
           const uint32_t b = (uint32_t)((d < 0 ? -d : d) - 1);
           const uint32_t c = b / kRlcFinePerCoarse;
-#if CPZ_RLC_INTER32
-          (void)j;
           ent[k] = ((uint64_t)c << 40) | ((uint32_t)(b % kRlcFinePerCoarse) << 25) | (d < 0 ? (1u << 24) : 0u) |
                    (uint32_t)t;
-#else
-          ent[k] = ((uint64_t)c << 40) | ((uint64_t)(b % kRlcFinePerCoarse) << 32) | (uint32_t)j |
-                   (d < 0 ? 0x80000000u : 0u);
-#endif
           rank[k] = atomicAdd(&cnt[c], 1u);
         }
       }
@@ -407,11 +396,7 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_coarse(RlcMsmArgs a) {
     for (uint32_t e = tid; e < nt; e += kRlcSortBlock) {
       const uint64_t v = buf[e];
       const uint32_t c = (uint32_t)(v >> 40);
-#if CPZ_RLC_INTER32
       inter[gbase[c] + (e - start[c])] = (uint32_t)v;
-#else
-      inter[gbase[c] + (e - start[c])] = v & 0xffffffffffull;
-#endif
     }
     __syncthreads();
     if (tid < kRlcCoarse) {
@@ -420,20 +405,6 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_coarse(RlcMsmArgs a) {
     }
     __syncthreads();
   }
-}
-
-// Where sorted entry e of a window lives in idx: every group of 64 chunks (one wave of
-// k_rlc_bucket, kRlcChunk * 64 entries) is stored transposed, [entry in chunk][chunk], so
-// that the wave's 64 lanes, each walking its own chunk, read 64 consecutive ids per step
-// (two 128-byte lines, each used once) instead of 64 lines 256 bytes apart that the point
-// gathers evict before the lane comes back for the next id.
-static_assert(kRlcChunk == 64, "idx_slot assumes 64-entry chunks and 64-lane waves");
-#ifndef CPZ_RLC_IDX_T
-#define CPZ_RLC_IDX_T 0  // 1: transposed groups (bucket -1 %, fine +0.15 ms: not kept)
-#endif
-__device__ __forceinline__ uint32_t idx_slot(uint32_t e) {
-  if (!CPZ_RLC_IDX_T) return e;
-  return (e & ~(uint32_t)(kRlcChunk * 64 - 1)) | ((e % kRlcChunk) * 64) | ((e / kRlcChunk) % 64);
 }
 
 __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_fine(RlcMsmArgs a) {
@@ -448,8 +419,7 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_fine(RlcMsmArgs a) {
   __syncthreads();
   uint32_t* idx = a.idx + (int64_t)w * a.istride;
   constexpr int U = 4;  // loads in flight per thread
-#if CPZ_RLC_INTER32
-  const uint32_t* inter = reinterpret_cast<const uint32_t*>(a.inter) + (int64_t)w * a.istride;
+  const uint32_t* inter = a.inter + (int64_t)w * a.istride;
   for (uint32_t e0 = r0 + tid; e0 < r1; e0 += U * kRlcSortBlock) {
     uint32_t v[U];
 #pragma unroll
@@ -462,29 +432,12 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_fine(RlcMsmArgs a) {
       if (v[k] == ~0u) continue;
       const uint32_t pos = atomicAdd(&cur[v[k] >> 25], 1u);
       const uint32_t id = (uint32_t)msm_point(a, v[k] & 0xffffffu) | ((v[k] << 7) & 0x80000000u);
-      if (staged) img[pos] = id; else idx[idx_slot(pos)] = id;
+      if (staged) img[pos] = id; else idx[pos] = id;
     }
   }
-#else
-  const uint64_t* inter = a.inter + (int64_t)w * a.istride;
-  for (uint32_t e0 = r0 + tid; e0 < r1; e0 += U * kRlcSortBlock) {
-    uint64_t v[U];
-#pragma unroll
-    for (int k = 0; k < U; k++) {
-      const uint32_t e = e0 + k * kRlcSortBlock;
-      v[k] = e < r1 ? inter[e] : ~0ull;  // entries have v >> 32 < 128: never ~0
-    }
-#pragma unroll
-    for (int k = 0; k < U; k++) {
-      if (v[k] == ~0ull) continue;
-      const uint32_t pos = atomicAdd(&cur[(uint32_t)(v[k] >> 32)], 1u);
-      if (staged) img[pos] = (uint32_t)v[k]; else idx[idx_slot(pos)] = (uint32_t)v[k];
-    }
-  }
-#endif
   if (!staged) return;
   __syncthreads();
-  for (uint32_t e = tid; e < r1 - r0; e += kRlcSortBlock) idx[idx_slot(r0 + e)] = img[e];
+  for (uint32_t e = tid; e < r1 - r0; e += kRlcSortBlock) idx[r0 + e] = img[e];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -507,77 +460,26 @@ __device__ __forceinline__ ge_p1p1 p1p1_identity_rlc() {
   return r;
 }
 
-#ifndef CPZ_RLC_BUCKET_LDS
-#define CPZ_RLC_BUCKET_LDS 0
-#endif
-#if CPZ_RLC_BUCKET_LDS
-// LDS-staged variant: the next entry's Niels point is brought into an LDS slot of the wave
-// by asynchronous direct-to-LDS loads (gfx950 global_load_lds_dwordx4) while the current
-// entry is added, instead of being prefetched into 30 VGPRs -- so the kernel fits 4 waves
-// per SIMD.  Each wave owns 8 x 64 x 16 B = 8 KB of LDS (32 KB per block).
-__device__ __forceinline__ void stage_point(uint4 (*slot)[64], const ge_niels* src) {
-  const uint4* g = reinterpret_cast<const uint4*>(src);
-#pragma unroll
-  for (int v = 0; v < 8; v++) __builtin_amdgcn_global_load_lds(g + v, &slot[v][0], 16, 0, 0);
-}
-
-__global__ void __launch_bounds__(256, 4) k_rlc_bucket(RlcMsmArgs a) {
-  __shared__ uint4 stage[4][8][64];
-  const int w = blockIdx.y;
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
-  const uint32_t total = off[kRlcBuckets];
-  const int64_t e0l = t * kRlcChunk;
-  if (e0l >= (int64_t)total) return;
-  const uint32_t e0 = (uint32_t)e0l;
-  const uint32_t e1 = e0 + kRlcChunk < total ? e0 + kRlcChunk : total;
-  const uint32_t* idx = a.idx + (int64_t)w * a.istride;
-  ge_p3* bw = a.buckets + (int64_t)w * kRlcBuckets;
-  ge_p3* heads = a.heads + (int64_t)w * a.hstride;
-  int lo = 0, hi = kRlcBuckets - 1;
+// The bucket holding sorted entry e, given that bucket b ended at e (off[b + 1] == e): the last
+// b' > b with off[b'] <= e.  A gallop, then a binary search, so a sparse window costs O(log gap)
+// dependent loads per bucket instead of one per empty bucket skipped -- a small batch spreads a
+// few entries over 2^15 buckets, and walking them one by one made k_rlc_bucket 2.2 ms at n = 1
+// (2^15 dependent offset loads on one lane) against 0.6 ms at n = 1000.  In a dense window the
+// next bucket is non-empty and this is the one load the walk made.
+__device__ __forceinline__ int next_bucket(const uint32_t* off, int b, uint32_t e) {
+  int lo = b + 1, step = 1;
+  while (lo + step < kRlcBuckets && off[lo + step] <= e) {
+    lo += step;
+    step <<= 1;
+  }
+  int hi = lo + step - 1 < kRlcBuckets - 1 ? lo + step - 1 : kRlcBuckets - 1;  // off[kRlcBuckets] > e
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (off[mid] <= e0) lo = mid; else hi = mid - 1;
+    if (off[mid] <= e) lo = mid; else hi = mid - 1;
   }
-  int b = lo;
-  uint32_t bend = off[b + 1];
-  bool head = off[b] < e0;
-  ge_p1p1 r = p1p1_identity_rlc();
-  uint32_t id = idx[idx_slot(e0)];
-  stage_point(stage[wv], a.pts + (id & 0x7fffffffu));
-  for (uint32_t e = e0; e < e1; e++) {
-    const bool neg = (id >> 31) != 0;
-    const uint32_t nid = e + 1 < e1 ? idx[idx_slot(e + 1)] : 0u;
-    ge_p3 acc = p1p1_to_p3(r);
-    // vmcnt counts loads and stores in issue order: the bucket-boundary loads go before the
-    // wait and the partial's store after the next point's staging, so the wait below never
-    // waits for a store issued in the same iteration
-    const bool emit = e == bend;
-    const int bo = b;
-    const bool ho = head;
-    if (emit) {
-      head = false;
-      do { b++; bend = off[b + 1]; } while (bend <= e);
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this entry's point is in LDS
-    ge_niels p;
-    uint4* pv = reinterpret_cast<uint4*>(&p);
-#pragma unroll
-    for (int v = 0; v < 8; v++) pv[v] = stage[wv][v][lane];
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): read before the slot is refilled
-    if (e + 1 < e1) stage_point(stage[wv], a.pts + (nid & 0x7fffffffu));
-    id = nid;
-    if (emit) {
-      if (ho) store_p3(heads + t, acc); else store_p3(bw + bo, acc);
-      acc = ge_identity();
-    }
-    r = ge_add_niels(acc, ge_niels_cneg(p, neg));
-  }
-  const ge_p3 v = p1p1_to_p3(r);
-  if (head) store_p3(heads + t, v); else store_p3(bw + b, v);
+  return lo;
 }
-#else
+
 // (141 VGPRs, 3 waves/SIMD; forcing 4 waves -- 128 VGPRs with spills -- measured 7 % slower)
 __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
   const int w = blockIdx.y;
@@ -601,24 +503,24 @@ __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
   uint32_t bend = off[b + 1];
   bool head = off[b] < e0;  // bucket b started in an earlier chunk
   ge_p1p1 r = p1p1_identity_rlc();
-  uint32_t id = idx[idx_slot(e0)];
+  uint32_t id = idx[e0];
   for (uint32_t e = e0; e < e1; e++) {
     const ge_niels p = load_niels(a.pts + (id & 0x7fffffffu));
     const bool neg = (id >> 31) != 0;
-    id = e + 1 < e1 ? idx[idx_slot(e + 1)] : 0u;
+    id = e + 1 < e1 ? idx[e + 1] : 0u;
     ge_p3 acc = p1p1_to_p3(r);
     if (e == bend) {  // bucket b complete: emit it (a store, no extra field work), restart
       if (head) store_p3(heads + t, acc); else store_p3(bw + b, acc);
       head = false;
       acc = ge_identity();
-      do { b++; bend = off[b + 1]; } while (bend <= e);
+      b = next_bucket(off, b, e);
+      bend = off[b + 1];
     }
     r = ge_add_niels(acc, ge_niels_cneg(p, neg));
   }
   const ge_p3 v = p1p1_to_p3(r);
   if (head) store_p3(heads + t, v); else store_p3(bw + b, v);
 }
-#endif
 
 // Buckets leave the fix-up in cached form (Y+X, Y-X, Z, 2dT, the same 160 bytes), so the
 // reduction kernels add them with 2 quad rounds and no conversion of their own.

@@ -143,7 +143,6 @@ struct cpz_ctx {
   DevBuf prefix;    // 2 StrobeSnap
   bool prefix_fixed = false;  // prefix[1] at the fixed position: k_challenge_noctx applies
   uint32_t chal_k1[50], chal_k2[50];  // its framing masks
-  DevBuf chal_fused;          // prefix[1] ^ k1, k2 (100 words): the challenge fused into k_verify_each
   bool ctx32_fixed = false;   // prefix[0] at the fixed position: 32-byte contexts' fast path
   uint32_t chal_c32[3][50];   // its framing masks (g and h folded in)
   DevBuf gh_words;  // 16 words
@@ -152,7 +151,6 @@ struct cpz_ctx {
   DevBuf c;         // n x 32
   DevBuf st;        // n
   DevBuf scratch;   // per-stream table slabs (kCachedEntries ge_cached per thread)
-  DevBuf work;      // work-queue counter (CPZ_VERIFY_DYNAMIC variant)
   // host-API staging (y1, y2, r1, r2, s, and challenges / witnesses / nonces)
   DevBuf in[7];
   DevBuf ctxb, ctxo, ctxp;
@@ -278,16 +276,6 @@ int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32]) {
   CPZ_HIP(hipMemcpyAsync(snap, ctx->prefix.p, sizeof(snap), hipMemcpyDeviceToHost, ctx->stream));
   CPZ_HIP(hipStreamSynchronize(ctx->stream));
   ctx->prefix_fixed = cpz::challenge_prefix_is_fixed(snap[1]) && cpz::challenge_masks(ctx->chal_k1, ctx->chal_k2);
-  if (ctx->prefix_fixed) {
-    uint32_t fw[100];
-    std::memcpy(fw, snap[1].state, 200);
-    for (int w = 0; w < 50; w++) {
-      fw[w] ^= ctx->chal_k1[w];
-      fw[50 + w] = ctx->chal_k2[w];
-    }
-    CPZ_HIP(ctx->chal_fused.ensure(sizeof(fw)));
-    CPZ_HIP(hipMemcpy(ctx->chal_fused.p, fw, sizeof(fw), hipMemcpyHostToDevice));
-  }
   {
     uint32_t gw[16];
     words_from_bytes(gw, g, h);
@@ -341,12 +329,6 @@ int verify_grid(cpz_ctx* ctx, size_t n) {
 // 4 / half 51.5 M, 3 / third 47.3 M, 4 / quarter 48.8 M.
 // Challenges per verify chunk on the chunk's stream (hidden under the other stream's verify
 // work; +0.5-1.1 % A/B on one box against one up-front challenge launch).
-#ifndef CPZ_VERIFY_FUSED
-#define CPZ_VERIFY_FUSED 0  // 1: no-context challenges computed inside k_verify_each (measured +0.1 %, not kept)
-#endif
-#ifndef CPZ_CHALLENGE_PER_CHUNK
-#define CPZ_CHALLENGE_PER_CHUNK 1
-#endif
 #ifndef CPZ_VERIFY_STREAMS
 #define CPZ_VERIFY_STREAMS 2
 #endif
@@ -453,12 +435,6 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->prefix.p);
   ca.c_out = c_buf;
   ca.status_out = status;
-#if !CPZ_CHALLENGE_PER_CHUNK
-  {
-    StageTimer t(ctx, 0, st);
-    CPZ_HIP(cpz::launch_challenge(ca, st));
-  }
-#endif
   cpz::VerifyArgs va;
   va.n = (int64_t)n;
   va.y1 = ca.y1;
@@ -472,34 +448,7 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   va.scratch = nullptr;  // set per launch
   va.eq_only = ca.eq_only;
   StageTimer span(ctx, 5, st);  // all chunks, all streams (the launches overlap)
-#if CPZ_VERIFY_FUSED
-  if (ca.ctx_off == nullptr && ctx->prefix_fixed) {
-    // no contexts on the fixed schedule: k_verify_each computes c and the response status
-    // itself (c_buf is left unwritten; no caller reads it after a verify)
-    va.fused = static_cast<const uint32_t*>(ctx->chal_fused.p);
-    return launch_verify_chunks(ctx, va, 1, st, rr, join);
-  }
-#endif
-#if defined(CPZ_VERIFY_DYNAMIC)
-  if (rr == nullptr) {  // device-resident batch: challenges up front, then one work-queue launch
-    {
-      StageTimer tc(ctx, 0, st);
-      CPZ_HIP(cpz::launch_challenge(ca, st));
-    }
-    const int g = verify_grid(ctx, n);
-    CPZ_HIP(ctx->scratch.ensure((size_t)g * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached)));
-    CPZ_HIP(ctx->work.ensure(64));
-    va.scratch = static_cast<char*>(ctx->scratch.p);
-    StageTimer t(ctx, 1, st);
-    CPZ_HIP(cpz::launch_verify_each_queue(va, g, static_cast<unsigned*>(ctx->work.p), st));
-    return CPZ_OK;
-  }
-#endif
-#if CPZ_CHALLENGE_PER_CHUNK
   return launch_verify_chunks(ctx, va, 1, st, rr, join, &ca);
-#else
-  return launch_verify_chunks(ctx, va, 1, st, rr, join);
-#endif
 }
 
 // Stage host inputs on the device.  Returns device pointers through out[].
@@ -562,12 +511,11 @@ int rlc_reserve_prepared(RlcPrepared& P, int64_t n) {
 int rlc_reserve_msm(RlcMsmSet& S, int64_t span) {
   if (span <= S.cap) return CPZ_OK;
   S.cap = 0;
-  const size_t inter_entry = CPZ_RLC_INTER32 ? sizeof(uint32_t) : sizeof(uint64_t);
   CPZ_HIP(S.counts.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcBuckets));
   CPZ_HIP(S.offsets.ensure(sizeof(uint32_t) * cpz::kRlcWindows * (cpz::kRlcBuckets + 1)));
   CPZ_HIP(S.bhist.ensure(sizeof(uint32_t) * cpz::kRlcWindows * cpz::kRlcSortGroups * cpz::kRlcBuckets));
   CPZ_HIP(S.idx.ensure((size_t)rlc_istride(span) * cpz::kRlcWindows * sizeof(uint32_t)));
-  CPZ_HIP(S.inter.ensure((size_t)rlc_istride(span) * cpz::kRlcWindows * inter_entry));
+  CPZ_HIP(S.inter.ensure((size_t)rlc_istride(span) * cpz::kRlcWindows * sizeof(uint32_t)));
   CPZ_HIP(S.buckets.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * cpz::kRlcBuckets));
   CPZ_HIP(S.heads.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * (size_t)(rlc_istride(span) / cpz::kRlcChunk)));
   const size_t nseg = (size_t)cpz::kRlcWindows * (cpz::kRlcBuckets / cpz::kRlcSegLen);
@@ -617,7 +565,7 @@ int rlc_msm_args(const RlcPrepared& P, RlcMsmSet& S, int64_t lo, int64_t hi, cpz
   m.bhist = static_cast<uint32_t*>(S.bhist.p);
   cpz::rlc_sort_geometry(m, (m.p1 - m.p0) + 2);
   m.idx = static_cast<uint32_t*>(S.idx.p);
-  m.inter = static_cast<uint64_t*>(S.inter.p);
+  m.inter = static_cast<uint32_t*>(S.inter.p);
   m.istride = rlc_istride(S.cap);
   m.buckets = static_cast<cpz::ge_p3*>(S.buckets.p);
   m.heads = static_cast<cpz::ge_p3*>(S.heads.p);
@@ -1477,7 +1425,6 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->c.release();
   ctx->st.release();
   ctx->scratch.release();
-  ctx->work.release();
   for (auto& b : ctx->in) b.release();
   ctx->ctxb.release();
   ctx->ctxo.release();

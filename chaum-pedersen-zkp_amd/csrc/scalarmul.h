@@ -12,11 +12,6 @@
 
 namespace cpz {
 
-// Issue a window's two table loads before its four doublings (1) or at their additions (0).
-#ifndef CPZ_TABLE_PREFETCH
-#define CPZ_TABLE_PREFETCH 1
-#endif
-
 constexpr int kTableV = 8;     // cached multiples 1..8 of a variable base (radix-16 digits)
 constexpr int kTableSlots = kTableV + 1;  // + the identity at slot 0 (digit 0 needs no select)
 constexpr int kTableB = 128;   // Niels multiples 1..128 of a fixed base (radix-256 digits)
@@ -231,18 +226,12 @@ CPZ_HD ge_p1p1 straus_half_comb(const SlabTable& tab_y, const SlabTable& tab_r, 
     for (int m = 7; m >= 0; m--) {
       const int du = ((int32_t)(wu << (28 - 4 * m))) >> 28;
       const int dv = ((int32_t)(wv << (28 - 4 * m))) >> 28;
-#if CPZ_TABLE_PREFETCH
       // both table loads issued before the four doublings, which hide their latency
       // (the tables live in the HBM-backed scratch slab; measured ~1 % faster)
       const ge_cached ey = cached_lookup(tab_y, du), er = cached_lookup(tab_r, dv);
       if (j != 3 || m != 7) cur = dbl4(cur);
       cur = ge_add_cached(p1p1_to_p3(cur), ey);
       cur = ge_add_cached(p1p1_to_p3(cur), er);
-#else
-      if (j != 3 || m != 7) cur = dbl4(cur);
-      cur = ge_add_cached(p1p1_to_p3(cur), cached_lookup(tab_y, du));
-      cur = ge_add_cached(p1p1_to_p3(cur), cached_lookup(tab_r, dv));
-#endif
     }
   }
   return comb_add(cur, comb, sdig);

@@ -57,12 +57,9 @@ CPZ_HD uint64_t KECCAK_RC(int i) {
 // (truth table imm = f(S0 = 0xF0, S1 = 0xCC, S2 = 0xAA)), so theta's five-way XOR and chi
 // are one instruction per 32 bits where plain code needs two.  LLVM does not form these
 // from the 64-bit expressions below by itself.
-#ifndef CPZ_KECCAK_BITOP3
-#define CPZ_KECCAK_BITOP3 1  // 0: plain XOR / AND-NOT (A/B variant)
-#endif
 template <int IMM>
 CPZ_HD uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
-#if defined(__HIP_DEVICE_COMPILE__) && CPZ_KECCAK_BITOP3
+#if defined(__HIP_DEVICE_COMPILE__)
   uint32_t lo, hi;
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(lo) : "v"((uint32_t)a), "v"((uint32_t)b), "v"((uint32_t)c),
       "i"(IMM));

@@ -16,14 +16,9 @@
 #include "scalarmul.h"
 #include "transcript.h"
 
-// Loops over the two points of an equation and over the two equations: rolled by default
-// (one copy of the decode / Straus code); -DCPZ_VERIFY_UNROLLED unrolls them (4 inlined
-// decodes, 2 Straus loops) for side-by-side measurement.
-#if defined(CPZ_VERIFY_UNROLLED)
-#define CPZ_EQ_LOOP _Pragma("unroll 2")
-#else
+// Loops over the two points of an equation and over the two equations stay rolled (one
+// copy of the decode / Straus code; unrolling them measured slower).
 #define CPZ_EQ_LOOP _Pragma("unroll 1")
-#endif
 
 namespace cpz {
 
@@ -133,24 +128,6 @@ CPZ_HD sc challenge_fixed(const uint32_t prefix[50], const uint32_t k1[50], cons
   xor_message<kTailR2>(st, r2);
   keccak_words(st);
   return sc_reduce_wide(st);  // challenge bytes 0..63 = state words 0..15
-}
-
-// challenge_fixed with the prefix and the first mask pre-combined (pk1 = prefix ^ k1): the
-// form k_verify_each uses when it computes the challenge itself.
-CPZ_HD sc challenge_fixed_pk(const uint32_t pk1[50], const uint32_t k2[50], const uint32_t y1[8], const uint32_t y2[8],
-                             const uint32_t r1[8], const uint32_t r2[8]) {
-  uint32_t st[50];
-#pragma unroll
-  for (int w = 0; w < 50; w++) st[w] = pk1[w];
-  xor_message<kTailY1>(st, y1);
-  xor_message<kTailY2>(st, y2);
-  xor_message<kTailR1>(st, r1);
-  keccak_words(st);
-#pragma unroll
-  for (int w = 0; w < 50; w++) st[w] ^= k2[w];
-  xor_message<kTailR2>(st, r2);
-  keccak_words(st);
-  return sc_reduce_wide(st);
 }
 
 // 32-byte-context tail: prefix = the state after Transcript::new, m = the three segments'
