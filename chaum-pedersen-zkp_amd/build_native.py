@@ -113,6 +113,22 @@ def build_cpp_test(force: bool = False) -> str:
     return CPP_TEST
 
 
+DROPIN_TEST = os.path.join(ROOT, "tests", "cpp", "dropin_test")
+
+
+def build_dropin_test(force: bool = False) -> str:
+    """The drop-in's call sequence through the C++ mirror (tests/test_gpu_dropin.py)."""
+    src = os.path.join(ROOT, "tests", "cpp", "dropin_test.cpp")
+    hdrs = [os.path.join(ROOT, "include", "cpz.h"), os.path.join(ROOT, "include", "cpz_batch.hpp")]
+    if not force and not _newer(DROPIN_TEST, [src, LIBCPZ] + hdrs):
+        return DROPIN_TEST
+    cxx = shutil.which("g++") or "g++"
+    _run([cxx, "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), src, "-o", DROPIN_TEST + ".tmp",
+          "-L", LIBDIR, "-lcpz", "-Wl,-rpath,$ORIGIN/../../chaum-pedersen-zkp_amd/lib"])
+    os.replace(DROPIN_TEST + ".tmp", DROPIN_TEST)
+    return DROPIN_TEST
+
+
 def build_oracle(force: bool = False) -> None:
     mk = os.path.join(ROOT, "oracle", "Makefile")
     if os.path.exists(mk):
@@ -124,6 +140,7 @@ def build_all(force: bool = False, verbose: bool = False) -> None:
     build_oracle(force)
     build_libcpz(force, verbose)
     build_cpp_test(force)
+    build_dropin_test(force)
 
 
 if __name__ == "__main__":

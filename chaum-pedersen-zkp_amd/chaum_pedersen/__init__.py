@@ -19,10 +19,8 @@ verification result on the CPU.
 """
 from __future__ import annotations
 
-import contextlib
 import ctypes
 import struct
-import threading
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -34,11 +32,14 @@ from ._native import (CpzError, STATUS_BAD_POINT, STATUS_BAD_SCALAR, STATUS_EQ_F
 __all__ = [
     "Error", "InvalidParams", "InvalidScalar", "InvalidGroupElement", "CpzError",
     "Parameters", "Statement", "Proof", "BatchVerifier", "Gpu", "VerifyResult", "Transcript", "Verifier", "Prover",
-    "MAX_BATCH_SIZE", "PROTOCOL_VERSION", "STATUS_OK", "STATUS_EQ_FAIL", "STATUS_BAD_POINT",
+    "MAX_BATCH_SIZE", "RLC_MIN_GROUP", "PROTOCOL_VERSION", "STATUS_OK", "STATUS_EQ_FAIL", "STATUS_BAD_POINT",
     "STATUS_BAD_SCALAR", "STATUS_IDENTITY", "STATUS_ZERO_S", "default_generators", "verify_each_multi", "verify_batch_multi",
 ]
 
 MAX_BATCH_SIZE = 1000          # batch.rs:48
+# Smallest Parameters group that BatchVerifier.verify sends to the RLC batch check (smaller
+# groups: per-proof verification); rust/reference-patch/gpu.rs RLC_MIN_GROUP, cpz_batch.hpp.
+RLC_MIN_GROUP = 2
 PROTOCOL_VERSION = 1           # gadgets.rs:12
 L = 2**252 + 27742317777372353535851937790883648493   # group order (ristretto.rs scalars)
 
@@ -275,6 +276,10 @@ def _ptr(a) -> Optional[int]:
     return None if a is None else a.ctypes.data
 
 
+def _flags(equations_only: bool) -> int:
+    return _native.CALL_EQUATIONS_ONLY if equations_only else 0
+
+
 def _torch_stream(stream):
     """Device entry points default to torch's current stream, so kernels are ordered with
     the torch ops that produce / consume the tensors."""
@@ -304,8 +309,6 @@ class Gpu:
         self._lib = lib
         self._h = h
         self.device = device
-        self._checks = True
-        self._mode_lock = threading.RLock()
 
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -325,7 +328,7 @@ class Gpu:
         self.close()
 
     # -- per-kernel timing (HIP events on the launch stream) -------------------------------
-    STAGES = ("challenge", "verify_each", "rlc_prepare", "rlc_msm", "fallback", "verify_span", "prove", "s7",
+    STAGES = ("challenge", "verify_each", "rlc_prepare", "rlc_msm", "fallback", "verify_span", "prove", "generators",
               "rlc_sort", "rlc_bucket", "rlc_bucket_fix", "rlc_reduce", "rlc_final", "s13", "s14", "s15")
 
     def set_timing(self, enable: bool) -> None:
@@ -348,36 +351,26 @@ class Gpu:
 
     # -- commitment checks (cpz_ctx_set_commitment_checks) ------------------------------------
     def set_commitment_checks(self, enable: bool) -> None:
-        """On (default): statuses 4 / 5 for identity commitments and zero s, the rejections of
-        Proof::from_bytes (gadgets.rs:474-482).  Off: the equations alone decide, as
-        verify_one (batch.rs:185-231) does for a Proof built with Proof::new."""
-        with self._mode_lock:
-            _native.check(self._lib.cpz_ctx_set_commitment_checks(self._h, 1 if enable else 0))
-            self._checks = bool(enable)
-
-    @contextlib.contextmanager
-    def commitment_checks(self, enable: bool):
-        """Scoped set_commitment_checks (restores the previous mode; calls on this object from
-        other threads wait for the scope)."""
-        with self._mode_lock:
-            prev = self._checks
-            self.set_commitment_checks(enable)
-            try:
-                yield self
-            finally:
-                self.set_commitment_checks(prev)
+        """The context's mode.  On (default): statuses 4 / 5 for identity commitments and zero s,
+        the rejections of Proof::from_bytes (gadgets.rs:474-482).  Off: the equations alone
+        decide, as verify_one (batch.rs:185-231) does for a Proof built with Proof::new.  The
+        mode applies to every later call on this context from any thread; for one call alone
+        pass equations_only=True to verify_each / verify_batch / verify_response."""
+        _native.check(self._lib.cpz_ctx_set_commitment_checks(self._h, 1 if enable else 0))
 
     # -- host-buffer entry points ---------------------------------------------------------
-    def verify_each(self, y1, y2, r1, r2, s, contexts=None, params: Optional[Parameters] = None) -> np.ndarray:
-        """Status per proof (uint8[n]) for (n, 32) byte arrays.  cpz_verify_each."""
+    def verify_each(self, y1, y2, r1, r2, s, contexts=None, params: Optional[Parameters] = None,
+                    equations_only: bool = False) -> np.ndarray:
+        """Status per proof (uint8[n]) for (n, 32) byte arrays.  cpz_verify_each_ex;
+        equations_only: commitment checks off for this call (CPZ_CALL_EQUATIONS_ONLY)."""
         params = params or Parameters()
         n = len(y1)
         arrs = [_rows(a, n, nm) for a, nm in ((y1, "y1"), (y2, "y2"), (r1, "r1"), (r2, "r2"), (s, "s"))]
         blob, off, present = _ctx_arrays(contexts, n)
         out = np.empty(n, dtype=np.uint8)
-        _native.check(self._lib.cpz_verify_each(
-            self._h, params.g, params.h, n, *[_ptr(a) for a in arrs], _ptr(blob), _ptr(off), _ptr(present),
-            _ptr(out)))
+        _native.check(self._lib.cpz_verify_each_ex(
+            self._h, _flags(equations_only), params.g, params.h, n, *[_ptr(a) for a in arrs], _ptr(blob), _ptr(off),
+            _ptr(present), _ptr(out)))
         return out
 
     def challenges(self, y1, y2, r1, r2, contexts=None, params: Optional[Parameters] = None) -> np.ndarray:
@@ -391,15 +384,16 @@ class Gpu:
             _ptr(out)))
         return out
 
-    def verify_response(self, y1, y2, r1, r2, s, c, params: Optional[Parameters] = None) -> np.ndarray:
+    def verify_response(self, y1, y2, r1, r2, s, c, params: Optional[Parameters] = None,
+                        equations_only: bool = False) -> np.ndarray:
         """Status per proof with caller-supplied challenges c ((n, 32) canonical scalars):
-        Verifier::verify_response (verifier/mod.rs:144-171), cpz_verify_response."""
+        Verifier::verify_response (verifier/mod.rs:144-171), cpz_verify_response_ex."""
         params = params or Parameters()
         n = len(y1)
         arrs = [_rows(a, n, nm) for a, nm in ((y1, "y1"), (y2, "y2"), (r1, "r1"), (r2, "r2"), (s, "s"), (c, "c"))]
         out = np.empty(n, dtype=np.uint8)
-        _native.check(self._lib.cpz_verify_response(self._h, params.g, params.h, n, *[_ptr(a) for a in arrs],
-                                                    _ptr(out)))
+        _native.check(self._lib.cpz_verify_response_ex(self._h, _flags(equations_only), params.g, params.h, n,
+                                                       *[_ptr(a) for a in arrs], _ptr(out)))
         return out
 
     def prove(self, x, k, contexts=None, params: Optional[Parameters] = None):
@@ -428,8 +422,8 @@ class Gpu:
         return ok, enc
 
     def verify_batch(self, y1, y2, r1, r2, s, seed: bytes, first_index: int = 0, contexts=None,
-                     params: Optional[Parameters] = None, statuses: bool = True):
-        """RLC batch check (cpz_verify_batch).  Returns (partial: bytes, batch_ok: bool,
+                     params: Optional[Parameters] = None, statuses: bool = True, equations_only: bool = False):
+        """RLC batch check (cpz_verify_batch_ex).  Returns (partial: bytes, batch_ok: bool,
         status: uint8[n] or None).  With statuses=True a failing batch runs the fallback
         search and status holds the exact per-entry outcome."""
         params = params or Parameters()
@@ -439,9 +433,9 @@ class Gpu:
         partial = ctypes.create_string_buffer(32)
         ok = ctypes.c_int(0)
         out = np.empty(n, dtype=np.uint8) if statuses else None
-        _native.check(self._lib.cpz_verify_batch(
-            self._h, params.g, params.h, n, *[_ptr(a) for a in arrs], _ptr(blob), _ptr(off), _ptr(present),
-            bytes(seed), first_index, partial, ctypes.byref(ok), _ptr(out)))
+        _native.check(self._lib.cpz_verify_batch_ex(
+            self._h, _flags(equations_only), params.g, params.h, n, *[_ptr(a) for a in arrs], _ptr(blob), _ptr(off),
+            _ptr(present), bytes(seed), first_index, partial, ctypes.byref(ok), _ptr(out)))
         return partial.raw, bool(ok.value), out
 
     def verify_batch_device(self, y1, y2, r1, r2, s, status_out, seed: bytes, first_index: int = 0,
@@ -660,18 +654,17 @@ class Verifier:
         g = self._gpu or _gpu()
         _validate_statement(g, self.statement)  # verifier/mod.rs:121
         one = lambda b: np.frombuffer(b, np.uint8).reshape(1, 32)
-        with g.commitment_checks(False):  # the equations only (verifier/mod.rs:144-171)
-            st = g.verify_each(one(self.statement.y1), one(self.statement.y2), one(proof.r1), one(proof.r2),
-                               one(proof.s), contexts=[transcript.context], params=self.params)
+        # a Proof value: the equations only (verifier/mod.rs:144-171), for this call alone
+        st = g.verify_each(one(self.statement.y1), one(self.statement.y2), one(proof.r1), one(proof.r2),
+                           one(proof.s), contexts=[transcript.context], params=self.params, equations_only=True)
         _raise_status(int(st[0]))
 
     def verify_response(self, challenge, proof: Proof) -> None:
         """verifier/mod.rs:144-171: the caller's challenge (int mod l or 32 canonical bytes)."""
         g = self._gpu or _gpu()
         one = lambda b: np.frombuffer(b, np.uint8).reshape(1, 32)
-        with g.commitment_checks(False):
-            st = g.verify_response(one(self.statement.y1), one(self.statement.y2), one(proof.r1), one(proof.r2),
-                                   one(proof.s), one(_scalar_bytes(challenge)), params=self.params)
+        st = g.verify_response(one(self.statement.y1), one(self.statement.y2), one(proof.r1), one(proof.r2),
+                               one(proof.s), one(_scalar_bytes(challenge)), params=self.params, equations_only=True)
         _raise_status(int(st[0]))
 
 
@@ -769,28 +762,42 @@ class BatchVerifier:
     def clear(self) -> None:
         self._entries.clear()
 
-    def verify(self, rng=None) -> List[VerifyResult]:
-        """batch.rs:171-183.  `rng` is accepted for signature parity; per-entry
-        verification consumes no randomness.  Entries are `Proof` values, which may have been
-        built with Proof(...) (Proof::new: no identity / zero-s checks), so the context runs
-        with commitment checks off: verify_one's equations alone decide (batch.rs:185-231)."""
+    def verify(self, rng=None, rlc_min_group: Optional[int] = None) -> List[VerifyResult]:
+        """batch.rs:171-183, through the call sequence of the Rust drop-in
+        (rust/reference-patch/gpu.rs; C++ mirror: include/cpz_batch.hpp): entries grouped by
+        Parameters in order of first appearance; a one-entry batch is verify_one
+        (cpz_verify_each, batch.rs:178-180) and draws nothing from `rng`; otherwise one 32-byte
+        seed from `rng` (an object with randbytes(), e.g. random.Random / secrets.SystemRandom;
+        None: os.urandom) keys every group's RLC check, groups take consecutive weight indices,
+        and a group of at least rlc_min_group entries (default RLC_MIN_GROUP) runs the RLC batch
+        check with its exact fallback (cpz_verify_batch), a smaller one cpz_verify_each.  Entries
+        are `Proof` values, which may have been built with Proof(...) (Proof::new: no identity /
+        zero-s checks), so every call is equations-only: verify_one's equations alone decide
+        (batch.rs:185-231).  Either entry point returns exactly verify_one's outcome per entry."""
         if not self._entries:
             raise InvalidParams("Cannot verify empty batch")
         gpu = self._gpu or _gpu()
+        rlc_min = RLC_MIN_GROUP if rlc_min_group is None else int(rlc_min_group)
         status = np.empty(len(self._entries), dtype=np.uint8)
-        # One bulk call per distinct Parameters (normally a single group).
-        groups = {}
+        groups = {}   # insertion order = order of first appearance
         for i, e in enumerate(self._entries):
             groups.setdefault((e.params.g, e.params.h), []).append(i)
+        single = len(self._entries) == 1
+        seed = None
+        first_index = 0
         for (g, h), idx in groups.items():
             ents = [self._entries[i] for i in idx]
-            with gpu.commitment_checks(False):
-                st = gpu.verify_each(
-                    np.frombuffer(b"".join(e.statement.y1 for e in ents), np.uint8).reshape(-1, 32),
-                    np.frombuffer(b"".join(e.statement.y2 for e in ents), np.uint8).reshape(-1, 32),
-                    np.frombuffer(b"".join(e.proof.r1 for e in ents), np.uint8).reshape(-1, 32),
-                    np.frombuffer(b"".join(e.proof.r2 for e in ents), np.uint8).reshape(-1, 32),
-                    np.frombuffer(b"".join(e.proof.s for e in ents), np.uint8).reshape(-1, 32),
-                    contexts=[e.context for e in ents], params=Parameters(g, h))
+            rows = [np.frombuffer(b"".join(getattr(e.statement if q in ("y1", "y2") else e.proof, q) for e in ents),
+                                  np.uint8).reshape(-1, 32) for q in ("y1", "y2", "r1", "r2", "s")]
+            ctxs = [e.context for e in ents]
+            if not single and len(idx) >= rlc_min:
+                if seed is None:   # drawn once, as the reference draws its weights (batch.rs:240)
+                    import os
+                    seed = rng.randbytes(32) if rng is not None else os.urandom(32)
+                _, _, st = gpu.verify_batch(*rows, seed, first_index=first_index, contexts=ctxs,
+                                            params=Parameters(g, h), equations_only=True)
+            else:
+                st = gpu.verify_each(*rows, contexts=ctxs, params=Parameters(g, h), equations_only=True)
+            first_index += len(idx)
             status[np.array(idx)] = st
         return [VerifyResult(s) for s in status]

@@ -34,11 +34,13 @@ EXPORTED = (
     "cpz_parse_proofs", "cpz_parse_proofs_device", "cpz_verify_each_multi", "cpz_verify_batch_multi",
     "cpz_verify_response", "cpz_verify_response_device", "cpz_prove", "cpz_prove_device", "cpz_decode_points",
     "cpz_abi_version", "cpz_ctx_set_commitment_checks", "cpz_ctx_stage_times_n", "cpz_ctx_fallback_stats",
+    "cpz_verify_each_ex", "cpz_verify_batch_ex", "cpz_verify_response_ex",
 )
+CALL_EQUATIONS_ONLY = 1   # CPZ_CALL_EQUATIONS_ONLY: commitment checks off for one call
 NUM_STAGES = 16
 FALLBACK_STATS = 6
 FALLBACK_PATHS = {0: "none", 1: "bisection", 2: "partitioned", 3: "per_proof"}
-ABI_VERSION = 3     # CPZ_ABI_VERSION of the cpz.h these declarations follow
+ABI_VERSION = 4     # CPZ_ABI_VERSION of the cpz.h these declarations follow
 
 
 class CpzError(RuntimeError):
@@ -67,6 +69,8 @@ def _declare(lib):
     lib.cpz_default_generators.argtypes = [_p, _p]
     lib.cpz_verify_each.restype = ctypes.c_int
     lib.cpz_verify_each.argtypes = [_p, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p, _p, _p]
+    lib.cpz_verify_each_ex.restype = ctypes.c_int
+    lib.cpz_verify_each_ex.argtypes = [_p, ctypes.c_uint32, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p, _p, _p]
     lib.cpz_verify_each_device.restype = ctypes.c_int
     lib.cpz_verify_each_device.argtypes = [_p, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p, _p, _p, _p]
     lib.cpz_challenges.restype = ctypes.c_int
@@ -81,6 +85,9 @@ def _declare(lib):
     lib.cpz_verify_batch.restype = ctypes.c_int
     lib.cpz_verify_batch.argtypes = ([_p, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p, _p, _p, ctypes.c_uint64,
                                      _p, ctypes.POINTER(ctypes.c_int), _p])
+    lib.cpz_verify_batch_ex.restype = ctypes.c_int
+    lib.cpz_verify_batch_ex.argtypes = ([_p, ctypes.c_uint32, _p, _p, ctypes.c_size_t] + [_p] * 5 +
+                                        [_p, _p, _p, _p, ctypes.c_uint64, _p, ctypes.POINTER(ctypes.c_int), _p])
     lib.cpz_verify_each_multi.restype = ctypes.c_int
     lib.cpz_verify_each_multi.argtypes = [_p, ctypes.c_int, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p, _p, _p]
     lib.cpz_verify_batch_multi.restype = ctypes.c_int
@@ -99,6 +106,8 @@ def _declare(lib):
     lib.cpz_combine_partials.argtypes = [_p, ctypes.c_size_t, _p, _p, ctypes.POINTER(ctypes.c_int)]
     lib.cpz_verify_response.restype = ctypes.c_int
     lib.cpz_verify_response.argtypes = [_p, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p]
+    lib.cpz_verify_response_ex.restype = ctypes.c_int
+    lib.cpz_verify_response_ex.argtypes = [_p, ctypes.c_uint32, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p]
     lib.cpz_verify_response_device.restype = ctypes.c_int
     lib.cpz_verify_response_device.argtypes = [_p, _p, _p, ctypes.c_size_t] + [_p] * 5 + [_p, _p, _p]
     lib.cpz_prove.restype = ctypes.c_int

@@ -41,6 +41,8 @@ struct ChallengeArgs {
   const uint8_t* ctx_bytes;      // concatenated contexts
   const uint64_t* ctx_off;       // n + 1 offsets, or null: no contexts
   const uint8_t* ctx_present;    // n flags (Some/None), or null: all Some when ctx_off set
+  const uint64_t* ctx_end = nullptr;  // non-null: entry i's context ends at ctx_end[i], not at
+                                      // ctx_off[i + 1] (gathered entries: the density probe)
   const StrobeSnap* prefix;      // [0] after Transcript::new(), [1] after append_parameters
   uint32_t* c_out;               // n x 8 words
   uint8_t* status_out;           // n (written when s != null)
@@ -70,6 +72,22 @@ struct ParseArgs {
   uint32_t* s;
   uint8_t* code;                 // n ParseCode
   uint32_t* aux;                 // n message values (length / version / trailing count), or null
+};
+
+// The batch check's density probe (runtime.hip, launch_probe): kProbeChunks chunks of `blk`
+// proofs at `starts`, gathered into contiguous rows (5 x 32 B per proof) and, with contexts,
+// per-entry [begin, end) offsets into the batch's own context blob and presence flags.
+constexpr int kProbeChunks = 16;
+struct ProbeGatherArgs {
+  int64_t starts[kProbeChunks];
+  int blk;
+  const uint32_t* rows[5];       // the batch's y1, y2, r1, r2, s
+  uint32_t* out_rows[5];         // kProbeChunks * blk rows each
+  const uint64_t* ctx_off;       // the batch's n + 1 offsets, or null
+  const uint8_t* ctx_present;    // the batch's flags, or null
+  uint64_t* out_begin;           // kProbeChunks * blk each (when ctx_off is set)
+  uint64_t* out_end;
+  uint8_t* out_present;
 };
 
 struct VerifyArgs {
@@ -111,6 +129,7 @@ struct ProveArgs {
 
 hipError_t launch_transcript_prefix(const uint32_t* gh_words, StrobeSnap* out, hipStream_t st);
 hipError_t launch_challenge(const ChallengeArgs& a, hipStream_t st);
+hipError_t launch_probe_gather(const ProbeGatherArgs& a, hipStream_t st);
 bool challenge_prefix_is_fixed(const StrobeSnap& snap);  // the no-context fast path applies
 bool challenge_prefix_is_ctx32(const StrobeSnap& snap);  // prefix[0]: the 32-byte-context fast path applies
 hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, hipStream_t st);

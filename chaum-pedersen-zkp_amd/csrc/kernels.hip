@@ -129,7 +129,8 @@ __global__ void __launch_bounds__(kChallengeBlock) k_challenge(ChallengeArgs a) 
   load_words8(y2, a.y2, i);
   load_words8(r1, a.r1, i);
   load_words8(r2, a.r2, i);
-  const uint64_t b0 = has_ctx ? a.ctx_off[i] : 0, b1 = has_ctx ? a.ctx_off[i + 1] : 0;
+  const uint64_t b0 = has_ctx ? a.ctx_off[i] : 0;
+  const uint64_t b1 = has_ctx ? (a.ctx_end ? a.ctx_end[i] : a.ctx_off[i + 1]) : 0;
   // Entries on a fixed schedule skip the LDS sponge: no context (k_challenge_noctx's tail)
   // or a 4-byte-aligned 32-byte context (the service's challenge ids).
   const bool fixed_noctx = !has_ctx && a.fast_noctx;
@@ -535,6 +536,31 @@ hipError_t launch_challenge(const ChallengeArgs& a, hipStream_t st) {
   }
   const int64_t blocks = (a.n + kChallengeBlock - 1) / kChallengeBlock;
   hipLaunchKernelGGL(k_challenge, dim3((unsigned)blocks), dim3(kChallengeBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+// One thread per gathered proof: its five rows (two 16-byte loads each) and, with contexts,
+// its context's [begin, end) in the batch's blob and its presence flag.
+__global__ void __launch_bounds__(256) k_probe_gather(ProbeGatherArgs a) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= kProbeChunks * a.blk) return;
+  const int64_t src = a.starts[j / a.blk] + j % a.blk;
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    uint32_t w[8];
+    load_words8(w, a.rows[q], src);
+    store_words8(a.out_rows[q], j, w);
+  }
+  if (a.ctx_off) {
+    a.out_begin[j] = a.ctx_off[src];
+    a.out_end[j] = a.ctx_off[src + 1];
+    a.out_present[j] = a.ctx_present ? a.ctx_present[src] : (uint8_t)1;
+  }
+}
+
+hipError_t launch_probe_gather(const ProbeGatherArgs& a, hipStream_t st) {
+  const int m = kProbeChunks * a.blk;
+  hipLaunchKernelGGL(k_probe_gather, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

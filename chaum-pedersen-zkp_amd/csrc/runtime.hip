@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -77,15 +78,28 @@ struct DevBuf {
 // the verify streams (whose launches must overlap) stay concurrent whatever other streams
 // the process creates.  Such a stream synchronises with the legacy default stream
 // (hipStreamDefault semantics), which only adds ordering.
-hipError_t stream_own_queue(hipStream_t* s, int cus) {
-  std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
-  for (int c = 0; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
-  hipError_t e = hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
-  if (e != hipSuccess) {
+//
+// Dedicated queues are capped per device (kMaxOwnQueues for the whole process): several
+// contexts per GPU (a pool, the multi-context entry points) would otherwise claim 4 queues
+// each and oversubscribe the hardware scheduler's queue slots.  Contexts take them in the
+// order they create streams -- the context stream at creation, the verify stream with the
+// first verify, the probe and copy streams last -- and streams beyond the cap are plain.
+constexpr int kMaxOwnQueues = 16;
+std::atomic<int> g_own_queues[64];
+
+hipError_t stream_own_queue(hipStream_t* s, int cus, int device, int* taken) {
+  std::atomic<int>* slot = device >= 0 && device < 64 ? &g_own_queues[device] : nullptr;
+  if (slot && slot->fetch_add(1) < kMaxOwnQueues) {
+    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+    for (int c = 0; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
+    if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
+      *taken += 1;
+      return hipSuccess;
+    }
     (void)hipGetLastError();
-    e = hipStreamCreateWithFlags(s, hipStreamDefault);
   }
-  return e;
+  if (slot) slot->fetch_sub(1);
+  return hipStreamCreateWithFlags(s, hipStreamDefault);
 }
 
 // Host-buffer pipeline chunk (proofs): 2^17 proofs = 20 MiB of inputs, ~2.8 ms of verify work.
@@ -126,6 +140,33 @@ struct RlcMsmSet {
   }
 };
 
+// Fixed-base tables and transcript prefix of one (g, h) pair (ensure_generators).
+struct GenSet {
+  bool valid = false;
+  uint64_t used = 0;  // LRU stamp
+  uint8_t gh[64];
+  DevBuf tab;       // 4 x 128 ge_niels (g, h, 2^128 g, 2^128 h)
+  DevBuf comb;      // fixed-base combs of g and h: 2 x 16 x 2^15 ge_niels (128 MiB)
+  DevBuf comb_q;    // 32 ge_p3: 2^(16 k) g, 2^(16 k) h
+  DevBuf prefix;    // 2 StrobeSnap
+  DevBuf gh_words;  // 16 words
+  bool prefix_fixed = false;  // prefix[1] at the fixed position: k_challenge_noctx applies
+  uint32_t chal_k1[50], chal_k2[50];  // its framing masks
+  bool ctx32_fixed = false;   // prefix[0] at the fixed position: 32-byte contexts' fast path
+  uint32_t chal_c32[3][50];   // its framing masks (g and h folded in)
+  void release() {
+    for (DevBuf* b : {&tab, &comb, &comb_q, &prefix, &gh_words}) b->release();
+    valid = false;
+  }
+};
+
+// (g, h) pairs whose tables a context keeps (128 MiB of combs each): a service verifying
+// batches of several Parameters groups rebuilds nothing while it uses at most this many.
+#ifndef CPZ_GEN_CACHE
+#define CPZ_GEN_CACHE 4
+#endif
+constexpr int kGenCache = CPZ_GEN_CACHE;
+
 }  // namespace
 
 struct cpz_ctx {
@@ -134,18 +175,10 @@ struct cpz_ctx {
   int verify_blocks_per_cu = 2;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  // (g, h) cache
-  bool have_gh = false;
-  uint8_t gh[64];
-  DevBuf tab;       // 4 x 128 ge_niels (g, h, 2^128 g, 2^128 h)
-  DevBuf comb;      // fixed-base combs of g and h: 2 x 16 x 2^15 ge_niels (128 MiB)
-  DevBuf comb_q;    // 32 ge_p3: 2^(16 k) g, 2^(16 k) h
-  DevBuf prefix;    // 2 StrobeSnap
-  bool prefix_fixed = false;  // prefix[1] at the fixed position: k_challenge_noctx applies
-  uint32_t chal_k1[50], chal_k2[50];  // its framing masks
-  bool ctx32_fixed = false;   // prefix[0] at the fixed position: 32-byte contexts' fast path
-  uint32_t chal_c32[3][50];   // its framing masks (g and h folded in)
-  DevBuf gh_words;  // 16 words
+  // fixed-base tables of the kGenCache most recently used (g, h) pairs; `gs` is the current one
+  GenSet gen[kGenCache];
+  GenSet* gs = nullptr;
+  uint64_t gen_clock = 0;
   DevBuf ok_flags;  // 2 ints
   // work buffers
   DevBuf c;         // n x 32
@@ -179,8 +212,13 @@ struct cpz_ctx {
   DevBuf pt_lists, pt_offs, pt_wsum, pt_part, pt_fail, pt_tmp, pt_blocks, pt_assign;
   // what the last batch call's fallback did (cpz_ctx_fallback_stats)
   uint64_t fb_stats[CPZ_FALLBACK_STATS] = {};
-  // commitment checks (statuses 4 and 5: the Proof::from_bytes rejections); off = equations only
+  // commitment checks (statuses 4 and 5: the Proof::from_bytes rejections); off = equations only.
+  // eq_only is the context's mode (cpz_ctx_set_commitment_checks); call_eq the mode of the call
+  // in progress (CallLock: the context's, or equations only for that call alone).
   bool eq_only = false;
+  bool call_eq = false;
+  // streams this context created on hardware queues of their own (released with it)
+  int own_queues = 0;
   // Completion of the last call's work on whatever stream it used: the *_device entry points
   // return without synchronising, and their kernels read context buffers (comb, tab, prefix,
   // c, scratch, RLC buffers) that the next call may rewrite on another stream.
@@ -194,6 +232,16 @@ struct cpz_ctx {
 };
 
 namespace {
+
+// One call's hold on the context: its mutex for the whole call, and the call's commitment-check
+// mode -- the context's (cpz_ctx_set_commitment_checks), or equations only for this call alone
+// (CPZ_CALL_EQUATIONS_ONLY), so callers sharing a context never change each other's mode.
+struct CallLock {
+  std::lock_guard<std::mutex> hold;
+  explicit CallLock(cpz_ctx* ctx, uint32_t flags = 0) : hold(ctx->mu) {
+    ctx->call_eq = ctx->eq_only || (flags & CPZ_CALL_EQUATIONS_ONLY) != 0;
+  }
+};
 
 hipEvent_t take_event(cpz_ctx* ctx) {
   if (!ctx->free_events.empty()) {
@@ -248,61 +296,74 @@ void words_from_bytes(uint32_t w[16], const uint8_t g[32], const uint8_t h[32]) 
   std::memcpy(w + 8, h, 32);
 }
 
+// Make the tables of (g, h) current: a cached set is reused, otherwise the least recently
+// used set (an unused one first) is rebuilt -- k_build_niels, k_transcript_prefix and the
+// 128 MiB combs (~3 ms), timed as stage 7 when timing is on.
 int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32]) {
-  if (ctx->have_gh && std::memcmp(ctx->gh, g, 32) == 0 && std::memcmp(ctx->gh + 32, h, 32) == 0) return CPZ_OK;
+  uint8_t both[64];
+  std::memcpy(both, g, 32);
+  std::memcpy(both + 32, h, 32);
+  GenSet* victim = nullptr;
+  for (GenSet& e : ctx->gen) {
+    if (e.valid && std::memcmp(e.gh, both, 64) == 0) {
+      e.used = ++ctx->gen_clock;
+      ctx->gs = &e;
+      return CPZ_OK;
+    }
+    if (!victim || (!e.valid && victim->valid) || (e.valid == victim->valid && e.used < victim->used)) victim = &e;
+  }
   // Parameters::with_generators (gadgets.rs:77-103): valid, non-identity, distinct.
   static const uint8_t zero[32] = {0};
   if (std::memcmp(g, zero, 32) == 0 || std::memcmp(h, zero, 32) == 0)
     return fail(CPZ_EGENERATOR, "generator cannot be identity");
   if (std::memcmp(g, h, 32) == 0) return fail(CPZ_EGENERATOR, "generators g and h must be different");
-  // the tables are about to be rebuilt: no earlier call's kernels may still be reading them
+  // a set is about to be rebuilt: no earlier call's kernels may still be reading it
   if (ctx->have_last) CPZ_HIP(hipEventSynchronize(ctx->last_done));
-  CPZ_HIP(ctx->tab.ensure(4 * cpz::kNielsEntries * sizeof(cpz::ge_niels)));  // g, h, 2^128 g, 2^128 h
-  CPZ_HIP(ctx->prefix.ensure(2 * sizeof(cpz::StrobeSnap)));
-  CPZ_HIP(ctx->gh_words.ensure(64));
+  GenSet& e = *victim;
+  e.valid = false;
+  if (ctx->gs == &e) ctx->gs = nullptr;
+  StageTimer timer(ctx, 7, ctx->stream);
+  CPZ_HIP(e.tab.ensure(4 * cpz::kNielsEntries * sizeof(cpz::ge_niels)));  // g, h, 2^128 g, 2^128 h
+  CPZ_HIP(e.prefix.ensure(2 * sizeof(cpz::StrobeSnap)));
+  CPZ_HIP(e.gh_words.ensure(64));
   CPZ_HIP(ctx->ok_flags.ensure(2 * sizeof(int)));
-  uint8_t both[64];
-  std::memcpy(both, g, 32);
-  std::memcpy(both + 32, h, 32);
-  CPZ_HIP(hipMemcpyAsync(ctx->gh_words.p, both, 64, hipMemcpyHostToDevice, ctx->stream));
-  CPZ_HIP(cpz::launch_build_niels(static_cast<const uint32_t*>(ctx->gh_words.p), 2,
-                                  static_cast<cpz::ge_niels*>(ctx->tab.p), static_cast<int*>(ctx->ok_flags.p),
-                                  ctx->stream));
-  CPZ_HIP(cpz::launch_transcript_prefix(static_cast<const uint32_t*>(ctx->gh_words.p),
-                                        static_cast<cpz::StrobeSnap*>(ctx->prefix.p), ctx->stream));
+  CPZ_HIP(hipMemcpyAsync(e.gh_words.p, both, 64, hipMemcpyHostToDevice, ctx->stream));
+  CPZ_HIP(cpz::launch_build_niels(static_cast<const uint32_t*>(e.gh_words.p), 2, static_cast<cpz::ge_niels*>(e.tab.p),
+                                  static_cast<int*>(ctx->ok_flags.p), ctx->stream));
+  CPZ_HIP(cpz::launch_transcript_prefix(static_cast<const uint32_t*>(e.gh_words.p),
+                                        static_cast<cpz::StrobeSnap*>(e.prefix.p), ctx->stream));
   int ok[2] = {0, 0};
   cpz::StrobeSnap snap[2];
   CPZ_HIP(hipMemcpyAsync(ok, ctx->ok_flags.p, sizeof(ok), hipMemcpyDeviceToHost, ctx->stream));
-  CPZ_HIP(hipMemcpyAsync(snap, ctx->prefix.p, sizeof(snap), hipMemcpyDeviceToHost, ctx->stream));
+  CPZ_HIP(hipMemcpyAsync(snap, e.prefix.p, sizeof(snap), hipMemcpyDeviceToHost, ctx->stream));
   CPZ_HIP(hipStreamSynchronize(ctx->stream));
-  ctx->prefix_fixed = cpz::challenge_prefix_is_fixed(snap[1]) && cpz::challenge_masks(ctx->chal_k1, ctx->chal_k2);
+  if (!ok[0] || !ok[1]) return fail(CPZ_EGENERATOR, "generator encoding does not decode to a ristretto255 point");
+  e.prefix_fixed = cpz::challenge_prefix_is_fixed(snap[1]) && cpz::challenge_masks(e.chal_k1, e.chal_k2);
   {
     uint32_t gw[16];
     words_from_bytes(gw, g, h);
-    ctx->ctx32_fixed = cpz::challenge_prefix_is_ctx32(snap[0]) && cpz::challenge_masks_ctx32(ctx->chal_c32, gw, gw + 8);
+    e.ctx32_fixed = cpz::challenge_prefix_is_ctx32(snap[0]) && cpz::challenge_masks_ctx32(e.chal_c32, gw, gw + 8);
   }
-  if (!ok[0] || !ok[1]) {
-    ctx->have_gh = false;
-    return fail(CPZ_EGENERATOR, "generator encoding does not decode to a ristretto255 point");
-  }
-  CPZ_HIP(ctx->comb.ensure((size_t)2 * cpz::kCombPerBase * sizeof(cpz::ge_niels)));
-  CPZ_HIP(ctx->comb_q.ensure((size_t)2 * cpz::kCombWindows * sizeof(cpz::ge_p3)));
-  CPZ_HIP(cpz::launch_build_comb(static_cast<const uint32_t*>(ctx->gh_words.p), static_cast<cpz::ge_p3*>(ctx->comb_q.p),
-                                 static_cast<cpz::ge_niels*>(ctx->comb.p), ctx->stream));
+  CPZ_HIP(e.comb.ensure((size_t)2 * cpz::kCombPerBase * sizeof(cpz::ge_niels)));
+  CPZ_HIP(e.comb_q.ensure((size_t)2 * cpz::kCombWindows * sizeof(cpz::ge_p3)));
+  CPZ_HIP(cpz::launch_build_comb(static_cast<const uint32_t*>(e.gh_words.p), static_cast<cpz::ge_p3*>(e.comb_q.p),
+                                 static_cast<cpz::ge_niels*>(e.comb.p), ctx->stream));
   CPZ_HIP(hipStreamSynchronize(ctx->stream));  // callers may launch on another stream
-  std::memcpy(ctx->gh, both, 64);
-  ctx->have_gh = true;
+  std::memcpy(e.gh, both, 64);
+  e.valid = true;
+  e.used = ++ctx->gen_clock;
+  ctx->gs = &e;
   return CPZ_OK;
 }
 
 // The fixed-schedule challenge paths and their masks (set per (g, h) by ensure_generators).
 void set_challenge_schedules(const cpz_ctx* ctx, cpz::ChallengeArgs& ca) {
-  ca.eq_only = ctx->eq_only ? 1 : 0;
-  ca.fast_noctx = ctx->prefix_fixed ? 1 : 0;
-  std::memcpy(ca.k1, ctx->chal_k1, sizeof(ca.k1));
-  std::memcpy(ca.k2, ctx->chal_k2, sizeof(ca.k2));
-  ca.fast_ctx32 = ctx->ctx32_fixed ? 1 : 0;
-  std::memcpy(ca.c32, ctx->chal_c32, sizeof(ca.c32));
+  ca.eq_only = ctx->call_eq ? 1 : 0;
+  ca.fast_noctx = ctx->gs->prefix_fixed ? 1 : 0;
+  std::memcpy(ca.k1, ctx->gs->chal_k1, sizeof(ca.k1));
+  std::memcpy(ca.k2, ctx->gs->chal_k2, sizeof(ca.k2));
+  ca.fast_ctx32 = ctx->gs->ctx32_fixed ? 1 : 0;
+  std::memcpy(ca.c32, ctx->gs->chal_c32, sizeof(ca.c32));
 }
 
 // Resident k_verify_each blocks on the whole chip (occupancy-limited).
@@ -368,7 +429,7 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
     if (!ctx->aux_start) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_start, hipEventDisableTiming));
     CPZ_HIP(hipEventRecord(ctx->aux_start, st));  // the aux streams start after st's prior work
     for (int k = 0; k < nst - 1; k++) {
-      if (!ctx->aux_stream[k]) CPZ_HIP(stream_own_queue(&ctx->aux_stream[k], ctx->cus));
+      if (!ctx->aux_stream[k]) CPZ_HIP(stream_own_queue(&ctx->aux_stream[k], ctx->cus, ctx->device, &ctx->own_queues));
       if (!ctx->aux_done[k]) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_done[k], hipEventDisableTiming));
       CPZ_HIP(hipStreamWaitEvent(ctx->aux_stream[k], ctx->aux_start, 0));
     }
@@ -399,6 +460,7 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
       cc.c_out = ca->c_out + 8 * a;
       cc.status_out = ca->status_out + a;
       if (ca->ctx_off) cc.ctx_off = ca->ctx_off + a;  // absolute offsets into ctx_bytes
+      if (ca->ctx_end) cc.ctx_end = ca->ctx_end + a;
       if (ca->ctx_present) cc.ctx_present = ca->ctx_present + a;
       StageTimer tc(ctx, 0, sc);
       CPZ_HIP(cpz::launch_challenge(cc, sc));
@@ -411,11 +473,11 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
 }
 
 // Challenge + verify of n proofs on `st`.  c_buf: where the challenges go (default: the
-// context's buffer from offset 0); rr / join: see VerifyRR.
+// context's buffer from offset 0); rr / join: see VerifyRR; ctx_end: see ChallengeArgs.
 int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
                    const void* s, const void* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
                    uint8_t* status, hipStream_t st, uint32_t* c_buf = nullptr, VerifyRR* rr = nullptr,
-                   bool join = true) {
+                   bool join = true, const uint64_t* ctx_end = nullptr) {
   if (!c_buf) {
     CPZ_HIP(ctx->c.ensure(n * 32));
     c_buf = static_cast<uint32_t*>(ctx->c.p);
@@ -423,7 +485,7 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   cpz::ChallengeArgs ca;
   set_challenge_schedules(ctx, ca);
   ca.n = (int64_t)n;
-  words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
+  words_from_bytes(ca.gh_words, ctx->gs->gh, ctx->gs->gh + 32);
   ca.y1 = static_cast<const uint32_t*>(y1);
   ca.y2 = static_cast<const uint32_t*>(y2);
   ca.r1 = static_cast<const uint32_t*>(r1);
@@ -432,7 +494,8 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   ca.ctx_bytes = static_cast<const uint8_t*>(ctx_bytes);
   ca.ctx_off = ctx_off;
   ca.ctx_present = ctx_present;
-  ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->prefix.p);
+  ca.ctx_end = ctx_end;
+  ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->gs->prefix.p);
   ca.c_out = c_buf;
   ca.status_out = status;
   cpz::VerifyArgs va;
@@ -444,7 +507,7 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   va.s = ca.s;
   va.c = ca.c_out;
   va.status = status;
-  va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
+  va.comb = static_cast<const cpz::ge_niels*>(ctx->gs->comb.p);
   va.scratch = nullptr;  // set per launch
   va.eq_only = ca.eq_only;
   StageTimer span(ctx, 5, st);  // all chunks, all streams (the launches overlap)
@@ -610,7 +673,7 @@ int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t part
       for (int k = 0; k < got; k++)
         if (marks[k]) ctx->free_events.push_back(marks[k]);
     CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_prep.bsum.p), b0, b1,
-                                static_cast<const cpz::ge_niels*>(ctx->tab.p), st, timed ? marks : nullptr));
+                                static_cast<const cpz::ge_niels*>(ctx->gs->tab.p), st, timed ? marks : nullptr));
     if (timed)
       for (int k = 0; k + 1 < cpz::kRlcMsmMarks; k++) ctx->marks.push_back({8 + k, marks[k], marks[k + 1]});
   }
@@ -630,7 +693,7 @@ int batch_challenges(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, con
   cpz::ChallengeArgs ca;
   set_challenge_schedules(ctx, ca);
   ca.n = (int64_t)n;
-  words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
+  words_from_bytes(ca.gh_words, ctx->gs->gh, ctx->gs->gh + 32);
   ca.y1 = static_cast<const uint32_t*>(y1);
   ca.y2 = static_cast<const uint32_t*>(y2);
   ca.r1 = static_cast<const uint32_t*>(r1);
@@ -639,7 +702,7 @@ int batch_challenges(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, con
   ca.ctx_bytes = static_cast<const uint8_t*>(ctx_bytes);
   ca.ctx_off = ctx_off;
   ca.ctx_present = ctx_present;
-  ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->prefix.p);
+  ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->gs->prefix.p);
   ca.c_out = static_cast<uint32_t*>(ctx->c.p);
   ca.status_out = status;
   StageTimer t(ctx, 0, st);
@@ -648,10 +711,13 @@ int batch_challenges(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, con
 }
 
 // Decode + weights + points/digits of the whole batch (after batch_challenges).
+// need_msm = false (the partitioned check): the span-sized MSM set is not reserved.
 int rlc_prepare_points(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
-                       const void* s, uint8_t* status, const uint8_t seed[32], uint64_t first_index, hipStream_t st) {
-  int rc = rlc_reserve(ctx, (int64_t)n);
+                       const void* s, uint8_t* status, const uint8_t seed[32], uint64_t first_index, hipStream_t st,
+                       bool need_msm = true) {
+  int rc = need_msm ? rlc_reserve(ctx, (int64_t)n) : rlc_reserve_prepared(ctx->rl_prep, (int64_t)n);
   if (rc) return rc;
+  CPZ_HIP(ctx->rl_flags.ensure(4 * sizeof(int)));
   cpz::RlcPrepArgs pa;
   pa.n = (int64_t)n;
   pa.first_index = first_index;
@@ -667,7 +733,7 @@ int rlc_prepare_points(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, c
   pa.digits = static_cast<int16_t*>(ctx->rl_prep.dig.p);
   pa.dstride = rlc_dstride(ctx->rl_prep.cap);
   pa.block_sums = static_cast<cpz::sc*>(ctx->rl_prep.bsum.p);
-  pa.eq_only = ctx->eq_only ? 1 : 0;
+  pa.eq_only = ctx->call_eq ? 1 : 0;
   pa.any_bad = static_cast<int*>(ctx->rl_flags.p) + 3;
   CPZ_HIP(hipMemsetAsync(pa.any_bad, 0, sizeof(int), st));
   {
@@ -686,24 +752,20 @@ int rlc_prepare(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const vo
   return rlc_prepare_points(ctx, n, y1, y2, r1, r2, s, status, seed, first_index, st);
 }
 
-// Batch-fail fallback (verify_individually, batch.rs:262-268, 314-318): locate the invalid
-// entries of [lo, hi) exactly.  Per-proof work here reuses the prepare's decoded points,
-// challenges and decode-level statuses (k_verify_prepared: the equations only).
-//   * Density probe (ranges >= kProbeMin): per-proof verification of kProbeChunks chunks of
-//     kRlcPrepBlock proofs spread over the range.  Two or more invalid entries in the probe
-//     (density >~ 1 / 2000: every 2^16-proof leaf of a bisection would fail too) -> the whole
-//     range per proof at once; C5's 0.1 % lands here.
-//   * Otherwise bisection: the range is cut in kFanout parts aligned to the weight blocks,
-//     each part's partial is one more MSM over the prepared points, identity parts are
-//     accepted, failing parts recurse; a range is verified per proof when it is <= kLeaf or
-//     when most of its parts fail.
+// Batch-fail fallback by bisection (verify_individually, batch.rs:262-268, 314-318): locate
+// the invalid entries of [lo, hi) exactly, for batches the density probe found sparse (or too
+// small to sample, below kProbeMin).  The range is cut in kFanout parts aligned to the weight
+// blocks, each part's partial is one more MSM over the prepared points, identity parts are
+// accepted, failing parts recurse; a range is verified per proof (k_verify_prepared: the
+// prepare's decoded points, challenges and decode-level statuses, the equations only) when it
+// is <= kLeaf or when most of its parts fail.
 constexpr int64_t kLeaf = 1 << 16;
 constexpr int kFanout = 8;
 constexpr int64_t kProbeMin = 1 << 20;
-constexpr int kProbeChunks = 16;
+using cpz::kProbeChunks;
 
 int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const void* y2, const void* r1, const void* r2,
-                 const void* s, uint8_t* status, hipStream_t st, int depth, bool allow_probe = true) {
+                 const void* s, uint8_t* status, hipStream_t st, int depth) {
   auto per_proof = [&](int64_t a, int64_t b) -> int {
     ctx->fb_stats[4] += (uint64_t)(b - a);
     cpz::VerifyArgs va;
@@ -715,46 +777,13 @@ int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const voi
     va.s = static_cast<const uint32_t*>(s) + 8 * a;
     va.c = static_cast<const uint32_t*>(ctx->c.p) + 8 * a;
     va.status = status + a;  // decode-level status in, final status out
-    va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
+    va.comb = static_cast<const cpz::ge_niels*>(ctx->gs->comb.p);
     va.scratch = nullptr;  // set per launch
-    va.eq_only = ctx->eq_only ? 1 : 0;
+    va.eq_only = ctx->call_eq ? 1 : 0;
     va.pre = static_cast<const cpz::ge_niels*>(ctx->rl_prep.pts.p) + 4 * a;
     return launch_verify_chunks(ctx, va, 4, st, nullptr, true);
   };
   if (hi - lo <= kLeaf || depth > 12) return per_proof(lo, hi);
-  if (depth == 0 && allow_probe && hi - lo >= kProbeMin) {
-    const int64_t blk = cpz::kRlcPrepBlock;
-    const int64_t span = (hi - lo) / kProbeChunks;
-    int64_t starts[kProbeChunks];
-    for (int k = 0; k < kProbeChunks; k++) {
-      starts[k] = lo + ((k * span + span / 2) / blk) * blk;
-      int rc = per_proof(starts[k], std::min(starts[k] + blk, hi));
-      if (rc) return rc;
-    }
-    std::vector<uint8_t> probe((size_t)(kProbeChunks * blk), 0);
-    for (int k = 0; k < kProbeChunks; k++) {
-      const int64_t m = std::min(starts[k] + blk, hi) - starts[k];
-      CPZ_HIP(hipMemcpyAsync(probe.data() + k * blk, status + starts[k], (size_t)m, hipMemcpyDeviceToHost, st));
-    }
-    CPZ_HIP(hipStreamSynchronize(st));
-    int bad = 0;
-    for (uint8_t v : probe) bad += (v == cpz::kStatusEqFail) ? 1 : 0;
-    if (bad >= 2) {
-      // dense: everything per proof (the probe chunks' statuses are final already; the
-      // ranges between them are verified now)
-      int64_t a = lo;
-      for (int k = 0; k < kProbeChunks; k++) {
-        if (starts[k] > a) {
-          int rc = per_proof(a, starts[k]);
-          if (rc) return rc;
-        }
-        a = std::min(starts[k] + blk, hi);
-      }
-      return a < hi ? per_proof(a, hi) : CPZ_OK;
-    }
-    // sparse: the probe chunks are verified; bisection re-verifies them harmlessly
-    // (k_verify_prepared leaves statuses that are already non-zero alone)
-  }
   int64_t cuts[kFanout + 1];
   for (int k = 0; k <= kFanout; k++) {
     int64_t c = lo + ((hi - lo) * k) / kFanout;
@@ -785,31 +814,44 @@ int rlc_fallback(cpz_ctx* ctx, int64_t lo, int64_t hi, const void* y1, const voi
 
 // The density probe of a fallback-enabled batch check, launched BEFORE the prepare on its own
 // stream so that it runs beside it: per-proof verification (challenge + k_verify_each) of
-// kProbeChunks chunks of kRlcPrepBlock proofs spread over the batch, gathered into a small
-// buffer.  Returns the number of chunk starts (0: no probe).
-int launch_probe(cpz_ctx* ctx, size_t n, const void* const rows[5], int64_t starts[kProbeChunks], hipStream_t st) {
+// kProbeChunks chunks of kRlcPrepBlock proofs spread over the batch, gathered by k_probe_gather
+// into one small launch -- the rows, and with contexts each entry's [begin, end) in the batch's
+// own context blob (the challenge kernel reads them through ChallengeArgs::ctx_end), so
+// batches with contexts (the service's, service.rs:512-517) are sampled the same way.
+// Returns the number of chunk starts.
+int launch_probe(cpz_ctx* ctx, size_t n, const void* const rows[5], const void* cb, const uint64_t* co,
+                 const uint8_t* cp, int64_t starts[kProbeChunks], hipStream_t st) {
   const int64_t blk = cpz::kRlcPrepBlock;
   const size_t m = (size_t)kProbeChunks * blk;
-  CPZ_HIP(ctx->probe.ensure(m * (5 * 32 + 32 + 1)));
-  if (!ctx->probe_stream) CPZ_HIP(stream_own_queue(&ctx->probe_stream, ctx->cus));
+  // rows (5 x 32 B), challenges (32 B), statuses (1 B), then context begin / end (2 x 8 B) and
+  // presence (1 B) per sampled entry
+  CPZ_HIP(ctx->probe.ensure(m * (5 * 32 + 32 + 1 + 16 + 1) + 16));
+  if (!ctx->probe_stream) CPZ_HIP(stream_own_queue(&ctx->probe_stream, ctx->cus, ctx->device, &ctx->own_queues));
   if (!ctx->probe_done) CPZ_HIP(hipEventCreateWithFlags(&ctx->probe_done, hipEventDisableTiming));
   if (!ctx->aux_start) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_start, hipEventDisableTiming));
   CPZ_HIP(hipEventRecord(ctx->aux_start, st));  // after everything before this call on st
   CPZ_HIP(hipStreamWaitEvent(ctx->probe_stream, ctx->aux_start, 0));
   uint8_t* base = static_cast<uint8_t*>(ctx->probe.p);
+  cpz::ProbeGatherArgs ga;
   const int64_t span = (int64_t)n / kProbeChunks;
-  for (int k = 0; k < kProbeChunks; k++) {
-    starts[k] = ((k * span + span / 2) / blk) * blk;
-    for (int q = 0; q < 5; q++)
-      CPZ_HIP(hipMemcpyAsync(base + (q * m + (size_t)k * blk) * 32, static_cast<const uint8_t*>(rows[q]) + starts[k] * 32,
-                             (size_t)blk * 32, hipMemcpyDeviceToDevice, ctx->probe_stream));
+  for (int k = 0; k < kProbeChunks; k++) ga.starts[k] = starts[k] = ((k * span + span / 2) / blk) * blk;
+  ga.blk = (int)blk;
+  for (int q = 0; q < 5; q++) {
+    ga.rows[q] = static_cast<const uint32_t*>(rows[q]);
+    ga.out_rows[q] = reinterpret_cast<uint32_t*>(base + q * m * 32);
   }
-  uint8_t* prow[5];
-  for (int q = 0; q < 5; q++) prow[q] = base + q * m * 32;
   uint32_t* pc = reinterpret_cast<uint32_t*>(base + 5 * m * 32);
   uint8_t* pst = base + 6 * m * 32;
-  int rc = enqueue_verify(ctx, m, prow[0], prow[1], prow[2], prow[3], prow[4], nullptr, nullptr, nullptr, pst,
-                          ctx->probe_stream, pc);
+  uint64_t* pbeg = reinterpret_cast<uint64_t*>(base + ((6 * m * 32 + m + 15) & ~(size_t)15));
+  ga.ctx_off = co;
+  ga.ctx_present = cp;
+  ga.out_begin = pbeg;
+  ga.out_end = pbeg + m;
+  ga.out_present = reinterpret_cast<uint8_t*>(pbeg + 2 * m);
+  CPZ_HIP(cpz::launch_probe_gather(ga, ctx->probe_stream));
+  int rc = enqueue_verify(ctx, m, ga.out_rows[0], ga.out_rows[1], ga.out_rows[2], ga.out_rows[3], ga.out_rows[4],
+                          co ? cb : nullptr, co ? ga.out_begin : nullptr, co ? ga.out_present : nullptr, pst,
+                          ctx->probe_stream, pc, nullptr, true, co ? ga.out_end : nullptr);
   if (rc) return rc;
   CPZ_HIP(hipEventRecord(ctx->probe_done, ctx->probe_stream));
   return kProbeChunks;
@@ -831,7 +873,7 @@ int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* stat
     if (!ctx->aux_start) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_start, hipEventDisableTiming));
     CPZ_HIP(hipEventRecord(ctx->aux_start, st));
     for (int k = 0; k < nst - 1; k++) {
-      if (!ctx->aux_stream[k]) CPZ_HIP(stream_own_queue(&ctx->aux_stream[k], ctx->cus));
+      if (!ctx->aux_stream[k]) CPZ_HIP(stream_own_queue(&ctx->aux_stream[k], ctx->cus, ctx->device, &ctx->own_queues));
       if (!ctx->aux_done[k]) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_done[k], hipEventDisableTiming));
       CPZ_HIP(hipStreamWaitEvent(ctx->aux_stream[k], ctx->aux_start, 0));
     }
@@ -841,9 +883,9 @@ int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* stat
   va.s = static_cast<const uint32_t*>(s);
   va.c = static_cast<const uint32_t*>(ctx->c.p);
   va.status = status;
-  va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
+  va.comb = static_cast<const cpz::ge_niels*>(ctx->gs->comb.p);
   va.pre = static_cast<const cpz::ge_niels*>(ctx->rl_prep.pts.p);
-  va.eq_only = ctx->eq_only ? 1 : 0;
+  va.eq_only = ctx->call_eq ? 1 : 0;
   for (int64_t c = 0; c < chunks; c++) {
     const int64_t g0 = c * full;
     const int g = (int)std::min<int64_t>(full, nb - g0);
@@ -875,12 +917,16 @@ constexpr int64_t kPartChunkBlocks = 65536;
 // half the blocks fail and plain per-proof verification is cheaper.
 constexpr int kPartMaxProbeBad = 12;
 
-// The partitioned fallback over the prepared batch: every block's partial (k_part_*), the
-// batch partial as their sum, and per-proof verification of the failing blocks only.
-int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, uint8_t partial[32], int* identity,
-                  hipStream_t st) {
+// Every buffer the partitioned check of n proofs uses: the prepared batch, the partial / flag
+// words of an MSM set, one chunk's sorted lists / assignment / offsets, and the whole batch's
+// window sums, partials, fail flags and failing-block list.  A failure leaves CPZ_ENOMEM (or the
+// HIP error) with no partial state: part_release frees the partitioned buffers.
+int part_reserve(cpz_ctx* ctx, int64_t n) {
   const int64_t nblk = (n + cpz::kPartProofs - 1) / cpz::kPartProofs;
   const int64_t chunk = std::min<int64_t>(nblk, kPartChunkBlocks);
+  if (int rc = rlc_reserve_prepared(ctx->rl_prep, n)) return rc;
+  if (int rc = rlc_reserve_msm(ctx->rl_msm, 1)) return rc;  // its partial / flag words
+  CPZ_HIP(ctx->rl_flags.ensure(4 * sizeof(int)));
   CPZ_HIP(ctx->pt_lists.ensure((size_t)chunk * cpz::kPartListCap * sizeof(uint16_t)));
   CPZ_HIP(ctx->pt_assign.ensure((size_t)chunk * cpz::kPartUnits * sizeof(uint16_t)));
   CPZ_HIP(ctx->pt_offs.ensure((size_t)chunk * cpz::kPartOffs * sizeof(uint16_t)));
@@ -889,7 +935,24 @@ int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, uin
   CPZ_HIP(ctx->pt_fail.ensure((size_t)nblk));
   CPZ_HIP(ctx->pt_tmp.ensure((size_t)((nblk + 63) / 64 + 16) * sizeof(cpz::ge_p3)));
   CPZ_HIP(ctx->pt_blocks.ensure((size_t)nblk * sizeof(uint32_t)));
-  if (int rc = rlc_reserve_msm(ctx->rl_msm, 1)) return rc;  // its partial / flag words
+  return CPZ_OK;
+}
+
+void part_release(cpz_ctx* ctx) {
+  for (DevBuf* b : {&ctx->pt_lists, &ctx->pt_offs, &ctx->pt_wsum, &ctx->pt_part, &ctx->pt_fail, &ctx->pt_tmp,
+                    &ctx->pt_blocks, &ctx->pt_assign})
+    b->release();
+  ctx->rl_prep.release();
+  (void)hipGetLastError();
+}
+
+// The partitioned fallback over the prepared batch (buffers from part_reserve): every block's
+// partial (k_part_*), the batch partial as their sum, and per-proof verification of the
+// failing blocks only.
+int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, uint8_t partial[32], int* identity,
+                  hipStream_t st) {
+  const int64_t nblk = (n + cpz::kPartProofs - 1) / cpz::kPartProofs;
+  const int64_t chunk = std::min<int64_t>(nblk, kPartChunkBlocks);
   {
     StageTimer t(ctx, 3, st);
     cpz::PartArgs pa;
@@ -898,7 +961,7 @@ int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, uin
     pa.digits = static_cast<const int16_t*>(ctx->rl_prep.dig.p);
     pa.dstride = rlc_dstride(ctx->rl_prep.cap);
     pa.block_sums = static_cast<const cpz::sc*>(ctx->rl_prep.bsum.p);
-    pa.tab = static_cast<const cpz::ge_niels*>(ctx->tab.p);
+    pa.tab = static_cast<const cpz::ge_niels*>(ctx->gs->tab.p);
     pa.lists = static_cast<uint16_t*>(ctx->pt_lists.p);
     pa.assign = static_cast<uint16_t*>(ctx->pt_assign.p);
     pa.offs = static_cast<uint16_t*>(ctx->pt_offs.p);
@@ -944,8 +1007,8 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
                       const void* s, const void* cb, const uint64_t* co, const uint8_t* cp, uint8_t* d_status,
                       const uint8_t seed[32], uint64_t first_index, uint8_t partial_out[32], int* batch_ok,
                       int fallback, uint8_t* host_status, hipStream_t st) {
-  // A fallback-enabled check of a large batch without contexts first samples its density,
-  // beside the batch's challenges (the probe's ~0.5 ms of per-proof latency hides under
+  // A fallback-enabled check of a large batch (with or without contexts) first samples its
+  // density, beside the batch's challenges (the probe's ~0.5 ms of per-proof latency hides under
   // them).  Two or more invalid entries among the kProbeChunks x 256 sampled: the batch
   // cannot pass and bisection cannot prune it (every range of a few thousand proofs fails).
   //   * up to kPartMaxProbeBad sampled (density up to ~0.3 %, configs[4]'s 0.1 %): the
@@ -956,10 +1019,10 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
   //     encoding) -- the cost of the per-proof path plus the probe.
   for (auto& v : ctx->fb_stats) v = 0;
   int64_t starts[kProbeChunks];
-  const bool probe = fallback && co == nullptr && (int64_t)n >= kProbeMin;
+  const bool probe = fallback && (int64_t)n >= kProbeMin;
   if (probe) {
     const void* rows[5] = {y1, y2, r1, r2, s};
-    int rc = launch_probe(ctx, n, rows, starts, st);
+    int rc = launch_probe(ctx, n, rows, cb, co, cp, starts, st);
     if (rc < 0) return rc;
   }
   int rc = batch_challenges(ctx, n, y1, y2, r1, r2, s, cb, co, cp, d_status, st);
@@ -974,9 +1037,16 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
     int bad = 0;
     for (uint8_t v : pst) bad += (v == cpz::kStatusEqFail) ? 1 : 0;
     ctx->fb_stats[1] = (uint64_t)bad;
+    // The partitioned check's buffers (the prepared batch, ~40 KB of window sums per block,
+    // one chunk's sorted lists) are reserved first; if the device cannot hold them they are
+    // released and the batch takes the per-proof path, which needs no extra memory.
+    if (bad >= 2 && bad <= kPartMaxProbeBad && part_reserve(ctx, (int64_t)n) != CPZ_OK) {
+      part_release(ctx);
+      bad = kPartMaxProbeBad + 1;
+    }
     if (bad >= 2 && bad <= kPartMaxProbeBad) {
       ctx->fb_stats[0] = CPZ_FALLBACK_PARTITIONED;
-      if ((rc = rlc_prepare_points(ctx, n, y1, y2, r1, r2, s, d_status, seed, first_index, st))) return rc;
+      if ((rc = rlc_prepare_points(ctx, n, y1, y2, r1, r2, s, d_status, seed, first_index, st, false))) return rc;
       uint8_t part[32];
       int ident = 0;
       if ((rc = part_fallback(ctx, (int64_t)n, s, d_status, part, &ident, st))) return rc;
@@ -1002,9 +1072,9 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
       va.s = static_cast<const uint32_t*>(s);
       va.c = static_cast<const uint32_t*>(ctx->c.p);
       va.status = d_status;  // response statuses from batch_challenges -> final statuses
-      va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
+      va.comb = static_cast<const cpz::ge_niels*>(ctx->gs->comb.p);
       va.scratch = nullptr;  // set per launch
-      va.eq_only = ctx->eq_only ? 1 : 0;
+      va.eq_only = ctx->call_eq ? 1 : 0;
       {
         StageTimer span(ctx, 4, st);  // wall time of the fallback; launches timed as verify_each
         if ((rc = launch_verify_chunks(ctx, va, 1, st, nullptr, true))) return rc;
@@ -1031,7 +1101,7 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
   if (batch_ok) *batch_ok = (ident && all_live) ? 1 : 0;
   if (!ident && fallback) {
     ctx->fb_stats[0] = CPZ_FALLBACK_BISECTION;
-    rc = rlc_fallback(ctx, 0, (int64_t)n, y1, y2, r1, r2, s, d_status, st, 0, !probe);
+    rc = rlc_fallback(ctx, 0, (int64_t)n, y1, y2, r1, r2, s, d_status, st, 0);
     if (rc) return rc;
     CPZ_HIP(hipStreamSynchronize(st));  // statuses complete on return (documented)
   }
@@ -1078,7 +1148,7 @@ int ctx_create(int device_ordinal, cpz_ctx** out) {
   // A blocking stream: it orders with the legacy default stream, so work queued by other
   // libraries (e.g. torch's default stream, handle 0, which the C ABI reads as "use the
   // context stream") is ordered with the verifier's kernels in both directions.
-  if (e == hipSuccess) e = stream_own_queue(&ctx->stream, prop.multiProcessorCount);
+  if (e == hipSuccess) e = stream_own_queue(&ctx->stream, prop.multiProcessorCount, device_ordinal, &ctx->own_queues);
   if (e != hipSuccess) {
     delete ctx;
     return fail(CPZ_EHIP, std::string("context setup: ") + hipGetErrorString(e));
@@ -1114,14 +1184,14 @@ int cpz_abi_version(void) { return CPZ_ABI_VERSION; }
 
 int cpz_ctx_fallback_stats(cpz_ctx* ctx, uint64_t out[CPZ_FALLBACK_STATS]) {
   if (!ctx || !out) return fail(CPZ_EINVAL, "null argument");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   std::memcpy(out, ctx->fb_stats, sizeof(ctx->fb_stats));
   return CPZ_OK;
 }
 
 int cpz_ctx_set_commitment_checks(cpz_ctx* ctx, int enable) {
   if (!ctx) return fail(CPZ_EINVAL, "null context");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   ctx->eq_only = enable == 0;
   return CPZ_OK;
 }
@@ -1131,10 +1201,19 @@ int cpz_verify_batch(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], siz
                      const uint8_t* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
                      const uint8_t seed[32], uint64_t first_index, uint8_t partial_out[32], int* batch_ok,
                      uint8_t* status_out) {
+  return cpz_verify_batch_ex(ctx, 0, g, h, n, y1, y2, r1, r2, s, ctx_bytes, ctx_off, ctx_present, seed, first_index,
+                              partial_out, batch_ok, status_out);
+}
+
+int cpz_verify_batch_ex(cpz_ctx* ctx, uint32_t flags, const uint8_t g[32], const uint8_t h[32], size_t n, const uint8_t* y1,
+                     const uint8_t* y2, const uint8_t* r1, const uint8_t* r2, const uint8_t* s,
+                     const uint8_t* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
+                     const uint8_t seed[32], uint64_t first_index, uint8_t partial_out[32], int* batch_ok,
+                     uint8_t* status_out) {
   if (!ctx || !g || !h || !seed) return fail(CPZ_EINVAL, "null context, generators or seed");
   if (n == 0) return fail(CPZ_EEMPTY, "Cannot verify empty batch");
   if (!y1 || !y2 || !r1 || !r2 || !s) return fail(CPZ_EINVAL, "null input pointer");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx, flags);
   CPZ_HIP(hipSetDevice(ctx->device));
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
@@ -1162,7 +1241,7 @@ int cpz_verify_batch_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[3
   if (!d_y1 || !d_y2 || !d_r1 || !d_r2 || !d_s || !d_status_out) return fail(CPZ_EINVAL, "null input pointer");
   if (!aligned16(d_y1) || !aligned16(d_y2) || !aligned16(d_r1) || !aligned16(d_r2) || !aligned16(d_s))
     return fail(CPZ_EINVAL, "device inputs must be 16-byte aligned");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
@@ -1180,11 +1259,11 @@ int cpz_msm(cpz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalar
   if ((int64_t)n + 2 > cpz::kRlcMaxMsmPoints) return fail(CPZ_EINVAL, "too many points for one MSM call");
   for (size_t j = 0; j < n; j++)
     if (scalars[32 * j + 31] & 0xe0) return fail(CPZ_EINVAL, "scalars must be below 2^253");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
   uint8_t g[32], h[32];
   cpz_default_generators(g, h);
-  int rc = ctx->have_gh ? CPZ_OK : ensure_generators(ctx, g, h);
+  int rc = ctx->gs ? CPZ_OK : ensure_generators(ctx, g, h);
   if (rc) return rc;
   if ((rc = order_after_last(ctx, ctx->stream))) return rc;
   // n points occupy the prepared set's point / digit rows from 0 (room for ceil(n / 4)
@@ -1208,7 +1287,7 @@ int cpz_msm(cpz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalar
                                static_cast<int*>(ctx->rl_flags.p) + 2, ctx->stream));
   // the extra points (g, h at e0) get zero scalars: empty block range
   CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_prep.bsum.p), 0, 0,
-                              static_cast<const cpz::ge_niels*>(ctx->tab.p), ctx->stream, nullptr));
+                              static_cast<const cpz::ge_niels*>(ctx->gs->tab.p), ctx->stream, nullptr));
   int flags[3];
   CPZ_HIP(hipMemcpyAsync(out, ctx->rl_msm.partial.p, 32, hipMemcpyDeviceToHost, ctx->stream));
   CPZ_HIP(hipMemcpyAsync(flags, ctx->rl_flags.p, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
@@ -1220,7 +1299,7 @@ int cpz_msm(cpz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalar
 int cpz_decode_points(cpz_ctx* ctx, size_t n, const uint8_t* points, uint8_t* ok_out, uint8_t* reencoded_out) {
   if (!ctx || !points || !ok_out) return fail(CPZ_EINVAL, "null argument");
   if (n == 0) return fail(CPZ_EEMPTY, "empty input");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
   int rc = order_after_last(ctx, ctx->stream);
   if (rc) return rc;
@@ -1247,7 +1326,7 @@ int cpz_combine_partials(cpz_ctx* ctx, size_t k, const uint8_t* partials, uint8_
       if (is_identity) *is_identity = 0;
       return CPZ_OK;
     }
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
   {
     int rc = order_after_last(ctx, ctx->stream);  // rl_flags is shared with the batch path
@@ -1365,7 +1444,7 @@ int cpz_verify_batch_multi(cpz_ctx* const* ctxs, int nctx, const uint8_t g[32], 
 
 int cpz_ctx_set_timing(cpz_ctx* ctx, int enable) {
   if (!ctx) return fail(CPZ_EINVAL, "null context");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   ctx->timing = enable != 0;
   return CPZ_OK;
 }
@@ -1376,7 +1455,7 @@ int cpz_ctx_stage_times(cpz_ctx* ctx, double ms_out[CPZ_NUM_STAGES], int launche
 
 int cpz_ctx_stage_times_n(cpz_ctx* ctx, int nstages, double* ms_out, int* launches_out) {
   if (!ctx || !ms_out || nstages <= 0) return fail(CPZ_EINVAL, "null argument or no stages");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
   for (int k = 0; k < nstages; k++) {
     ms_out[k] = 0.0;
@@ -1416,11 +1495,7 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
     for (auto e : all) (void)hipEventDestroy(e);
   }
   if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
-  ctx->tab.release();
-  ctx->comb.release();
-  ctx->comb_q.release();
-  ctx->prefix.release();
-  ctx->gh_words.release();
+  for (GenSet& e : ctx->gen) e.release();
   ctx->ok_flags.release();
   ctx->c.release();
   ctx->st.release();
@@ -1457,6 +1532,7 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->rl_flags.release();
   ctx->rl_parts.release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->device >= 0 && ctx->device < 64) g_own_queues[ctx->device].fetch_sub(ctx->own_queues);
   delete ctx;
 }
 
@@ -1481,7 +1557,7 @@ int verify_each_pipelined(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], 
   CPZ_HIP(ctx->st.ensure(n));
   CPZ_HIP(ctx->c.ensure(n * 32));  // each chunk's challenges at its own offset
   VerifyRR rr;
-  if (!ctx->copy_stream) CPZ_HIP(stream_own_queue(&ctx->copy_stream, ctx->cus));
+  if (!ctx->copy_stream) CPZ_HIP(stream_own_queue(&ctx->copy_stream, ctx->cus, ctx->device, &ctx->own_queues));
   if (!ctx->copy_done) CPZ_HIP(hipEventCreateWithFlags(&ctx->copy_done, hipEventDisableTiming));
   uint8_t* st = static_cast<uint8_t*>(ctx->st.p);
   for (size_t off = 0; off < n; off += kPipeChunk) {
@@ -1521,7 +1597,7 @@ int cpz_verify_each_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32
   if (!aligned16(d_y1) || !aligned16(d_y2) || !aligned16(d_r1) || !aligned16(d_r2) || !aligned16(d_s))
     return fail(CPZ_EINVAL, "device inputs must be 16-byte aligned");
   if (d_ctx_off && !d_ctx_bytes) return fail(CPZ_EINVAL, "ctx_off given without ctx_bytes");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
@@ -1537,11 +1613,18 @@ int cpz_verify_each(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size
                     const uint8_t* y2, const uint8_t* r1, const uint8_t* r2, const uint8_t* s,
                     const uint8_t* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
                     uint8_t* status_out) {
+  return cpz_verify_each_ex(ctx, 0, g, h, n, y1, y2, r1, r2, s, ctx_bytes, ctx_off, ctx_present, status_out);
+}
+
+int cpz_verify_each_ex(cpz_ctx* ctx, uint32_t flags, const uint8_t g[32], const uint8_t h[32], size_t n, const uint8_t* y1,
+                    const uint8_t* y2, const uint8_t* r1, const uint8_t* r2, const uint8_t* s,
+                    const uint8_t* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
+                    uint8_t* status_out) {
   if (!ctx || !g || !h) return fail(CPZ_EINVAL, "null context or generators");
   if (n == 0) return fail(CPZ_EEMPTY, "Cannot verify empty batch");
   if (!y1 || !y2 || !r1 || !r2 || !s || !status_out) return fail(CPZ_EINVAL, "null input pointer");
   if (ctx_off && !ctx_bytes && ctx_off[n] != ctx_off[0]) return fail(CPZ_EINVAL, "ctx_off given without ctx_bytes");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx, flags);
   CPZ_HIP(hipSetDevice(ctx->device));
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
@@ -1569,7 +1652,7 @@ int cpz_challenges(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_
   if (!ctx || !g || !h) return fail(CPZ_EINVAL, "null context or generators");
   if (n == 0) return fail(CPZ_EEMPTY, "empty input");
   if (!y1 || !y2 || !r1 || !r2 || !c_out) return fail(CPZ_EINVAL, "null input pointer");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
@@ -1585,7 +1668,7 @@ int cpz_challenges(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_
   cpz::ChallengeArgs ca;
   set_challenge_schedules(ctx, ca);
   ca.n = (int64_t)n;
-  words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
+  words_from_bytes(ca.gh_words, ctx->gs->gh, ctx->gs->gh + 32);
   ca.y1 = static_cast<const uint32_t*>(dev[0]);
   ca.y2 = static_cast<const uint32_t*>(dev[1]);
   ca.r1 = static_cast<const uint32_t*>(dev[2]);
@@ -1594,7 +1677,7 @@ int cpz_challenges(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_
   ca.ctx_bytes = static_cast<const uint8_t*>(dcb);
   ca.ctx_off = dco;
   ca.ctx_present = dcp;
-  ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->prefix.p);
+  ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->gs->prefix.p);
   ca.c_out = static_cast<uint32_t*>(ctx->c.p);
   ca.status_out = nullptr;
   CPZ_HIP(cpz::launch_challenge(ca, ctx->stream));
@@ -1610,7 +1693,7 @@ int cpz_parse_proofs_device(cpz_ctx* ctx, size_t n, const void* d_blob, const ui
   if (!d_blob || !d_off || !d_r1 || !d_r2 || !d_s || !d_code) return fail(CPZ_EINVAL, "null input pointer");
   if (!aligned16(d_r1) || !aligned16(d_r2) || !aligned16(d_s))
     return fail(CPZ_EINVAL, "device row outputs must be 16-byte aligned");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   cpz::ParseArgs pa;
@@ -1637,7 +1720,7 @@ int cpz_parse_proofs(cpz_ctx* ctx, size_t n, const uint8_t* blob, const uint64_t
   const size_t bytes = (size_t)(off[n] - off[0]);
   std::vector<uint64_t> rel(n + 1);
   for (size_t i = 0; i <= n; i++) rel[i] = off[i] - off[0];
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
   hipStream_t st = ctx->stream;
   CPZ_HIP(ctx->pz_blob.ensure(bytes + 16));
@@ -1689,7 +1772,7 @@ int prove_impl(cpz_ctx* ctx, size_t n, uint64_t first_index, const uint8_t* seed
   if (seed_k) std::memcpy(pa.seed_k, seed_k, 32);
   pa.x_in = static_cast<const uint32_t*>(d_x);
   pa.k_in = static_cast<const uint32_t*>(d_k);
-  pa.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
+  pa.comb = static_cast<const cpz::ge_niels*>(ctx->gs->comb.p);
   pa.y1 = static_cast<uint32_t*>(d_y1);
   pa.y2 = static_cast<uint32_t*>(d_y2);
   pa.r1 = static_cast<uint32_t*>(d_r1);
@@ -1703,7 +1786,7 @@ int prove_impl(cpz_ctx* ctx, size_t n, uint64_t first_index, const uint8_t* seed
   cpz::ChallengeArgs ca;
   set_challenge_schedules(ctx, ca);
   ca.n = (int64_t)n;
-  words_from_bytes(ca.gh_words, ctx->gh, ctx->gh + 32);
+  words_from_bytes(ca.gh_words, ctx->gs->gh, ctx->gs->gh + 32);
   ca.y1 = pa.y1;
   ca.y2 = pa.y2;
   ca.r1 = pa.r1;
@@ -1712,7 +1795,7 @@ int prove_impl(cpz_ctx* ctx, size_t n, uint64_t first_index, const uint8_t* seed
   ca.ctx_bytes = static_cast<const uint8_t*>(d_ctx_bytes);
   ca.ctx_off = d_ctx_off;
   ca.ctx_present = d_ctx_present;
-  ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->prefix.p);
+  ca.prefix = static_cast<const cpz::StrobeSnap*>(ctx->gs->prefix.p);
   ca.c_out = static_cast<uint32_t*>(ctx->c.p);
   ca.status_out = nullptr;
   StageTimer t(ctx, 6, st);
@@ -1733,7 +1816,7 @@ int prove_host(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
                const uint8_t* seed_x, const uint8_t* seed_k, const uint8_t* x, const uint8_t* k,
                const uint8_t* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present, uint8_t* y1, uint8_t* y2,
                uint8_t* r1, uint8_t* r2, uint8_t* s) {
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
@@ -1771,7 +1854,7 @@ int verify_response_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2,
                          const void* s, const void* c, uint8_t* status, hipStream_t st) {
   CPZ_HIP(ctx->c.ensure(n * 32));
   CPZ_HIP(cpz::launch_response_prep((int64_t)n, static_cast<const uint32_t*>(s), static_cast<const uint32_t*>(c),
-                                    static_cast<uint32_t*>(ctx->c.p), status, ctx->eq_only ? 1 : 0, st));
+                                    static_cast<uint32_t*>(ctx->c.p), status, ctx->call_eq ? 1 : 0, st));
   cpz::VerifyArgs va;
   va.n = (int64_t)n;
   va.y1 = static_cast<const uint32_t*>(y1);
@@ -1781,9 +1864,9 @@ int verify_response_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2,
   va.s = static_cast<const uint32_t*>(s);
   va.c = static_cast<const uint32_t*>(ctx->c.p);
   va.status = status;
-  va.comb = static_cast<const cpz::ge_niels*>(ctx->comb.p);
+  va.comb = static_cast<const cpz::ge_niels*>(ctx->gs->comb.p);
   va.scratch = nullptr;  // set per launch
-  va.eq_only = ctx->eq_only ? 1 : 0;
+  va.eq_only = ctx->call_eq ? 1 : 0;
   StageTimer span(ctx, 5, st);
   return launch_verify_chunks(ctx, va, 1, st, nullptr, true);
 }
@@ -1802,7 +1885,7 @@ int cpz_prove_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], siz
     if (!p) return fail(CPZ_EINVAL, "null input or output pointer");
   if (!rows_aligned(rows, 7)) return fail(CPZ_EINVAL, "device rows must be 16-byte aligned");
   if (d_ctx_off && !d_ctx_bytes) return fail(CPZ_EINVAL, "ctx_off given without ctx_bytes");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
@@ -1833,7 +1916,7 @@ int cpz_prove_synthetic_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t 
   if (!d_y1 || !d_y2 || !d_r1 || !d_r2 || !d_s) return fail(CPZ_EINVAL, "null output pointer");
   const void* rows[5] = {d_y1, d_y2, d_r1, d_r2, d_s};
   if (!rows_aligned(rows, 5)) return fail(CPZ_EINVAL, "device outputs must be 16-byte aligned");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
@@ -1866,7 +1949,7 @@ int cpz_verify_response_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t 
     if (!p) return fail(CPZ_EINVAL, "null input pointer");
   if (!d_status_out) return fail(CPZ_EINVAL, "null output pointer");
   if (!rows_aligned(rows, 6)) return fail(CPZ_EINVAL, "device inputs must be 16-byte aligned");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;
@@ -1880,10 +1963,16 @@ int cpz_verify_response_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t 
 int cpz_verify_response(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_t n, const uint8_t* y1,
                         const uint8_t* y2, const uint8_t* r1, const uint8_t* r2, const uint8_t* s, const uint8_t* c,
                         uint8_t* status_out) {
+  return cpz_verify_response_ex(ctx, 0, g, h, n, y1, y2, r1, r2, s, c, status_out);
+}
+
+int cpz_verify_response_ex(cpz_ctx* ctx, uint32_t flags, const uint8_t g[32], const uint8_t h[32], size_t n, const uint8_t* y1,
+                        const uint8_t* y2, const uint8_t* r1, const uint8_t* r2, const uint8_t* s, const uint8_t* c,
+                        uint8_t* status_out) {
   if (!ctx || !g || !h) return fail(CPZ_EINVAL, "null context or generators");
   if (n == 0) return fail(CPZ_EEMPTY, "Cannot verify empty batch");
   if (!y1 || !y2 || !r1 || !r2 || !s || !c || !status_out) return fail(CPZ_EINVAL, "null input pointer");
-  std::lock_guard<std::mutex> lock(ctx->mu);
+  CallLock lock(ctx, flags);
   CPZ_HIP(hipSetDevice(ctx->device));
   int rc = ensure_generators(ctx, g, h);
   if (rc) return rc;

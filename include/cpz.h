@@ -54,8 +54,9 @@ extern "C" {
 /* ABI revision of this header (cpz_abi_version): bumped whenever an entry point's signature or
  * an array size it writes changes, so that callers built against another header can refuse
  * to run instead of passing wrongly sized buffers.  3: CPZ_NUM_STAGES = 16,
- * cpz_ctx_stage_times_n, cpz_ctx_set_commitment_checks. */
-#define CPZ_ABI_VERSION 3
+ * cpz_ctx_stage_times_n, cpz_ctx_set_commitment_checks.  4: per-call flags (the _ex entry
+ * points, CPZ_CALL_EQUATIONS_ONLY), stage 7 (generator tables), density probe with contexts. */
+#define CPZ_ABI_VERSION 4
 
 typedef struct cpz_ctx cpz_ctx;
 
@@ -78,8 +79,17 @@ void cpz_ctx_destroy(cpz_ctx *ctx);
  * equations alone -- e.g. a nonce k = 0 gives r1 = r2 = identity and an accepted proof.
  * enable = 0 gives exactly that: identity commitments and zero s are not reported, the
  * equations decide (and such entries keep their RLC weight).  Applies to every later call
- * on the context. */
+ * on the context, from any thread: callers that share a context and need the equations-only
+ * mode for their own calls pass CPZ_CALL_EQUATIONS_ONLY to the _ex entry points instead. */
 int cpz_ctx_set_commitment_checks(cpz_ctx *ctx, int enable);
+
+/* Per-call flags of the _ex entry points (cpz_verify_each_ex, cpz_verify_batch_ex,
+ * cpz_verify_response_ex): each behaves as its plain form with these options for that call
+ * alone -- the context's own mode and other threads' calls are unaffected.
+ *   CPZ_CALL_EQUATIONS_ONLY  commitment checks off for this call (as
+ *                            cpz_ctx_set_commitment_checks(ctx, 0)): what verify_one does
+ *                            with a Proof value (the mirrors of BatchVerifier / Verifier). */
+#define CPZ_CALL_EQUATIONS_ONLY 1u
 
 /* Thread-local description of the last error returned on this thread. */
 const char *cpz_last_error(void);
@@ -96,6 +106,10 @@ int cpz_verify_each(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size
                     const uint8_t *y1, const uint8_t *y2, const uint8_t *r1, const uint8_t *r2,
                     const uint8_t *s, const uint8_t *ctx_bytes, const uint64_t *ctx_off,
                     const uint8_t *ctx_present, uint8_t *status_out);
+int cpz_verify_each_ex(cpz_ctx *ctx, uint32_t flags, const uint8_t g[32], const uint8_t h[32], size_t n,
+                       const uint8_t *y1, const uint8_t *y2, const uint8_t *r1, const uint8_t *r2,
+                       const uint8_t *s, const uint8_t *ctx_bytes, const uint64_t *ctx_off,
+                       const uint8_t *ctx_present, uint8_t *status_out);
 
 /* Same with device-resident, 16-byte aligned inputs/outputs, enqueued on `stream`
  * (a hipStream_t, or NULL for the context's own stream, which is a blocking stream and so
@@ -122,6 +136,9 @@ int cpz_challenges(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_
 int cpz_verify_response(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
                         const uint8_t *y1, const uint8_t *y2, const uint8_t *r1, const uint8_t *r2,
                         const uint8_t *s, const uint8_t *c, uint8_t *status_out);
+int cpz_verify_response_ex(cpz_ctx *ctx, uint32_t flags, const uint8_t g[32], const uint8_t h[32], size_t n,
+                           const uint8_t *y1, const uint8_t *y2, const uint8_t *r1, const uint8_t *r2,
+                           const uint8_t *s, const uint8_t *c, uint8_t *status_out);
 int cpz_verify_response_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
                                const void *d_y1, const void *d_y2, const void *d_r1, const void *d_r2,
                                const void *d_s, const void *d_c, void *d_status_out, void *stream);
@@ -167,8 +184,8 @@ int cpz_prove_synthetic_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t 
  *   status_out   optional (n): exact per-entry statuses.  When the batch fails, a fallback
  *                search (sub-range RLC partials, per-proof verification at the leaves)
  *                locates the invalid entries (verify_individually, batch.rs:314-318).
- *                With a fallback, a batch of >= 2^20 entries without contexts is first
- *                sampled (4096 entries verified per proof, beside the batch's challenges):
+ *                With a fallback, a batch of >= 2^20 entries (with or without contexts) is
+ *                first sampled (4096 entries verified per proof, beside the batch's challenges):
  *                if two or more sampled entries are invalid the batch cannot pass and
  *                bisection could not prune it.  Up to 12 sampled invalid entries (density
  *                up to ~0.3 %): the partitioned check -- every 256-proof block's own RLC
@@ -183,6 +200,11 @@ int cpz_verify_batch(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], siz
                      const uint8_t *s, const uint8_t *ctx_bytes, const uint64_t *ctx_off,
                      const uint8_t *ctx_present, const uint8_t seed[32], uint64_t first_index,
                      uint8_t partial_out[32], int *batch_ok, uint8_t *status_out);
+int cpz_verify_batch_ex(cpz_ctx *ctx, uint32_t flags, const uint8_t g[32], const uint8_t h[32], size_t n,
+                        const uint8_t *y1, const uint8_t *y2, const uint8_t *r1, const uint8_t *r2,
+                        const uint8_t *s, const uint8_t *ctx_bytes, const uint64_t *ctx_off,
+                        const uint8_t *ctx_present, const uint8_t seed[32], uint64_t first_index,
+                        uint8_t partial_out[32], int *batch_ok, uint8_t *status_out);
 int cpz_verify_batch_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
                             const void *d_y1, const void *d_y2, const void *d_r1, const void *d_r2,
                             const void *d_s, const void *d_ctx_bytes, const uint64_t *d_ctx_off,
@@ -286,7 +308,9 @@ int cpz_verify_batch_multi(cpz_ctx *const *ctxs, int nctx, const uint8_t g[32], 
  * Stages: 0 = k_challenge, 1 = k_verify_each, 2 = RLC decode/weights, 3 = RLC MSM,
  * 4 = fallback, 5 = the whole per-proof verify of one call (first to last k_verify_each,
  * whose launches overlap on several streams), 6 = prover (commitments / statements, then
- * challenges + responses); phases of the RLC MSM (inside stage 3): 8 = bucket sort, 9 =
+ * challenges + responses), 7 = generator tables (a (g, h) pair's combs and transcript prefix
+ * built: a cache miss, one launch each; a context keeps the tables of its 4 most recently used
+ * pairs); phases of the RLC MSM (inside stage 3): 8 = bucket sort, 9 =
  * bucket accumulation (k_rlc_bucket), 10 = bucket fix-up, 11 = bucket reduction (segment +
  * window), 12 = window combine + encode (k_rlc_final).  cpz_ctx_stage_times synchronises, writes the summed milliseconds and
  * launch counts per stage since the last call, and resets them. */

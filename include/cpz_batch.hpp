@@ -17,16 +17,25 @@
 // error kind (src/error.rs:5-17).  Points and scalars stay as their 32-byte encodings:
 // decoding and all checks run on the GPU.  Verifier and BatchVerifier hold Proof values,
 // which may have been built directly (Proof::new, gadgets.rs:317: no identity / zero-s
-// checks), so they verify with commitment checks off -- the equations alone decide, as
-// verify_one (batch.rs:185-231) and verify_with_transcript (verifier/mod.rs:120-171) do;
+// checks), so their calls pass CPZ_CALL_EQUATIONS_ONLY -- the equations alone decide, as
+// verify_one (batch.rs:185-231) and verify_with_transcript (verifier/mod.rs:120-171) do --
+// for those calls only (the context's own mode, Device::set_commitment_checks, is untouched);
 // proof_from_bytes still applies from_bytes' checks.
+//
+// BatchVerifier::verify issues exactly the call sequence of the Rust drop-in
+// (rust/reference-patch/gpu.rs): entries grouped by Parameters in order of first appearance;
+// a one-entry batch -> cpz_verify_each_ex (batch.rs:178-180, the rng untouched); otherwise a
+// 32-byte seed drawn once from the caller's rng keys every group's RLC check, groups take
+// consecutive weight indices (first_index), and a group of at least rlc_min_group entries runs
+// cpz_verify_batch_ex (RLC + exact fallback), a smaller one cpz_verify_each_ex.
 #pragma once
 
 #include <array>
 #include <cstdint>
 #include <cstring>
-#include <map>
+#include <functional>
 #include <optional>
+#include <random>
 #include <string>
 #include <utility>
 #include <vector>
@@ -36,6 +45,11 @@
 namespace chaum_pedersen {
 
 constexpr std::size_t MAX_BATCH_SIZE = 1000;  // batch.rs:48
+
+// Smallest Parameters group that takes the RLC batch check rather than per-proof
+// verification (both return verify_one's outcome per entry).  The same threshold as
+// rust/reference-patch/gpu.rs (RLC_MIN_GROUP); measured in profiles/r04_small_batch.json.
+constexpr std::size_t RLC_MIN_GROUP = 2;
 
 using Bytes32 = std::array<uint8_t, 32>;
 
@@ -66,7 +80,6 @@ struct Parameters {  // gadgets.rs:25-118
   Bytes32 g, h;
   Parameters() { cpz_default_generators(g.data(), h.data()); }
   Parameters(const Bytes32& g_, const Bytes32& h_) : g(g_), h(h_) {}
-  bool operator<(const Parameters& o) const { return std::make_pair(g, h) < std::make_pair(o.g, o.h); }
 };
 
 struct Statement {  // gadgets.rs:177-239
@@ -126,26 +139,13 @@ class Device {
   Device& operator=(const Device&) = delete;
   bool ok() const { return rc_ == CPZ_OK && ctx_ != nullptr; }
   cpz_ctx* get() const { return ctx_; }
-  // cpz_ctx_set_commitment_checks; the mirrors below switch it off around their calls
+  // cpz_ctx_set_commitment_checks: the context's mode for every later call on it (the mirrors
+  // below do not use it: their calls pass CPZ_CALL_EQUATIONS_ONLY)
   int set_commitment_checks(bool on) { return cpz_ctx_set_commitment_checks(ctx_, on ? 1 : 0); }
 
  private:
   cpz_ctx* ctx_ = nullptr;
   int rc_ = CPZ_EINVAL;
-};
-
-// Commitment checks off for the lifetime of the guard (restored to the default, on).
-class EquationsOnly {
- public:
-  explicit EquationsOnly(Device& dev) : dev_(dev) { rc_ = dev_.set_commitment_checks(false); }
-  ~EquationsOnly() { (void)dev_.set_commitment_checks(true); }
-  EquationsOnly(const EquationsOnly&) = delete;
-  EquationsOnly& operator=(const EquationsOnly&) = delete;
-  int rc() const { return rc_; }
-
- private:
-  Device& dev_;
-  int rc_ = CPZ_OK;
 };
 
 // Statement::validate (gadgets.rs:234-238 -> ristretto.rs:173-185): y1 and y2 must be group
@@ -184,24 +184,22 @@ class Verifier {
   Result verify_with_transcript(const Proof& pr, const std::optional<std::vector<uint8_t>>& context) const {
     Result v = validate_statement(*dev_, st_);  // verifier/mod.rs:121
     if (v.is_err()) return v;
-    EquationsOnly eq(*dev_);
-    if (eq.rc() != CPZ_OK) return Result::err(ErrorKind::Device, cpz_last_error());
     uint8_t st = 0, present = context ? 1 : 0, pad = 0;
     const uint64_t off[2] = {0, context ? context->size() : 0};
     const uint8_t* cb = (context && !context->empty()) ? context->data() : &pad;
-    const int rc = cpz_verify_each(dev_->get(), params_.g.data(), params_.h.data(), 1, st_.y1.data(), st_.y2.data(),
-                                   pr.r1.data(), pr.r2.data(), pr.s.data(), context ? cb : nullptr,
-                                   context ? off : nullptr, context ? &present : nullptr, &st);
+    const int rc = cpz_verify_each_ex(dev_->get(), CPZ_CALL_EQUATIONS_ONLY, params_.g.data(), params_.h.data(), 1,
+                                      st_.y1.data(), st_.y2.data(), pr.r1.data(), pr.r2.data(), pr.s.data(),
+                                      context ? cb : nullptr, context ? off : nullptr, context ? &present : nullptr,
+                                      &st);
     if (rc != CPZ_OK) return Result::err(ErrorKind::Device, cpz_last_error());
     return status_result(st);
   }
   // verifier/mod.rs:144-171: the caller's challenge (32 canonical little-endian bytes)
   Result verify_response(const Bytes32& challenge, const Proof& pr) const {
-    EquationsOnly eq(*dev_);
-    if (eq.rc() != CPZ_OK) return Result::err(ErrorKind::Device, cpz_last_error());
     uint8_t st = 0;
-    const int rc = cpz_verify_response(dev_->get(), params_.g.data(), params_.h.data(), 1, st_.y1.data(),
-                                       st_.y2.data(), pr.r1.data(), pr.r2.data(), pr.s.data(), challenge.data(), &st);
+    const int rc = cpz_verify_response_ex(dev_->get(), CPZ_CALL_EQUATIONS_ONLY, params_.g.data(), params_.h.data(), 1,
+                                          st_.y1.data(), st_.y2.data(), pr.r1.data(), pr.r2.data(), pr.s.data(),
+                                          challenge.data(), &st);
     if (rc != CPZ_OK) return Result::err(ErrorKind::Device, cpz_last_error());
     return status_result(st);
   }
@@ -267,24 +265,57 @@ class BatchVerifier {
 
   void clear() { entries_.clear(); }
 
-  // batch.rs:171-183.  `overall` is Err for an empty batch (and device failures);
-  // otherwise the vector holds one Result per entry, in entry order.
-  std::vector<Result> verify(Result* overall = nullptr) const {
+  // The caller's randomness (the reference's rng: &mut impl CryptoRngCore, batch.rs:171):
+  // fills `len` bytes.  os_rng reads the OS entropy source.
+  using FillBytes = std::function<void(uint8_t*, std::size_t)>;
+  static void os_rng(uint8_t* out, std::size_t len) {
+    std::random_device rd;
+    for (std::size_t i = 0; i < len; i += 4) {
+      const uint32_t v = rd();
+      for (std::size_t k = 0; k < 4 && i + k < len; k++) out[i + k] = (uint8_t)(v >> (8 * k));
+    }
+  }
+
+  // What verify issued for one Parameters group (tests: the drop-in's call sequence).
+  struct Dispatch {
+    bool rlc = false;             // cpz_verify_batch_ex (else cpz_verify_each_ex)
+    std::size_t entries = 0;
+    uint64_t first_index = 0;     // the group's first weight index
+    Bytes32 seed{};               // the batch's seed (every group's)
+    Bytes32 partial{};            // the group's RLC partial (rlc only)
+    int batch_ok = 0;
+  };
+
+  // Groups of at least this many entries take the RLC check (RLC_MIN_GROUP by default).
+  void set_rlc_min_group(std::size_t m) { rlc_min_group_ = m; }
+
+  // batch.rs:171-183.  `overall` is Err for an empty batch (and device failures); otherwise
+  // the vector holds one Result per entry, in entry order.  `log` (optional) receives one
+  // Dispatch per group, in group order.
+  std::vector<Result> verify(Result* overall = nullptr) const { return verify(os_rng, overall); }
+  std::vector<Result> verify(const FillBytes& rng, Result* overall = nullptr,
+                             std::vector<Dispatch>* log = nullptr) const {
     if (overall) *overall = Result::ok();
     if (entries_.empty()) {
       if (overall) *overall = Result::err(ErrorKind::InvalidParams, "Cannot verify empty batch");
       return {};
     }
     std::vector<Result> out(entries_.size());
-    EquationsOnly eq(*dev_);  // Proof values: verify_one's equations alone
-    if (eq.rc() != CPZ_OK) {
-      if (overall) *overall = Result::err(ErrorKind::Device, cpz_last_error());
-      return {};
+    // Parameters groups in order of first appearance (gpu.rs: a Vec searched per entry)
+    std::vector<std::pair<Parameters, std::vector<std::size_t>>> groups;
+    for (std::size_t i = 0; i < entries_.size(); i++) {
+      std::size_t k = 0;
+      while (k < groups.size() && !(groups[k].first.g == entries_[i].params.g && groups[k].first.h == entries_[i].params.h))
+        k++;
+      if (k == groups.size()) groups.push_back({entries_[i].params, {}});
+      groups[k].second.push_back(i);
     }
-    std::map<Parameters, std::vector<std::size_t>> groups;  // one bulk call per Parameters
-    for (std::size_t i = 0; i < entries_.size(); i++) groups[entries_[i].params].push_back(i);
-    for (const auto& kv : groups) {
-      const auto& idx = kv.second;
+    const bool single = entries_.size() == 1;  // batch.rs:178-180: verify_one, no randomness
+    Bytes32 seed{};
+    bool have_seed = false;
+    uint64_t first_index = 0;
+    for (const auto& grp : groups) {
+      const auto& idx = grp.second;
       const std::size_t n = idx.size();
       std::vector<uint8_t> y1(32 * n), y2(32 * n), r1(32 * n), r2(32 * n), s(32 * n), ctx_bytes, present(n), st(n);
       std::vector<uint64_t> off(n + 1, 0);
@@ -304,13 +335,34 @@ class BatchVerifier {
         off[k + 1] = ctx_bytes.size();
       }
       if (ctx_bytes.empty()) ctx_bytes.push_back(0);
-      const int rc = cpz_verify_each(dev_->get(), kv.first.g.data(), kv.first.h.data(), n, y1.data(), y2.data(),
-                                     r1.data(), r2.data(), s.data(), any_ctx ? ctx_bytes.data() : nullptr,
-                                     any_ctx ? off.data() : nullptr, any_ctx ? present.data() : nullptr, st.data());
+      const uint8_t* cb = any_ctx ? ctx_bytes.data() : nullptr;
+      const uint64_t* co = any_ctx ? off.data() : nullptr;
+      const uint8_t* cp = any_ctx ? present.data() : nullptr;
+      const Parameters& p = grp.first;
+      Dispatch d;
+      d.entries = n;
+      d.first_index = first_index;
+      int rc;
+      if (!single && n >= rlc_min_group_) {
+        if (!have_seed) {  // drawn once per verify, as the reference draws its weights (batch.rs:240)
+          rng(seed.data(), seed.size());
+          have_seed = true;
+        }
+        d.rlc = true;
+        d.seed = seed;
+        rc = cpz_verify_batch_ex(dev_->get(), CPZ_CALL_EQUATIONS_ONLY, p.g.data(), p.h.data(), n, y1.data(), y2.data(),
+                                 r1.data(), r2.data(), s.data(), cb, co, cp, seed.data(), first_index,
+                                 d.partial.data(), &d.batch_ok, st.data());
+      } else {
+        rc = cpz_verify_each_ex(dev_->get(), CPZ_CALL_EQUATIONS_ONLY, p.g.data(), p.h.data(), n, y1.data(), y2.data(),
+                                r1.data(), r2.data(), s.data(), cb, co, cp, st.data());
+      }
       if (rc != CPZ_OK) {
         if (overall) *overall = Result::err(ErrorKind::Device, cpz_last_error());
         return {};
       }
+      first_index += n;
+      if (log) log->push_back(d);
       for (std::size_t k = 0; k < n; k++) out[idx[k]] = status_result(st[k]);
     }
     return out;
@@ -325,6 +377,7 @@ class BatchVerifier {
   };
   Device* dev_;
   std::vector<Entry> entries_;
+  std::size_t rlc_min_group_ = RLC_MIN_GROUP;
 };
 
 }  // namespace chaum_pedersen

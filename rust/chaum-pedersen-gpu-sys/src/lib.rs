@@ -46,7 +46,8 @@ pub const CPZ_PARSE_IDENTITY: u8 = 19;
 pub const CPZ_PARSE_ZERO_S: u8 = 20;
 
 pub const CPZ_NUM_STAGES: usize = 16;
-pub const CPZ_ABI_VERSION: c_int = 3;
+pub const CPZ_ABI_VERSION: c_int = 4;
+pub const CPZ_CALL_EQUATIONS_ONLY: u32 = 1;
 pub const CPZ_FALLBACK_STATS: usize = 6;
 pub const CPZ_FALLBACK_NONE: u64 = 0;
 pub const CPZ_FALLBACK_BISECTION: u64 = 1;
@@ -71,6 +72,9 @@ extern "C" {
     pub fn cpz_verify_each(ctx: *mut cpz_ctx, g: *const u8, h: *const u8, n: usize, y1: *const u8, y2: *const u8,
                            r1: *const u8, r2: *const u8, s: *const u8, ctx_bytes: *const u8, ctx_off: *const u64,
                            ctx_present: *const u8, status_out: *mut u8) -> c_int;
+    pub fn cpz_verify_each_ex(ctx: *mut cpz_ctx, flags: u32, g: *const u8, h: *const u8, n: usize, y1: *const u8,
+                              y2: *const u8, r1: *const u8, r2: *const u8, s: *const u8, ctx_bytes: *const u8,
+                              ctx_off: *const u64, ctx_present: *const u8, status_out: *mut u8) -> c_int;
     pub fn cpz_verify_each_device(ctx: *mut cpz_ctx, g: *const u8, h: *const u8, n: usize, d_y1: *const c_void,
                                   d_y2: *const c_void, d_r1: *const c_void, d_r2: *const c_void, d_s: *const c_void,
                                   d_ctx_bytes: *const c_void, d_ctx_off: *const u64, d_ctx_present: *const u8,
@@ -80,6 +84,9 @@ extern "C" {
                           ctx_present: *const u8, c_out: *mut u8) -> c_int;
     pub fn cpz_verify_response(ctx: *mut cpz_ctx, g: *const u8, h: *const u8, n: usize, y1: *const u8, y2: *const u8,
                                r1: *const u8, r2: *const u8, s: *const u8, c: *const u8, status_out: *mut u8) -> c_int;
+    pub fn cpz_verify_response_ex(ctx: *mut cpz_ctx, flags: u32, g: *const u8, h: *const u8, n: usize,
+                                  y1: *const u8, y2: *const u8, r1: *const u8, r2: *const u8, s: *const u8,
+                                  c: *const u8, status_out: *mut u8) -> c_int;
     pub fn cpz_verify_response_device(ctx: *mut cpz_ctx, g: *const u8, h: *const u8, n: usize, d_y1: *const c_void,
                                       d_y2: *const c_void, d_r1: *const c_void, d_r2: *const c_void,
                                       d_s: *const c_void, d_c: *const c_void, d_status_out: *mut c_void,
@@ -104,6 +111,10 @@ extern "C" {
                             r1: *const u8, r2: *const u8, s: *const u8, ctx_bytes: *const u8, ctx_off: *const u64,
                             ctx_present: *const u8, seed: *const u8, first_index: u64, partial_out: *mut u8,
                             batch_ok: *mut c_int, status_out: *mut u8) -> c_int;
+    pub fn cpz_verify_batch_ex(ctx: *mut cpz_ctx, flags: u32, g: *const u8, h: *const u8, n: usize, y1: *const u8,
+                               y2: *const u8, r1: *const u8, r2: *const u8, s: *const u8, ctx_bytes: *const u8,
+                               ctx_off: *const u64, ctx_present: *const u8, seed: *const u8, first_index: u64,
+                               partial_out: *mut u8, batch_ok: *mut c_int, status_out: *mut u8) -> c_int;
     pub fn cpz_verify_batch_device(ctx: *mut cpz_ctx, g: *const u8, h: *const u8, n: usize, d_y1: *const c_void,
                                    d_y2: *const c_void, d_r1: *const c_void, d_r2: *const c_void, d_s: *const c_void,
                                    d_ctx_bytes: *const c_void, d_ctx_off: *const u64, d_ctx_present: *const u8,

@@ -12,6 +12,12 @@ use std::ptr;
 /// A 32-byte encoding (compressed ristretto255 point or little-endian scalar).
 pub type Bytes32 = [u8; 32];
 
+/// Per-call flags (`CPZ_CALL_*`) of the `*_with` methods: options for that call alone.
+pub type CallFlags = u32;
+/// Commitment checks off for one call: the equations alone decide, as `verify_one`
+/// (batch.rs:185-231) does for a `Proof` value (`CPZ_CALL_EQUATIONS_ONLY`).
+pub const EQUATIONS_ONLY: CallFlags = sys::CPZ_CALL_EQUATIONS_ONLY;
+
 /// A device / argument failure of a whole call (`CPZ_E*` code + `cpz_last_error`).
 #[derive(Debug, Clone, PartialEq, Eq)]
 pub struct GpuError {
@@ -186,7 +192,9 @@ impl Gpu {
     /// Commitment checks (`cpz_ctx_set_commitment_checks`): on (the default) reports identity
     /// commitments and zero s as `Proof::from_bytes` would (gadgets.rs:474-482); off lets the
     /// two equations alone decide, as `verify_one` (batch.rs:185-231) does for a `Proof`
-    /// built with `Proof::new` -- what a `BatchVerifier` holds.
+    /// built with `Proof::new` -- what a `BatchVerifier` holds.  This is the context's mode
+    /// for every later call from any thread; `EQUATIONS_ONLY` on a `*_with` call is the same
+    /// for that call alone.
     pub fn set_commitment_checks(&self, enable: bool) -> Result<(), GpuError> {
         // SAFETY: ctx is live; the C side locks it.
         check(unsafe { sys::cpz_ctx_set_commitment_checks(self.ctx, enable as c_int) })
@@ -194,14 +202,21 @@ impl Gpu {
 
     /// Per-entry statuses of `BatchVerifier::verify` (batch.rs:171-231) for any n.
     pub fn verify_each(&self, g: &Bytes32, h: &Bytes32, entries: &[Entry<'_>]) -> Result<Vec<u8>, GpuError> {
+        self.verify_each_with(0, g, h, entries)
+    }
+
+    /// `verify_each` with per-call flags (`cpz_verify_each_ex`).
+    pub fn verify_each_with(&self, flags: CallFlags, g: &Bytes32, h: &Bytes32, entries: &[Entry<'_>])
+                            -> Result<Vec<u8>, GpuError> {
         let soa = Soa::new(entries);
         let (cb, co, cp) = soa.ctx_ptrs();
         let mut st = vec![0u8; entries.len()];
         let r = &soa.rows;
         // SAFETY: every row holds 32 * n bytes; contexts hold n + 1 offsets / n flags.
         check(unsafe {
-            sys::cpz_verify_each(self.ctx, g.as_ptr(), h.as_ptr(), entries.len(), r[0].as_ptr(), r[1].as_ptr(),
-                                 r[2].as_ptr(), r[3].as_ptr(), r[4].as_ptr(), cb, co, cp, st.as_mut_ptr())
+            sys::cpz_verify_each_ex(self.ctx, flags, g.as_ptr(), h.as_ptr(), entries.len(), r[0].as_ptr(),
+                                    r[1].as_ptr(), r[2].as_ptr(), r[3].as_ptr(), r[4].as_ptr(), cb, co, cp,
+                                    st.as_mut_ptr())
         })?;
         Ok(st)
     }
@@ -209,6 +224,12 @@ impl Gpu {
     /// `Verifier::verify_response` (verifier/mod.rs:144-171) with caller challenges.
     pub fn verify_response(&self, g: &Bytes32, h: &Bytes32, entries: &[Entry<'_>], challenges: &[Bytes32])
                            -> Result<Vec<u8>, GpuError> {
+        self.verify_response_with(0, g, h, entries, challenges)
+    }
+
+    /// `verify_response` with per-call flags (`cpz_verify_response_ex`).
+    pub fn verify_response_with(&self, flags: CallFlags, g: &Bytes32, h: &Bytes32, entries: &[Entry<'_>],
+                                challenges: &[Bytes32]) -> Result<Vec<u8>, GpuError> {
         assert_eq!(entries.len(), challenges.len());
         let soa = Soa::new(entries);
         let c: Vec<u8> = challenges.iter().flatten().copied().collect();
@@ -216,8 +237,9 @@ impl Gpu {
         let r = &soa.rows;
         // SAFETY: as verify_each; c holds 32 * n bytes.
         check(unsafe {
-            sys::cpz_verify_response(self.ctx, g.as_ptr(), h.as_ptr(), entries.len(), r[0].as_ptr(), r[1].as_ptr(),
-                                     r[2].as_ptr(), r[3].as_ptr(), r[4].as_ptr(), c.as_ptr(), st.as_mut_ptr())
+            sys::cpz_verify_response_ex(self.ctx, flags, g.as_ptr(), h.as_ptr(), entries.len(), r[0].as_ptr(),
+                                        r[1].as_ptr(), r[2].as_ptr(), r[3].as_ptr(), r[4].as_ptr(), c.as_ptr(),
+                                        st.as_mut_ptr())
         })?;
         Ok(st)
     }
@@ -227,6 +249,12 @@ impl Gpu {
     /// batch.rs:314-318).  Returns (partial encoding, batch_ok, statuses).
     pub fn verify_batch(&self, g: &Bytes32, h: &Bytes32, entries: &[Entry<'_>], seed: &Bytes32, first_index: u64)
                         -> Result<(Bytes32, bool, Vec<u8>), GpuError> {
+        self.verify_batch_with(0, g, h, entries, seed, first_index)
+    }
+
+    /// `verify_batch` with per-call flags (`cpz_verify_batch_ex`).
+    pub fn verify_batch_with(&self, flags: CallFlags, g: &Bytes32, h: &Bytes32, entries: &[Entry<'_>], seed: &Bytes32,
+                             first_index: u64) -> Result<(Bytes32, bool, Vec<u8>), GpuError> {
         let soa = Soa::new(entries);
         let (cb, co, cp) = soa.ctx_ptrs();
         let mut partial = [0u8; 32];
@@ -235,9 +263,9 @@ impl Gpu {
         let r = &soa.rows;
         // SAFETY: as verify_each; partial holds 32 bytes, ok is a local.
         check(unsafe {
-            sys::cpz_verify_batch(self.ctx, g.as_ptr(), h.as_ptr(), entries.len(), r[0].as_ptr(), r[1].as_ptr(),
-                                  r[2].as_ptr(), r[3].as_ptr(), r[4].as_ptr(), cb, co, cp, seed.as_ptr(), first_index,
-                                  partial.as_mut_ptr(), &mut ok, st.as_mut_ptr())
+            sys::cpz_verify_batch_ex(self.ctx, flags, g.as_ptr(), h.as_ptr(), entries.len(), r[0].as_ptr(),
+                                     r[1].as_ptr(), r[2].as_ptr(), r[3].as_ptr(), r[4].as_ptr(), cb, co, cp,
+                                     seed.as_ptr(), first_index, partial.as_mut_ptr(), &mut ok, st.as_mut_ptr())
         })?;
         Ok((partial, ok != 0, st))
     }

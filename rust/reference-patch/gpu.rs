@@ -6,19 +6,31 @@
 //! (service.rs:529-540, examples/batch_verification.rs:46, benches/batch_verification.rs:33).
 //! The three edits to the reference are listed in dispatch.rs.
 //!
-//! What the GPU computes, per `Parameters` group of entries:
+//! What the GPU computes, per `Parameters` group of entries (groups in order of first
+//! appearance):
 //!   * n == 1 (batch.rs:178-180): `verify_one` -- cpz_verify_each; `rng` is not touched,
 //!     as in the reference.
-//!   * n >= 2 (batch.rs:233-269): a 32-byte seed drawn from `rng` (the reference draws its
-//!     weights from it, batch.rs:240) keys the random-linear-combination check
-//!     (cpz_verify_batch: the batch equation with the weights on every term, one Pippenger
-//!     MSM); a failing batch runs the fallback search, which returns exactly `verify_one`'s
-//!     outcome per entry (verify_individually, batch.rs:262-268, 314-318).  Groups share the
-//!     seed and take consecutive weight indices (`first_index`).
-//! The context runs with commitment checks off: a `Proof` may have been built with
-//! `Proof::new` (no identity / zero-s checks, gadgets.rs:252, 278, 317), and `verify_one`
-//! judges it by the two equations alone -- so the result vector is the reference's for every
-//! batch, not only for proofs that came through `Proof::from_bytes`.
+//!   * n >= 2 (batch.rs:233-269): a 32-byte seed drawn once from `rng` (the reference draws
+//!     its weights from it, batch.rs:240) keys the random-linear-combination check of every
+//!     group of at least RLC_MIN_GROUP entries (cpz_verify_batch: the batch equation with the
+//!     weights on every term, one Pippenger MSM); a failing batch runs the fallback search,
+//!     which returns exactly `verify_one`'s outcome per entry (verify_individually,
+//!     batch.rs:262-268, 314-318).  A smaller group runs cpz_verify_each, which returns the
+//!     same outcome.  Groups take consecutive weight indices (`first_index`).
+//! Every call passes EQUATIONS_ONLY: a `Proof` may have been built with `Proof::new` (no
+//! identity / zero-s checks, gadgets.rs:252, 278, 317), and `verify_one` judges it by the
+//! two equations alone -- so the result vector is the reference's for every batch, not only
+//! for proofs that came through `Proof::from_bytes`.  The flag is per call: other users of
+//! the library's contexts keep their own mode.
+//!
+//! Contexts: a pool of CONTEXTS_PER_DEVICE contexts on every visible GPU.  Each `verify`
+//! checks one out for its duration (a free one, round-robin over the devices), so concurrent
+//! callers -- the service's handlers, service.rs:529-540 -- run side by side on every GPU
+//! instead of queueing on one context of GPU 0.  A context keeps the tables of its 4 most
+//! recently used (g, h) pairs, so batches whose groups alternate Parameters rebuild nothing.
+//!
+//! The C++ mirror of this call sequence (include/cpz_batch.hpp, BatchVerifier::verify) is
+//! what tests/test_gpu_dropin.py runs on the GPU against the oracle.
 //!
 //! Host work per entry is the four compressions the C ABI's 32-byte rows need (y1, y2, r1,
 //! r2) and one scalar copy; g and h are compressed once per group (entries are grouped by
@@ -26,21 +38,63 @@
 //! for large batches.  No `unsafe` appears here, so the crate keeps `#![forbid(unsafe_code)]`
 //! (src/lib.rs:64): the FFI lives in chaum-pedersen-gpu / chaum-pedersen-gpu-sys, whose
 //! build.rs runs hipcc (the crate's own build.rs:1-12 keeps running tonic-build only).
-use std::sync::OnceLock;
+use std::sync::atomic::{AtomicUsize, Ordering};
+use std::sync::{Mutex, MutexGuard, OnceLock, TryLockError};
 
-use chaum_pedersen_gpu::{Entry, EntryError, Gpu};
+use chaum_pedersen_gpu::{device_count, Entry, EntryError, Gpu, EQUATIONS_ONLY};
 use rand_core::CryptoRngCore;
 
 use super::{BatchEntry, BatchVerifier};
 use crate::{Element, Error, Parameters, Ristretto255, Result};
 
-/// The process's verifier context on GPU 0, with commitment checks off (see above).
-fn gpu() -> Result<&'static Gpu> {
-    static GPU: OnceLock<std::result::Result<Gpu, String>> = OnceLock::new();
-    GPU.get_or_init(|| {
-        let g = Gpu::new(0).map_err(|e| e.to_string())?;
-        g.set_commitment_checks(false).map_err(|e| e.to_string())?;
-        Ok(g)
+/// Contexts per visible GPU: two batches in flight on one GPU overlap one's latency-bound
+/// MSM tails with the other's VALU-bound work (1.06-1.075x one at a time, BENCH_r03
+/// rlc.two_in_flight).
+const CONTEXTS_PER_DEVICE: usize = 2;
+
+/// Smallest `Parameters` group sent to the RLC batch check; smaller groups are verified per
+/// proof (cpz_verify_each).  Both return `verify_one`'s outcome; the threshold only picks the
+/// faster entry point at the batch sizes this API carries (n <= 1000, batch.rs:48), from the
+/// per-call latency table profiles/r04_small_batch.json (bench.py small_batch).
+const RLC_MIN_GROUP: usize = 2;
+
+/// The process's verifier contexts (see above).
+struct Pool {
+    slots: Vec<Mutex<Gpu>>,
+    next: AtomicUsize,
+}
+
+impl Pool {
+    /// A free context, searched round-robin from a shared cursor (consecutive slots are on
+    /// different GPUs); when every context is busy, the cursor's own slot, waited for.
+    fn checkout(&self) -> MutexGuard<'_, Gpu> {
+        let n = self.slots.len();
+        let start = self.next.fetch_add(1, Ordering::Relaxed);
+        for k in 0..n {
+            match self.slots[(start + k) % n].try_lock() {
+                Ok(g) => return g,
+                Err(TryLockError::Poisoned(p)) => return p.into_inner(),
+                Err(TryLockError::WouldBlock) => {}
+            }
+        }
+        self.slots[start % n].lock().unwrap_or_else(|p| p.into_inner())
+    }
+}
+
+fn pool() -> Result<&'static Pool> {
+    static POOL: OnceLock<std::result::Result<Pool, String>> = OnceLock::new();
+    POOL.get_or_init(|| {
+        let devices = device_count();
+        if devices == 0 {
+            return Err("no GPU visible to the HIP runtime".to_string());
+        }
+        let mut slots = Vec::with_capacity(devices * CONTEXTS_PER_DEVICE);
+        for _ in 0..CONTEXTS_PER_DEVICE {
+            for d in 0..devices {
+                slots.push(Mutex::new(Gpu::new(d).map_err(|e| e.to_string())?));
+            }
+        }
+        Ok(Pool { slots, next: AtomicUsize::new(0) })
     })
     .as_ref()
     .map_err(|e| Error::InvalidParams(e.clone()))
@@ -114,7 +168,7 @@ pub(super) fn verify<R: CryptoRngCore + ?Sized>(batch: &BatchVerifier, rng: &mut
     if entries.is_empty() {
         return Err(Error::InvalidParams("Cannot verify empty batch".to_string()));
     }
-    let gpu = gpu()?;
+    let gpu = pool()?.checkout();
     let mut groups: Vec<Group<'_>> = Vec::new();
     for (i, e) in entries.iter().enumerate() {
         let (g, h) = (e.params.generator_g(), e.params.generator_h());
@@ -129,19 +183,20 @@ pub(super) fn verify<R: CryptoRngCore + ?Sized>(batch: &BatchVerifier, rng: &mut
     for grp in &groups {
         let rows = group_rows(entries, &grp.idx);
         let (g, h) = &grp.enc;
-        let status = if entries.len() == 1 {
-            gpu.verify_each(g, h, &rows).map_err(|e| Error::InvalidParams(e.to_string()))?
+        let status = if entries.len() == 1 || rows.len() < RLC_MIN_GROUP {
+            gpu.verify_each_with(EQUATIONS_ONLY, g, h, &rows).map_err(|e| Error::InvalidParams(e.to_string()))?
         } else {
             let seed = seed.get_or_insert_with(|| {
                 let mut s = [0u8; 32];
                 rng.fill_bytes(&mut s);
                 s
             });
-            let (_partial, _ok, st) =
-                gpu.verify_batch(g, h, &rows, seed, first_index).map_err(|e| Error::InvalidParams(e.to_string()))?;
-            first_index += rows.len() as u64;
+            let (_partial, _ok, st) = gpu
+                .verify_batch_with(EQUATIONS_ONLY, g, h, &rows, seed, first_index)
+                .map_err(|e| Error::InvalidParams(e.to_string()))?;
             st
         };
+        first_index += rows.len() as u64;
         for (k, &i) in grp.idx.iter().enumerate() {
             out[i] = Some(entry_result(status[k]));
         }

@@ -241,21 +241,31 @@ def test_commitment_checks_off_equals_verify_one_on_constructed_proofs(gpu):
     eq_only = [O.verify_one(r, commitment_checks=False) for r in recs]
     assert default == [0, 4, 4, 5] and eq_only == [0, 0, 0, 1]
     assert list(gpu.verify_each(*rows)) == default
-    with gpu.commitment_checks(False):
+    # per call (CPZ_CALL_EQUATIONS_ONLY): the context's mode is untouched
+    assert list(gpu.verify_each(*rows, equations_only=True)) == eq_only
+    _, bok, st = gpu.verify_batch(*rows, seed=bytes(range(32)), equations_only=True)
+    assert not bok and list(st) == eq_only
+    # the RLC weights the identity-commitment entries (they are valid): the partial is the
+    # oracle's with the same checks off, i.e. the s = 0 entry's alone
+    part, _, _ = gpu.verify_batch(*rows, seed=bytes(range(32)), statuses=False, equations_only=True)
+    want = O.rlc_partial(recs, bytes(range(32)), commitment_checks=False)
+    assert part == O.ristretto_encode(want)
+    assert part == O.ristretto_encode(O.rlc_partial([s0], bytes(range(32)), base_index=3,
+                                                    commitment_checks=False))
+    _, bok, st = gpu.verify_batch(*[r[:3] for r in rows], seed=bytes(range(32)), equations_only=True)
+    assert bok and not st.any()
+    c = gpu.challenges(*rows[:4])
+    assert list(gpu.verify_response(*rows, c, equations_only=True)) == eq_only
+    assert list(gpu.verify_each(*rows)) == default
+    # the context's mode (cpz_ctx_set_commitment_checks): every call until it is switched back
+    gpu.set_commitment_checks(False)
+    try:
         assert list(gpu.verify_each(*rows)) == eq_only
         _, bok, st = gpu.verify_batch(*rows, seed=bytes(range(32)))
         assert not bok and list(st) == eq_only
-        # the RLC weights the identity-commitment entries (they are valid): the partial is the
-        # oracle's with the same checks off, i.e. the s = 0 entry's alone
-        part, _, _ = gpu.verify_batch(*rows, seed=bytes(range(32)), statuses=False)
-        want = O.rlc_partial(recs, bytes(range(32)), commitment_checks=False)
-        assert part == O.ristretto_encode(want)
-        assert part == O.ristretto_encode(O.rlc_partial([s0], bytes(range(32)), base_index=3,
-                                                        commitment_checks=False))
-        _, bok, st = gpu.verify_batch(*[r[:3] for r in rows], seed=bytes(range(32)))
-        assert bok and not st.any()
-        c = gpu.challenges(*rows[:4])
         assert list(gpu.verify_response(*rows, c)) == eq_only
+    finally:
+        gpu.set_commitment_checks(True)
     # back to the default mode
     assert list(gpu.verify_each(*rows)) == default
     _, bok, st = gpu.verify_batch(*rows, seed=bytes(range(32)))
@@ -289,3 +299,74 @@ def test_add_time_statement_validation_and_capacity(gpu, golden):
     assert b.is_empty()
     b.add(cp.Parameters(), cp.Statement(rec.y1, rec.y2), cp.Proof(rec.r1, rec.r2, rec.s))
     assert b.len() == 1 and b.verify()[0].is_ok()
+
+
+def test_equations_only_is_per_call_across_threads(gpu):
+    """CPZ_CALL_EQUATIONS_ONLY applies to its own call only: one thread verifies
+    with the flag while another, on the same context, verifies in the context's default mode;
+    neither ever sees the other's mode."""
+    import threading
+    x = O.bench_scalar(b"x", 5151)
+    recs = [O.prove(x, 7), O.prove(x, 0)]          # valid; nonce 0: identity commitments
+    rows = _cons_rows(recs)
+    bad = []
+
+    def run(eq, want):
+        for _ in range(25):
+            got = list(gpu.verify_each(*rows, equations_only=eq))
+            if got != want:
+                bad.append((eq, got))
+            _, _, st = gpu.verify_batch(*rows, seed=bytes(32), equations_only=eq)
+            if list(st) != want:
+                bad.append((eq, "batch", list(st)))
+
+    th = [threading.Thread(target=run, args=(True, [0, 0])), threading.Thread(target=run, args=(False, [0, 4]))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not bad, bad[:4]
+
+
+def test_generator_cache_two_pairs_two_contexts(golden):
+    """A context keeps the tables of several (g, h) pairs: two host threads, each on its own
+    context, alternate the default and the golden custom generators -- each context builds
+    each pair's tables once (stage 7 counts the builds) and every status is right."""
+    import threading
+    cg = golden["custom_generators"]
+    pa = cp.Parameters()
+    pb = cp.Parameters(bytes.fromhex(cg["g"]), bytes.fromhex(cg["h"]))
+    rows = {}
+    with cp.Gpu(0) as g0:
+        for key, p in (("a", pa), ("b", pb)):
+            out = g0.prove([O.bench_scalar(b"x", i) for i in range(40)],
+                           [O.bench_scalar(b"k", i) for i in range(40)], params=p)
+            rows[key] = [out[q] for q in ("y1", "y2", "r1", "r2", "s")]
+    gpus = [cp.Gpu(0), cp.Gpu(0)]
+    builds, bad = [0, 0], []
+
+    def run(k):
+        g = gpus[k]
+        g.set_timing(True)
+        g.stage_times()
+        for it in range(8):
+            key, p, other = ("a", pa, pb) if (it + k) % 2 == 0 else ("b", pb, pa)
+            if list(g.verify_each(*rows[key], params=p)) != [0] * 40:
+                bad.append((k, it, "own"))
+            if list(g.verify_each(*rows[key], params=other)) != [1] * 40:   # wrong generators
+                bad.append((k, it, "other"))
+            _, ok, st = g.verify_batch(*rows[key], seed=bytes(range(32)), params=p)
+            if not ok or st.any():
+                bad.append((k, it, "batch"))
+        builds[k] = g.stage_times().get("generators", (0.0, 0))[1]
+        g.set_timing(False)
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for g in gpus:
+        g.close()
+    assert not bad, bad[:4]
+    assert builds == [2, 2], builds

@@ -133,9 +133,31 @@ def test_patch_serves_verify_with_the_reference_signature():
 def test_patch_draws_the_seed_from_rng_and_uses_the_batch_check():
     g = _code("rust/reference-patch/gpu.rs")
     assert "rng.fill_bytes(&mut s)" in g                  # weights keyed by rng (batch.rs:240)
-    assert "gpu.verify_batch(" in g and "gpu.verify_each(" in g
-    assert "entries.len() == 1" in g                     # n == 1 -> verify_one, rng untouched
-    assert "set_commitment_checks(false)" in g           # Proof::new entries: equations only
+    assert "gpu.verify_each_with(EQUATIONS_ONLY," in g   # Proof::new entries: equations only, per call
+    assert ".verify_batch_with(EQUATIONS_ONLY," in g
+    assert "set_commitment_checks" not in g              # never the shared context mode
+    assert "entries.len() == 1 || rows.len() < RLC_MIN_GROUP" in g   # n == 1 -> verify_one, rng untouched
+    assert "first_index += rows.len() as u64;" in g      # consecutive weight indices, every group
+
+
+def test_patch_pools_contexts_over_every_gpu():
+    """gpu.rs keeps CONTEXTS_PER_DEVICE (>= 2) contexts on every visible GPU and checks one
+    out per verify call, instead of one static context on GPU 0; its RLC threshold is the
+    C++ mirror's and the Python mirror's (the call sequence tests/test_gpu_dropin.py runs)."""
+    g = _code("rust/reference-patch/gpu.rs")
+    m = re.search(r"const CONTEXTS_PER_DEVICE: usize = (\d+);", g)
+    assert m and int(m.group(1)) >= 2
+    assert "for d in 0..devices" in g and "device_count()" in g
+    assert "pool()?.checkout()" in g and "try_lock()" in g
+    assert "Gpu::new(0)" not in g
+    rust_min = int(re.search(r"const RLC_MIN_GROUP: usize = (\d+);", g).group(1))
+    hpp = open(os.path.join(ROOT, "include", "cpz_batch.hpp")).read()
+    assert int(re.search(r"constexpr std::size_t RLC_MIN_GROUP = (\d+);", hpp).group(1)) == rust_min
+    import chaum_pedersen as cp
+    assert cp.RLC_MIN_GROUP == rust_min
+    # the safe crate exposes the per-call flag the patch uses
+    wrap = open(os.path.join(ROOT, "rust", "chaum-pedersen-gpu", "src", "lib.rs")).read()
+    assert "pub const EQUATIONS_ONLY: CallFlags = sys::CPZ_CALL_EQUATIONS_ONLY;" in wrap
 
 
 def test_patch_compresses_generators_once_per_group():
