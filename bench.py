@@ -22,7 +22,8 @@ At N = 1 the same run also measures (reported beside value, never as value): the
 check of the same proofs with per-kernel roofline fractions (configs[2]), the 2^24-proof
 batch with 0.1 % forged proofs through the batch check + fallback (configs[4]), the prover
 (proof generation, published ~144 us/proof, lib.rs:55), the host-buffer entry point (PCIe
-included), and the CPU baseline.
+included), the per-call latency of BatchVerifier-sized batches (n = 1 .. 1000, both entry
+points, beside the CPU's BatchVerifier::verify), and the CPU baseline.
 
 Prints ONE JSON line on rank 0.
 """
@@ -59,19 +60,25 @@ def _profile(name):
     return (_load_json(os.path.join("profiles", cands[-1])) or {}) if cands else {}
 
 
-def mad_peak_at_kernel_clock(oc):
-    """The v_mad_i64_i32 issue ceiling at the clock k_verify_each itself runs at: the best
-    measured lane rate per SIMD cycle (tools/ubench/clock_rates.hip, profiles/rNN_clock_rates.json:
-    event-timed launch cycles at the measured shader clock) x 1024 SIMDs x the kernel's own
-    shader clock (in-kernel s_memtime / s_memrealtime probe of a timing-only build,
-    profiles/rNN_verify_clock_probe.json).  None when either file is missing."""
+def _newest_profile(suffix):
     pdir = os.path.join(ROOT, "profiles")
-    cr_f = sorted(f for f in os.listdir(pdir) if f.endswith("_clock_rates.json"))
-    pr_f = sorted(f for f in os.listdir(pdir) if f.endswith("_verify_clock_probe.json"))
-    if not cr_f or not pr_f:
-        return None
-    cr = _load_json(os.path.join("profiles", cr_f[-1])) or {}
-    pr = _load_json(os.path.join("profiles", pr_f[-1])) or {}
+    cands = sorted(f for f in os.listdir(pdir) if f.endswith(suffix))
+    return (cands[-1], _load_json(os.path.join("profiles", cands[-1])) or {}) if cands else (None, {})
+
+
+def mad_peak_at_kernel_clock(oc, kernel="k_verify_each"):
+    """The v_mad_i64_i32 issue ceiling at the clock `kernel` itself runs at: the best measured
+    lane rate per SIMD cycle (tools/ubench/clock_rates.hip, profiles/rNN_clock_rates.json:
+    event-timed launch cycles at the measured shader clock) x 1024 SIMDs x the kernel's own
+    shader clock from the in-kernel s_memtime / s_memrealtime probe of a timing-only build
+    (profiles/rNN_verify_clock_probe.json for k_verify_each, profiles/rNN_rlc_clock_probe.json
+    for k_rlc_prepare / k_rlc_bucket).  None when either file is missing."""
+    cr_name, cr = _newest_profile("_clock_rates.json")
+    if kernel == "k_verify_each":
+        pr_name, pr = _newest_profile("_verify_clock_probe.json")
+    else:
+        pr_name, pr = _newest_profile("_rlc_clock_probe.json")
+        pr = pr.get(kernel) or {}
     rows = [r for r in cr.get("rows", []) if r.get("op") == "v_mad_i64_i32"]
     clk = (pr.get("shader_clock_ghz") or {}).get("mean")
     if not rows or not clk:
@@ -81,7 +88,7 @@ def mad_peak_at_kernel_clock(oc):
     lanes = best.get("lanes_per_simd_cycle") or best["gops"] * 1e9 / (simds * best["clock_ghz"] * 1e9)
     return {"peak": lanes * simds * clk * 1e9, "lanes_per_simd_cycle": lanes, "clock_ghz": clk,
             "best_waves_per_simd": best.get("waves_per_simd"), "ubench_clock_ghz": best.get("clock_ghz"),
-            "sources": ["profiles/" + cr_f[-1], "profiles/" + pr_f[-1]]}
+            "sources": ["profiles/" + cr_name, "profiles/" + pr_name]}
 
 
 def cpu_threads(requested: int) -> dict:
@@ -124,17 +131,29 @@ def _bump_s(torch, t, idx):
 
 
 def rlc_roofline(stages, n, steps, oc):
-    """Per-kernel fractions of the RLC step from the runtime's HIP-event stage times."""
+    """Per-kernel fractions of the RLC step from the runtime's HIP-event stage times, each
+    MAD-bound kernel priced on the headline's basis: the v_mad issue rate x 1024 SIMDs x that
+    kernel's own shader clock (in-kernel probe, mad_peak_at_kernel_clock)."""
     r = oc.get("rlc", {})
-    peak = oc["peaks"]["v_mad_i64_i32_lane_ops_per_s"]
     hbm = oc["peaks"]["hbm_bytes_per_s"]
     ms = {k: (v[0] / steps) for k, v in stages.items()}
-    out = {"unit_mad": "Tmad/s", "peak_mad": peak / 1e12, "unit_hbm": "GB/s", "peak_hbm": hbm / 1e9,
-           "kernel_ms_per_step": ms}
+    out = {"unit_mad": "Tmad/s", "unit_hbm": "GB/s", "peak_hbm": hbm / 1e9, "kernel_ms_per_step": ms}
+
+    def priced(kernel, achieved):
+        kc = mad_peak_at_kernel_clock(oc, kernel)
+        if not kc:
+            return {"achieved": achieved, "frac": None, "peak": None,
+                    "peak_basis": "unpriced: no in-kernel clock probe of %s under profiles/" % kernel}
+        pk = kc["peak"] / 1e12
+        return {"achieved": achieved, "peak": pk, "frac": achieved / pk, "peak_clock_ghz": kc["clock_ghz"],
+                "peak_basis": "v_mad_i64_i32 %.2f lanes / SIMD cycle x 1024 SIMDs x %s's own shader clock %.3f GHz "
+                              "(in-kernel probe)" % (kc["lanes_per_simd_cycle"], kernel, kc["clock_ghz"]),
+                "peak_sources": kc["sources"]}
+
     prep = r.get("prepare_per_proof", {}).get("mads")
     if prep and ms.get("rlc_prepare"):
         a = prep * n / (ms["rlc_prepare"] * 1e-3) / 1e12
-        out["k_rlc_prepare"] = {"bound": "valu-int", "mads_per_proof": prep, "achieved": a, "frac": a / (peak / 1e12)}
+        out["k_rlc_prepare"] = dict(bound="valu-int", mads_per_proof=prep, **priced("k_rlc_prepare", a))
     ent = r.get("bucket_entries_per_proof")
     bk = r.get("bucket_per_entry", {})
     if ent and ms.get("rlc_bucket"):
@@ -142,12 +161,11 @@ def rlc_roofline(stages, n, steps, oc):
         a = bk["mads"] * ent * n / t / 1e12
         gbs = bk["bytes"] * ent * n / t / 1e9
         pmc = _profile("rlc_bucket_pmc")
-        out["k_rlc_bucket"] = {"bound": "valu-int", "mads_per_entry": bk["mads"], "entries_per_proof": ent,
-                               "achieved": a, "frac": a / (peak / 1e12),
-                               "algorithmic_bytes_per_entry": bk["bytes"], "achieved_gbs": gbs,
-                               "hbm_frac": gbs / (hbm / 1e9),
-                               "traffic_bytes_per_2p20": pmc.get("hbm_bytes_per_2p20"),
-                               "traffic_source": pmc.get("source")}
+        out["k_rlc_bucket"] = dict(bound="valu-int", mads_per_entry=bk["mads"], entries_per_proof=ent,
+                                   **priced("k_rlc_bucket", a),
+                                   algorithmic_bytes_per_entry=bk["bytes"], achieved_gbs=gbs,
+                                   hbm_frac=gbs / (hbm / 1e9), traffic_bytes_per_2p20=pmc.get("hbm_bytes_per_2p20"),
+                                   traffic_source=pmc.get("source"))
     tails = sum(ms.get(k, 0.0) for k in ("rlc_sort", "rlc_bucket_fix", "rlc_reduce", "rlc_final"))
     out["sort_plus_tails_ms"] = tails
     return out
@@ -234,15 +252,17 @@ def small_batch_table(gpu=None, sizes=SMALL_SIZES, stages=False, cpu=True):
         sub = [rows[k][:n] for k in keys]
         subf = [forged[k][:n] for k in keys]
         r = {"n": n}
-        r["verify_each_ms"], _ = _median_call_ms(lambda: gpu.verify_each(*sub))
-        st = gpu.verify_each(*sub)
+        # equations-only per call, as the drop-in issues them (gpu.rs, cpz_batch.hpp)
+        r["verify_each_ms"], _ = _median_call_ms(lambda: gpu.verify_each(*sub, equations_only=True))
+        st = gpu.verify_each(*sub, equations_only=True)
         assert not st.any(), "small_batch: valid proofs rejected"
-        r["verify_batch_ms"], _ = _median_call_ms(lambda: gpu.verify_batch(*sub, WEIGHT_SEED))
-        _, ok, st = gpu.verify_batch(*sub, WEIGHT_SEED)
+        r["verify_batch_ms"], _ = _median_call_ms(lambda: gpu.verify_batch(*sub, WEIGHT_SEED, equations_only=True))
+        _, ok, st = gpu.verify_batch(*sub, WEIGHT_SEED, equations_only=True)
         assert ok and not st.any(), "small_batch: valid batch rejected"
         if n >= 2:
-            r["verify_batch_one_forged_ms"], _ = _median_call_ms(lambda: gpu.verify_batch(*subf, WEIGHT_SEED))
-            _, ok, st = gpu.verify_batch(*subf, WEIGHT_SEED)
+            r["verify_batch_one_forged_ms"], _ = _median_call_ms(
+                lambda: gpu.verify_batch(*subf, WEIGHT_SEED, equations_only=True))
+            _, ok, st = gpu.verify_batch(*subf, WEIGHT_SEED, equations_only=True)
             assert (not ok) and st[0] == 1 and not st[1:].any(), "small_batch: forged entry not located"
         if stages:
             gpu.set_timing(True)
@@ -266,6 +286,79 @@ def small_batch_table(gpu=None, sizes=SMALL_SIZES, stages=False, cpu=True):
                       "semantics: defective equation + per-entry fallback, batch.rs:171-318), one thread"}
     if own:
         gpu.close()
+    return out
+
+
+def c5_extra(gpu, torch, dev, stream, n5, ctx_len):
+    """configs[4]: n5 proofs, 0.1 % forged, through the batch check + fallback -> the exact
+    invalid set, timed against cpz_verify_each of the same batch.  ctx_len = 32: every proof
+    carries a 32-byte transcript context (the service's challenge ids, service.rs:512-517) and
+    half the forgeries are a replayed context instead of a wrong y1."""
+    import numpy as np
+    nf = max(1, n5 // 1000)
+    t5 = {k: torch.empty((n5, 32), dtype=torch.uint8, device=dev) for k in ("y1", "y2", "r1", "r2", "s")}
+    cx = {}
+    if ctx_len:
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(555)
+        cx["ctx_bytes"] = torch.randint(0, 256, (n5 * ctx_len,), dtype=torch.int32, device=dev,
+                                        generator=gen).to(torch.uint8)
+        cx["ctx_off"] = torch.arange(n5 + 1, dtype=torch.int64, device=dev) * ctx_len
+    gpu.prove_synthetic_device(n5, SEED_X, SEED_K, t5["y1"], t5["y2"], t5["r1"], t5["r2"], t5["s"], stream=stream, **cx)
+    idx = np.sort(np.random.default_rng(2024).choice(n5, size=nf, replace=False))
+    bump, swap = idx[0::2], idx[1::2]
+    _bump_s(torch, t5, bump)
+    dst = torch.from_numpy(swap.astype(np.int64)).to(dev)
+    if ctx_len:   # the proof presented under another entry's context (a replayed challenge id)
+        cv = cx["ctx_bytes"].view(n5, ctx_len)
+        cv.index_copy_(0, dst, cv.index_select(0, (dst + 1) % n5).clone())
+    else:
+        src = torch.from_numpy(((swap + 7) % n5).astype(np.int64)).to(dev)
+        t5["y1"].index_copy_(0, dst, t5["y1"].index_select(0, src).clone())
+    rows = [t5[k] for k in ("y1", "y2", "r1", "r2", "s")]
+    st5 = torch.empty(n5, dtype=torch.uint8, device=dev)
+    gpu.verify_batch_device(*rows, st5, WEIGHT_SEED, fallback=True, stream=stream, **cx)  # warm-up (allocations)
+    st5.fill_(0xFF)
+    gpu.set_timing(True)
+    gpu.stage_times()
+    torch.cuda.synchronize(dev)
+    c0 = time.perf_counter()
+    partial, ok = gpu.verify_batch_device(*rows, st5, WEIGHT_SEED, fallback=True, stream=stream, **cx)
+    torch.cuda.synchronize(dev)
+    c_el = time.perf_counter() - c0
+    c_st = gpu.stage_times()
+    c_fb = gpu.fallback_stats()
+    got = st5.cpu().numpy()
+    exact = (not ok) and np.array_equal(np.nonzero(got)[0], idx) and set(got[idx].tolist()) == {1}
+    if not exact:
+        raise SystemExit("bench: C5 fallback did not return exactly the forged set")
+    st5.fill_(0xFF)
+    torch.cuda.synchronize(dev)
+    p0 = time.perf_counter()
+    gpu.verify_each_device(*rows, st5, stream=stream, **cx)
+    torch.cuda.synchronize(dev)
+    p_el = time.perf_counter() - p0
+    gpu.set_timing(False)
+    pp = st5.cpu().numpy()
+    if not np.array_equal(pp, got):
+        raise SystemExit("bench: C5 per-proof statuses differ from the fallback's")
+    ms = {k: v[0] for k, v in c_st.items()}
+    out = {"workload": "configs[4]: %d proofs%s, %d forged (half s+1, half %s), RLC batch check + fallback "
+                       "(density probe beside the challenges; at this density the partitioned check: every "
+                       "256-proof block's RLC partial, per-proof verification of the failing blocks only) -> "
+                       "exact invalid set" % (n5, (" with %d-byte contexts" % ctx_len) if ctx_len else "", nf,
+                                              "a replayed context" if ctx_len else "wrong y1"),
+           "proofs": n5, "forged": nf, "ms": c_el * 1e3, "proofs_per_s": n5 / c_el, "exact_set": True,
+           "phase_ms": {"challenge": ms.get("challenge", 0.0), "rlc_prepare": ms.get("rlc_prepare", 0.0),
+                        "rlc_msm": ms.get("rlc_msm", 0.0), "fallback_per_proof": ms.get("fallback", 0.0)},
+           "fallback": c_fb,
+           "per_proof_only_ms": p_el * 1e3,
+           "ratio_to_per_proof": c_el / p_el,
+           "partial": partial.hex(),
+           "note": "per_proof_only_ms: cpz_verify_each of the same batch (same statuses); rlc_msm is the "
+                   "partitioned MSM (k_part_*), fallback_per_proof the per-proof pass over the failing blocks"}
+    del t5, st5, cx
+    torch.cuda.empty_cache()
     return out
 
 
@@ -295,6 +388,8 @@ def main():
                     help="add the two-batches-in-flight figure to the RLC extra (0: one batch at a time only, "
                          "e.g. under a profiler whose per-kernel averages should not mix the two)")
     ap.add_argument("--host-e2e", type=int, default=None, help="override --extras for the host-buffer extra")
+    ap.add_argument("--small-batch", type=int, default=None,
+                    help="override --extras for the small-batch latency table (the drop-in's n <= 1000 regime)")
     ap.add_argument("--c5-n", type=int, default=1 << 24, help="configs[4] batch size (0.1 %% forged)")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N > 1 ('nccl' = RCCL over xGMI; 'gloo' only for rehearsals)")
@@ -419,61 +514,10 @@ def main():
                      "two_in_flight": (rlc_two_in_flight(cp, gpu, t, n, args.steps, local_rank, lo)
                                        if args.rlc_inflight else None)}
 
-    c5 = None
+    c5 = c5_ctx = None
     if args.mode == "each" and solo and args.extras and args.c5_n:
-        n5, nf = args.c5_n, max(1, args.c5_n // 1000)
-        t5 = {k: torch.empty((n5, 32), dtype=torch.uint8, device=dev) for k in t}
-        gpu.prove_synthetic_device(n5, SEED_X, SEED_K, t5["y1"], t5["y2"], t5["r1"], t5["r2"], t5["s"], stream=stream)
-        idx = np.sort(np.random.default_rng(2024).choice(n5, size=nf, replace=False))
-        bump, swap = idx[0::2], idx[1::2]
-        _bump_s(torch, t5, bump)
-        dst = torch.from_numpy(swap.astype(np.int64)).to(dev)
-        src = torch.from_numpy(((swap + 7) % n5).astype(np.int64)).to(dev)
-        t5["y1"].index_copy_(0, dst, t5["y1"].index_select(0, src).clone())
-        st5 = torch.empty(n5, dtype=torch.uint8, device=dev)
-        gpu.verify_batch_device(*(t5[k] for k in ("y1", "y2", "r1", "r2", "s")), st5, WEIGHT_SEED, fallback=True,
-                                stream=stream)  # warm-up (allocations)
-        st5.fill_(0xFF)
-        gpu.set_timing(True)
-        gpu.stage_times()
-        torch.cuda.synchronize(dev)
-        c0 = time.perf_counter()
-        partial, ok = gpu.verify_batch_device(*(t5[k] for k in ("y1", "y2", "r1", "r2", "s")), st5, WEIGHT_SEED,
-                                              fallback=True, stream=stream)
-        torch.cuda.synchronize(dev)
-        c_el = time.perf_counter() - c0
-        c_st = gpu.stage_times()
-        c_fb = gpu.fallback_stats()
-        got = st5.cpu().numpy()
-        exact = (not ok) and np.array_equal(np.nonzero(got)[0], idx) and set(got[idx].tolist()) == {1}
-        if not exact:
-            raise SystemExit("bench: C5 fallback did not return exactly the forged set")
-        st5.fill_(0xFF)
-        torch.cuda.synchronize(dev)
-        p0 = time.perf_counter()
-        gpu.verify_each_device(*(t5[k] for k in ("y1", "y2", "r1", "r2", "s")), st5, stream=stream)
-        torch.cuda.synchronize(dev)
-        p_el = time.perf_counter() - p0
-        gpu.set_timing(False)
-        pp = st5.cpu().numpy()
-        if not np.array_equal(pp, got):
-            raise SystemExit("bench: C5 per-proof statuses differ from the fallback's")
-        ms = {k: v[0] for k, v in c_st.items()}
-        c5 = {"workload": "configs[4]: %d proofs, %d forged (half s+1, half wrong y1), RLC batch check + fallback "
-                          "(density probe beside the challenges; at this density the partitioned check: every "
-                          "256-proof block's RLC partial, per-proof verification of the failing blocks only) -> "
-                          "exact invalid set" % (n5, nf),
-              "proofs": n5, "forged": nf, "ms": c_el * 1e3, "proofs_per_s": n5 / c_el, "exact_set": True,
-              "phase_ms": {"challenge": ms.get("challenge", 0.0), "rlc_prepare": ms.get("rlc_prepare", 0.0),
-                           "rlc_msm": ms.get("rlc_msm", 0.0), "fallback_per_proof": ms.get("fallback", 0.0)},
-              "fallback": c_fb,
-              "per_proof_only_ms": p_el * 1e3,
-              "ratio_to_per_proof": c_el / p_el,
-              "partial": partial.hex(),
-              "note": "per_proof_only_ms: cpz_verify_each of the same batch (same statuses); rlc_msm is the "
-                      "partitioned MSM (k_part_*), fallback_per_proof the per-proof pass over the failing blocks"}
-        del t5, st5
-        torch.cuda.empty_cache()
+        c5 = c5_extra(gpu, torch, dev, stream, args.c5_n, 0)
+        c5_ctx = c5_extra(gpu, torch, dev, stream, args.c5_n, 32)
 
     prove = None
     if args.mode == "each" and solo and args.extras:
@@ -516,6 +560,10 @@ def main():
         host_e2e = {"workload": "cpz_verify_each from pageable host arrays (H2D of 5 x 32 B/proof + D2H of statuses)",
                     "proofs_per_s": n * steps_h / h_el, "ms_per_call": h_el * 1e3 / steps_h, "calls": steps_h}
         del hrows
+
+    small = None
+    if args.mode == "each" and solo and extra(args.small_batch):
+        small = small_batch_table(gpu, cpu=not args.no_cpu_baseline)
 
     value = total_proofs * args.steps / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
@@ -569,8 +617,9 @@ def main():
         rr = rlc_roofline(stages, n, args.steps, oc)
         pk = rr.get("k_rlc_prepare", {})
         roofline = {"kernel": "k_rlc_prepare (the RLC step's largest kernel; k_rlc_bucket below)",
-                    "bound": "valu-int", "achieved": pk.get("achieved"), "peak": peak_mad / 1e12, "unit": "Tmad/s",
-                    "frac": pk.get("frac"), "traffic": None, "rlc": rr}
+                    "bound": "valu-int", "achieved": pk.get("achieved"), "peak": pk.get("peak"), "unit": "Tmad/s",
+                    "frac": pk.get("frac"), "peak_clock_ghz": pk.get("peak_clock_ghz"),
+                    "peak_basis": pk.get("peak_basis"), "traffic": None, "rlc": rr}
 
     cpu = None
     if rank == 0 and solo and not args.no_cpu_baseline:
@@ -618,10 +667,14 @@ def main():
             line["rlc"] = rlc_extra
         if c5:
             line["c5"] = c5
+        if c5_ctx:
+            line["c5_ctx"] = c5_ctx
         if prove:
             line["prove"] = prove
         if host_e2e:
             line["host_e2e"] = host_e2e
+        if small:
+            line["small_batch"] = small
         if args.same_device:
             # several ranks on one GPU: a correctness rehearsal of the multi-rank path, not a
             # measurement -- no rate is reported

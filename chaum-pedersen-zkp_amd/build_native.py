@@ -83,6 +83,17 @@ def build_libcpz(force: bool = False, verbose: bool = False, out: str = LIBCPZ, 
     return out
 
 
+CLOCK_PROBE_LIB = os.path.join(LIBDIR, "timing", "clock_probe.so")
+
+
+def build_clock_probe(force: bool = False) -> str:
+    """Timing-only build with the in-kernel clock probes (csrc/timing_only.h): k_verify_each,
+    k_rlc_prepare, k_rlc_bucket stamp their shader clock; tools/time_verify.py reads them.
+    Not part of build_all: only the measurement runs load it (CPZ_LIB)."""
+    os.makedirs(os.path.dirname(CLOCK_PROBE_LIB), exist_ok=True)
+    return build_libcpz(force, out=CLOCK_PROBE_LIB, defines=("CPZ_CLOCK_PROBE", "CPZ_TIMING_ONLY"))
+
+
 def build_hosttest(force: bool = False) -> str:
     src = os.path.join(ROOT, "tests", "native", "hostlib.cpp")
     if not force and not _newer(HOSTTEST, [src] + _headers()):

@@ -15,6 +15,10 @@ constexpr int kRlcBuckets = 1 << 15;     // |digit| in [1, 2^15]
 #endif
 constexpr int kRlcSegLen = CPZ_RLC_SEGLEN;  // buckets per reduction segment
 constexpr int kRlcPrepBlock = 256;       // proofs per prepare block (= block_sums granule)
+#ifndef CPZ_RLC_PREP_WIDE_MAX
+#define CPZ_RLC_PREP_WIDE_MAX (1 << 15)
+#endif
+constexpr int64_t kRlcPrepWideMax = CPZ_RLC_PREP_WIDE_MAX;  // up to this many proofs: four lanes per proof
 constexpr int kRlcSortBlock = 1024;
 #ifndef CPZ_RLC_SORT_CHUNK
 #define CPZ_RLC_SORT_CHUNK (1 << 16)
@@ -22,7 +26,9 @@ constexpr int kRlcSortBlock = 1024;
 constexpr int kRlcSortGroups = 64;      // max blocks per window in the counting sort
 constexpr int64_t kRlcSortChunk = CPZ_RLC_SORT_CHUNK;  // target points per sort block
 constexpr int kNielsEntriesRlc = kTableB;
-constexpr int kRlcChunk = 64;            // sorted entries per bucket-accumulation thread
+constexpr int kRlcChunk = 64;            // sorted entries per bucket-accumulation thread (at most)
+constexpr int kRlcMinChunk = 4;          // ... and at least (small MSMs, rlc_sort_geometry)
+constexpr int64_t kRlcMinHeads = 2048;   // head slots per window whatever the MSM's size
 // Points of one MSM (its flat positions t, incl. the two extras): the 32-bit entries hold t
 // in 24 bits and all-ones is their empty marker.
 constexpr int64_t kRlcMaxMsmPoints = (1ll << 24) - 1;
@@ -42,8 +48,10 @@ struct RlcPrepArgs {
   int16_t* digits;               // [16][dstride] signed radix-2^16 digits
   int64_t dstride;
   sc* block_sums;                // [ceil(n/256)][2]
+  sc* quarter_sums = nullptr;    // [ceil(n/64)][2]: scratch of the four-lanes-per-proof prepare
   int* any_bad;                  // set to 1 if some proof has a non-zero decode-level status
   int eq_only = 0;               // commitment checks off: identity r1 / r2 keep their weight
+  uint64_t* clock_probe = nullptr;  // CPZ_CLOCK_PROBE builds only: 5 words per wave (rlc_dev.h)
 };
 
 struct RlcMsmArgs {
@@ -57,12 +65,13 @@ struct RlcMsmArgs {
   uint32_t* bhist;               // [16][groups][2^15] per-sort-block histograms -> block bases
   int groups;                    // sort blocks per window
   int64_t chunk;                 // points per sort block
+  int echunk = kRlcChunk;        // sorted entries per k_rlc_bucket thread (rlc_sort_geometry)
   uint32_t* idx;                 // [16][istride]
   uint32_t* inter;               // [16][istride] coarse-sorted entries (32-bit)
   int64_t istride;
   ge_p3* buckets;                // [16][2^15]
   ge_p3* heads;                  // [16][hstride] partials of buckets begun in an earlier chunk
-  int64_t hstride;               // >= ceil(istride / kRlcChunk)
+  int64_t hstride;               // >= ceil(points / echunk)
   ge_p3* seg_s;                  // [16][2^15 / kRlcSegLen]
   ge_p3* seg_w;                  // [16][2^15 / kRlcSegLen]
   ge_p3* win;                    // [16]
@@ -73,6 +82,7 @@ struct RlcMsmArgs {
   // the sum -- into partial_out / identity_out.  total == nullptr: a single MSM.
   ge_p3* total = nullptr;
   int total_first = 1, total_last = 1;
+  uint64_t* clock_probe = nullptr;  // CPZ_CLOCK_PROBE builds only: k_rlc_bucket, 5 words per wave
 };
 
 // ---- partitioned batch check (part.hip) --------------------------------------------------
@@ -117,7 +127,7 @@ hipError_t launch_part_sum(const ge_p3* part, int64_t nblk, ge_p3* tmp, uint32_t
                            hipStream_t st);
 
 hipError_t launch_rlc_prepare(const RlcPrepArgs& a, hipStream_t st);
-// Sort geometry for `npts` MSM points: sets a.groups / a.chunk.
+// Sort and accumulation geometry for `npts` MSM points: sets a.groups / a.chunk / a.echunk.
 void rlc_sort_geometry(RlcMsmArgs& a, int64_t npts);
 // marks (optional, timing): kRlcMsmMarks events recorded on `st` at the phase boundaries
 // (start | sort: extra, hist, bscan, scan, coarse, fine | bucket | bucket fix | segment + window

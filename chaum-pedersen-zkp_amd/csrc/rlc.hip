@@ -49,6 +49,8 @@ __global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_prepare(RlcPrepArgs a)
   __shared__ sc red_a[kRlcPrepBlock];
   __shared__ sc red_b[kRlcPrepBlock];
   const int64_t i = (int64_t)blockIdx.x * kRlcPrepBlock + threadIdx.x;
+  ClockStamp clk;
+  clk.start();
   sc zero;
 #pragma unroll
   for (int k = 0; k < 8; k++) zero.w[k] = 0;
@@ -113,6 +115,7 @@ __global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_prepare(RlcPrepArgs a)
         for (int wv = 0; wv < kRlcWindows; wv++) a.digits[(int64_t)wv * a.dstride + 4 * i + q] = 0;
     }
   }
+  clk.stop(a.clock_probe, i >> 6);
   // block sums of a_i s_i, b_i s_i (mod l)
   __syncthreads();
   for (int off = kRlcPrepBlock / 2; off > 0; off >>= 1) {
@@ -126,6 +129,103 @@ __global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_prepare(RlcPrepArgs a)
     a.block_sums[2 * blockIdx.x] = red_a[0];
     a.block_sums[2 * blockIdx.x + 1] = red_b[0];
   }
+}
+
+// Small batches (launch_rlc_prepare: n <= kRlcPrepWideMax): four lanes per proof -- lane q
+// writes point q's digits and decodes point q -- so a BatchVerifier-sized batch waits for one
+// decode per lane instead of four in sequence (on one lane per proof the prepare took 0.28 -
+// 0.37 ms at n = 1 .. 1000, a latency, with most of the chip idle).  The weights' ChaCha20
+// block is recomputed by each of the four lanes.  A block is 64 proofs: its a s and b s sums
+// go to quarter_sums, and k_rlc_bsum4 adds each 256-proof block's four into block_sums.
+__global__ void __launch_bounds__(256, 2) k_rlc_prepare4(RlcPrepArgs a) {
+  __shared__ sc red_a[64];
+  __shared__ sc red_b[64];
+  const int q = threadIdx.x & 3, p = threadIdx.x >> 2;
+  const int64_t i = (int64_t)blockIdx.x * 64 + p;
+  sc zero;
+#pragma unroll
+  for (int k = 0; k < 8; k++) zero.w[k] = 0;
+  if (q == 0) red_a[p] = zero;
+  if (q == 2) red_b[p] = zero;
+  bool ok = true, ident = false;
+  if (i < a.n) {
+    {
+      // q = 0: -r1 (a), 1: -y1 (a c), 2: -r2 (b), 3: -y2 (b c), as k_rlc_prepare
+      uint32_t blk[16];
+      chacha20_block(blk, a.seed, a.first_index + (uint64_t)i, 0);
+      const uint32_t* u = q < 2 ? blk : blk + 4;
+      int16_t d[kRlcWindows];
+      if (q & 1) {
+        sc c;
+        rlc_load8(c.w, a.c, i);
+        recode16(d, sc_mul(rlc_weight(u), c).w);
+      } else {
+#pragma unroll
+        for (int wv = 0; wv < kRlcWindows; wv++) d[wv] = wv < 8 ? (int16_t)(u[wv >> 1] >> (16 * (wv & 1))) : (int16_t)0;
+        sc sv;
+        rlc_load8(sv.w, a.s, i);
+        (q == 0 ? red_a : red_b)[p] = sc_mul(rlc_weight(u), sv);
+      }
+#pragma unroll
+      for (int wv = 0; wv < kRlcWindows; wv++) a.digits[(int64_t)wv * a.dstride + 4 * i + q] = d[wv];
+    }
+    const uint32_t* src = q == 0 ? a.r1 : (q == 1 ? a.y1 : (q == 2 ? a.r2 : a.y2));
+    uint32_t w[8];
+    rlc_load8(w, src, i);
+    ident = !(q & 1) && words8_zero(w);
+    ge_p3 P;
+    ok = ristretto_decode(P, w);
+    store_niels(a.pts + 4 * i + q, niels_from_p3_affine(P, true));
+  }
+  // the proof's four lanes are consecutive lanes of one wave: OR their flags
+  int f = (ok ? 0 : 1) | (ident ? 2 : 0);
+  f |= __shfl_xor(f, 1);
+  f |= __shfl_xor(f, 2);
+  if (i < a.n) {
+    const uint8_t st_s = a.status[i];
+    uint8_t st;
+    if (f & 1) st = kStBadPoint;
+    else if (st_s == kStBadScalar) st = kStBadScalar;
+    else if ((f & 2) && !a.eq_only) st = kStIdentity;
+    else if (st_s == kStZeroS) st = kStZeroS;
+    else st = kStOk;
+    if (q == 0) a.status[i] = st;  // after the quad's loads of it: one wave, in program order
+    if (st != kStOk) {  // zero weight: no digits, no block-sum terms
+      if (q == 0) {
+        atomicOr(a.any_bad, 1);
+        red_a[p] = zero;
+      }
+      if (q == 2) red_b[p] = zero;
+#pragma unroll
+      for (int wv = 0; wv < kRlcWindows; wv++) a.digits[(int64_t)wv * a.dstride + 4 * i + q] = 0;
+    }
+  }
+  __syncthreads();
+  for (int off = 32; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+      red_a[threadIdx.x] = sc_add(red_a[threadIdx.x], red_a[threadIdx.x + off]);
+      red_b[threadIdx.x] = sc_add(red_b[threadIdx.x], red_b[threadIdx.x + off]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    a.quarter_sums[2 * blockIdx.x] = red_a[0];
+    a.quarter_sums[2 * blockIdx.x + 1] = red_b[0];
+  }
+}
+
+// block_sums of a wide prepare: 256-proof block b is quarters 4 b .. 4 b + 3 (those that exist).
+__global__ void __launch_bounds__(64) k_rlc_bsum4(const sc* __restrict__ quarter_sums, int64_t nq,
+                                                  sc* __restrict__ block_sums, int64_t nb) {
+  const int64_t t = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (t >= 2 * nb) return;
+  const int64_t b = t >> 1;
+  const int ab = (int)(t & 1);
+  sc acc;
+#pragma unroll
+  for (int k = 0; k < 8; k++) acc.w[k] = 0;
+  for (int64_t k = 4 * b; k < 4 * b + 4 && k < nq; k++) acc = sc_add(acc, quarter_sums[2 * k + ab]);
+  block_sums[2 * b + ab] = acc;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -442,7 +542,7 @@ __global__ void __launch_bounds__(kRlcSortBlock) k_rlc_fine(RlcMsmArgs a) {
 
 // ---------------------------------------------------------------------------------------
 // Bucket accumulation: B[w][b] = sum of (+/-) points in bucket b of window w, load-balanced.
-// Window w's sorted entries [0, E_w) are cut into chunks of kRlcChunk; thread (w, t) adds
+// Window w's sorted entries [0, E_w) are cut into chunks of echunk; thread (w, t) adds
 // exactly the points of chunk t (every lane of a wave does the same number of additions,
 // whatever the bucket sizes -- the top window's 8x fuller buckets included).  A bucket that
 // starts inside chunk t is owned by t, which writes its partial to B[w][b]; the partial of
@@ -484,12 +584,14 @@ __device__ __forceinline__ int next_bucket(const uint32_t* off, int b, uint32_t 
 __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
   const int w = blockIdx.y;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  ClockStamp clk;
+  clk.start();
   const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
   const uint32_t total = off[kRlcBuckets];
-  const int64_t e0l = t * kRlcChunk;
+  const int64_t e0l = t * a.echunk;
   if (e0l >= (int64_t)total) return;
   const uint32_t e0 = (uint32_t)e0l;
-  const uint32_t e1 = e0 + kRlcChunk < total ? e0 + kRlcChunk : total;
+  const uint32_t e1 = e0 + (uint32_t)a.echunk < total ? e0 + (uint32_t)a.echunk : total;
   const uint32_t* idx = a.idx + (int64_t)w * a.istride;
   ge_p3* bw = a.buckets + (int64_t)w * kRlcBuckets;
   ge_p3* heads = a.heads + (int64_t)w * a.hstride;
@@ -520,6 +622,7 @@ __global__ void __launch_bounds__(256) k_rlc_bucket(RlcMsmArgs a) {
   }
   const ge_p3 v = p1p1_to_p3(r);
   if (head) store_p3(heads + t, v); else store_p3(bw + b, v);
+  clk.stop(a.clock_probe, ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6));
 }
 
 // Buckets leave the fix-up in cached form (Y+X, Y-X, Z, 2dT, the same 160 bytes), so the
@@ -555,7 +658,7 @@ __global__ void __launch_bounds__(256, CPZ_RLC_FIX_WAVES) k_rlc_bucket_fix(RlcMs
     store_cached(dst, ge_cached_identity());
     return;
   }
-  const uint32_t c0 = s / kRlcChunk, c1 = (e - 1) / kRlcChunk;
+  const uint32_t c0 = s / (uint32_t)a.echunk, c1 = (e - 1) / (uint32_t)a.echunk;
   const ge_p3* heads = a.heads + (int64_t)w * a.hstride;
   ge_p3 v = load_p3(a.buckets + t);
   for (uint32_t c = c0 + 1; c <= c1; c++) v = ge_add(v, load_p3(heads + c));
@@ -745,6 +848,15 @@ __global__ void k_rlc_combine(const uint32_t* __restrict__ parts, int k, uint32_
 // ---------------------------------------------------------------------------------------
 hipError_t launch_rlc_prepare(const RlcPrepArgs& a, hipStream_t st) {
   const int64_t blocks = (a.n + kRlcPrepBlock - 1) / kRlcPrepBlock;
+  if (a.n <= kRlcPrepWideMax && a.quarter_sums) {
+    const int64_t nq = (a.n + 63) / 64;
+    hipLaunchKernelGGL(k_rlc_prepare4, dim3((unsigned)nq), dim3(256), 0, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_rlc_bsum4, dim3((unsigned)((2 * blocks + 63) / 64)), dim3(64), 0, st, a.quarter_sums, nq,
+                       a.block_sums, blocks);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_rlc_prepare, dim3((unsigned)blocks), dim3(kRlcPrepBlock), 0, st, a);
   return hipGetLastError();
 }
@@ -755,6 +867,14 @@ void rlc_sort_geometry(RlcMsmArgs& a, int64_t npts) {
   if (g < 1) g = 1;
   a.groups = (int)g;
   a.chunk = ((npts + g - 1) / g + 63) & ~(int64_t)63;  // whole 16-byte digit loads (k_rlc_hist)
+  // Entries per k_rlc_bucket thread: kRlcChunk for a large MSM (load-balanced, enough threads
+  // anyway); a small one (a BatchVerifier batch, a bisection leaf) is cut finer so that at
+  // least ~2048 threads share each window, since a thread's additions are one dependent chain
+  // -- 64 of them on one lane took 0.34-0.40 ms at n = 20 .. 1000 proofs.  A window holds at
+  // most npts entries, so ceil(npts / echunk) <= max(npts / kRlcChunk, kRlcMinHeads) heads.
+  int e = kRlcMinChunk;
+  while (e < kRlcChunk && (int64_t)e * kRlcMinHeads < npts) e <<= 1;
+  a.echunk = e;
 }
 
 hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0, int64_t b1, const ge_niels* tab,
@@ -789,7 +909,7 @@ hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0,
   hipLaunchKernelGGL(k_rlc_fine, dim3(kRlcCoarse, kRlcWindows), dim3(kRlcSortBlock), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = mark(1)) != hipSuccess) return e;
-  const int64_t chunks = (a.istride + kRlcChunk - 1) / kRlcChunk;  // per window, upper bound
+  const int64_t chunks = ((a.p1 - a.p0) + 2 + a.echunk - 1) / a.echunk;  // per window: entries <= points
   hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((chunks + 255) / 256), kRlcWindows), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = mark(2)) != hipSuccess) return e;

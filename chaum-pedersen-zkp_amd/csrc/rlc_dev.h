@@ -9,6 +9,40 @@
 
 namespace cpz {
 
+// In-kernel clock probe of the RLC kernels (CPZ_CLOCK_PROBE timing-only builds, timing_only.h;
+// tools/time_verify.py MODE=rlc): per wave, lane 0 stores shader-clock (s_memtime) and
+// constant 100 MHz (s_memrealtime) ticks of the wave's work, its absolute 100 MHz start and
+// end, and its hardware id at probe[5 * wave] -- the clock the kernel ran at, against which
+// bench.py prices its MAD rate.  Product builds compile none of it.
+struct ClockStamp {
+  uint64_t t0 = 0, q0 = 0;
+  __device__ __forceinline__ void start() {
+#if defined(CPZ_CLOCK_PROBE)
+    t0 = __builtin_amdgcn_s_memtime();
+    q0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  }
+  __device__ __forceinline__ void stop(uint64_t* probe, int64_t wave) const {
+#if defined(CPZ_CLOCK_PROBE)
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), q1 = __builtin_amdgcn_s_memrealtime();
+    if (probe && (threadIdx.x & 63) == 0) {
+      uint32_t hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      uint64_t* out = probe + 5 * wave;
+      out[0] = t1 - t0;
+      out[1] = q1 - q0;
+      out[2] = q0;
+      out[3] = q1;
+      out[4] = (uint64_t)hw | ((uint64_t)xcc << 32);
+    }
+#else
+    (void)probe;
+    (void)wave;
+#endif
+  }
+};
+
 __device__ __forceinline__ void rlc_load8(uint32_t w[8], const uint32_t* base, int64_t i) {
   const uint4* p = reinterpret_cast<const uint4*>(base + 8 * i);
   const uint4 a = p[0], b = p[1];

@@ -121,10 +121,10 @@ bool is_no_partial(const uint8_t p[32]) {
 //   RlcMsmSet    sort / bucket / reduction buffers of ONE MSM, its partial and identity flag.
 //                Capacity: proofs of one MSM (a span of at most CPZ_RLC_SPAN proofs).
 struct RlcPrepared {
-  DevBuf pts, dig, bsum;
+  DevBuf pts, dig, bsum, qsum;
   int64_t cap = 0;
   void release() {
-    for (DevBuf* b : {&pts, &dig, &bsum}) b->release();
+    for (DevBuf* b : {&pts, &dig, &bsum, &qsum}) b->release();
     cap = 0;
   }
 };
@@ -224,6 +224,12 @@ struct cpz_ctx {
   // c, scratch, RLC buffers) that the next call may rewrite on another stream.
   hipEvent_t last_done = nullptr;
   bool have_last = false;
+#if defined(CPZ_CLOCK_PROBE)
+  // timing-only builds: the in-kernel clock stamps of the last k_rlc_prepare [0] and
+  // k_rlc_bucket [1] launch (cpz_ctx_clock_probe), 5 words per wave
+  DevBuf clk[2];
+  size_t clk_waves[2] = {0, 0};
+#endif
   // optional per-kernel timing
   bool timing = false;
   struct Mark { int stage; hipEvent_t a, b; };
@@ -554,8 +560,13 @@ int stage_inputs(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], int count
 // digits row stride: 4 points per proof + g, h, rounded to 8 so that every window row starts
 // 16-byte aligned (k_rlc_hist reads 8 digits per load)
 int64_t rlc_dstride(int64_t cap) { return (4 * cap + 2 + 7) & ~(int64_t)7; }
-// sorted-entry row stride: whole 4096-entry groups (k_rlc_fine stores them transposed)
+// sorted-entry row stride: whole 4096-entry groups
 int64_t rlc_istride(int64_t cap) { return (4 * cap + 2 + 4095) & ~(int64_t)4095; }
+// bucket-head slots per window: one per k_rlc_bucket thread of any MSM the set can hold
+// (rlc_sort_geometry: ceil(points / echunk) <= max(points / kRlcChunk, kRlcMinHeads))
+int64_t rlc_hstride(int64_t cap) {
+  return std::max<int64_t>((rlc_istride(cap) + cpz::kRlcChunk - 1) / cpz::kRlcChunk, cpz::kRlcMinHeads);
+}
 
 // The prepared set for a batch of n proofs.
 int rlc_reserve_prepared(RlcPrepared& P, int64_t n) {
@@ -566,6 +577,7 @@ int rlc_reserve_prepared(RlcPrepared& P, int64_t n) {
   CPZ_HIP(P.pts.ensure((size_t)npts * sizeof(cpz::ge_niels)));
   CPZ_HIP(P.dig.ensure((size_t)rlc_dstride(n) * cpz::kRlcWindows * sizeof(int16_t)));
   CPZ_HIP(P.bsum.ensure((size_t)nblk * 2 * sizeof(cpz::sc)));
+  CPZ_HIP(P.qsum.ensure((size_t)((std::min(n, cpz::kRlcPrepWideMax) + 63) / 64) * 2 * sizeof(cpz::sc)));
   P.cap = n;
   return CPZ_OK;
 }
@@ -580,7 +592,7 @@ int rlc_reserve_msm(RlcMsmSet& S, int64_t span) {
   CPZ_HIP(S.idx.ensure((size_t)rlc_istride(span) * cpz::kRlcWindows * sizeof(uint32_t)));
   CPZ_HIP(S.inter.ensure((size_t)rlc_istride(span) * cpz::kRlcWindows * sizeof(uint32_t)));
   CPZ_HIP(S.buckets.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * cpz::kRlcBuckets));
-  CPZ_HIP(S.heads.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * (size_t)(rlc_istride(span) / cpz::kRlcChunk)));
+  CPZ_HIP(S.heads.ensure(sizeof(cpz::ge_p3) * cpz::kRlcWindows * (size_t)rlc_hstride(span)));
   const size_t nseg = (size_t)cpz::kRlcWindows * (cpz::kRlcBuckets / cpz::kRlcSegLen);
   CPZ_HIP(S.segs.ensure(sizeof(cpz::ge_p3) * nseg));
   CPZ_HIP(S.segw.ensure(sizeof(cpz::ge_p3) * nseg));
@@ -632,7 +644,7 @@ int rlc_msm_args(const RlcPrepared& P, RlcMsmSet& S, int64_t lo, int64_t hi, cpz
   m.istride = rlc_istride(S.cap);
   m.buckets = static_cast<cpz::ge_p3*>(S.buckets.p);
   m.heads = static_cast<cpz::ge_p3*>(S.heads.p);
-  m.hstride = (m.istride + cpz::kRlcChunk - 1) / cpz::kRlcChunk;
+  m.hstride = rlc_hstride(S.cap);
   m.seg_s = static_cast<cpz::ge_p3*>(S.segs.p);
   m.seg_w = static_cast<cpz::ge_p3*>(S.segw.p);
   m.win = static_cast<cpz::ge_p3*>(S.win.p);
@@ -663,6 +675,15 @@ int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t part
     }
     const int64_t b0 = slo / cpz::kRlcPrepBlock;
     const int64_t b1 = (shi + cpz::kRlcPrepBlock - 1) / cpz::kRlcPrepBlock;
+#if defined(CPZ_CLOCK_PROBE)
+    {  // k_rlc_bucket's grid: (ceil(chunks / 256), 16) blocks of 4 waves (launch_rlc_msm)
+      const int64_t chunks = ((m.p1 - m.p0) + 2 + m.echunk - 1) / m.echunk;
+      ctx->clk_waves[1] = (size_t)((chunks + 255) / 256) * cpz::kRlcWindows * 4;
+      CPZ_HIP(ctx->clk[1].ensure(ctx->clk_waves[1] * 40));
+      CPZ_HIP(hipMemsetAsync(ctx->clk[1].p, 0, ctx->clk_waves[1] * 40, st));
+      m.clock_probe = static_cast<uint64_t*>(ctx->clk[1].p);
+    }
+#endif
     StageTimer t(ctx, 3, st);
     // phase marks (stages 8-12) when timing: sort, bucket, bucket fix, segment + window, final
     hipEvent_t marks[cpz::kRlcMsmMarks];
@@ -733,9 +754,16 @@ int rlc_prepare_points(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, c
   pa.digits = static_cast<int16_t*>(ctx->rl_prep.dig.p);
   pa.dstride = rlc_dstride(ctx->rl_prep.cap);
   pa.block_sums = static_cast<cpz::sc*>(ctx->rl_prep.bsum.p);
+  pa.quarter_sums = static_cast<cpz::sc*>(ctx->rl_prep.qsum.p);
   pa.eq_only = ctx->call_eq ? 1 : 0;
   pa.any_bad = static_cast<int*>(ctx->rl_flags.p) + 3;
   CPZ_HIP(hipMemsetAsync(pa.any_bad, 0, sizeof(int), st));
+#if defined(CPZ_CLOCK_PROBE)
+  ctx->clk_waves[0] = (size_t)((n + cpz::kRlcPrepBlock - 1) / cpz::kRlcPrepBlock) * (cpz::kRlcPrepBlock / 64);
+  CPZ_HIP(ctx->clk[0].ensure(ctx->clk_waves[0] * 40));
+  CPZ_HIP(hipMemsetAsync(ctx->clk[0].p, 0, ctx->clk_waves[0] * 40, st));
+  pa.clock_probe = static_cast<uint64_t*>(ctx->clk[0].p);
+#endif
   {
     StageTimer t(ctx, 2, st);
     CPZ_HIP(cpz::launch_rlc_prepare(pa, st));
@@ -1180,6 +1208,22 @@ int cpz_ctx_create(int device_ordinal, cpz_ctx** out) {
 int cpz_ctx_create_timing_only(int device_ordinal, cpz_ctx** out) { return ctx_create(device_ordinal, out); }
 #endif
 
+#if defined(CPZ_CLOCK_PROBE)
+// The clock stamps of the last k_rlc_prepare (kernel 0) or k_rlc_bucket (kernel 1) launch:
+// up to max_waves records of 5 words (a wave that did no work leaves zeros); *got = the
+// launch's waves.  Exported by CPZ_CLOCK_PROBE builds alone (tools/time_verify.py MODE=rlc).
+int cpz_ctx_clock_probe(cpz_ctx* ctx, int kernel, uint64_t* out, size_t max_waves, size_t* got) {
+  if (!ctx || !out || !got || kernel < 0 || kernel > 1) return fail(CPZ_EINVAL, "bad arguments");
+  CallLock lock(ctx);
+  CPZ_HIP(hipSetDevice(ctx->device));
+  CPZ_HIP(hipDeviceSynchronize());
+  const size_t w = std::min(max_waves, ctx->clk_waves[kernel]);
+  if (w) CPZ_HIP(hipMemcpy(out, ctx->clk[kernel].p, w * 40, hipMemcpyDeviceToHost));
+  *got = ctx->clk_waves[kernel];
+  return CPZ_OK;
+}
+#endif
+
 int cpz_abi_version(void) { return CPZ_ABI_VERSION; }
 
 int cpz_ctx_fallback_stats(cpz_ctx* ctx, uint64_t out[CPZ_FALLBACK_STATS]) {
@@ -1531,6 +1575,9 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
     b->release();
   ctx->rl_flags.release();
   ctx->rl_parts.release();
+#if defined(CPZ_CLOCK_PROBE)
+  for (DevBuf& b : ctx->clk) b.release();
+#endif
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->device >= 0 && ctx->device < 64) g_own_queues[ctx->device].fetch_sub(ctx->own_queues);
   delete ctx;

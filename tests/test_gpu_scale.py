@@ -134,7 +134,8 @@ def test_c3_service_contexts_partial_and_bisection(gpu):
     ctxs = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(n)]
     rows = gpu.prove_synthetic(n, SX, SK, contexts=ctxs)
     rows = {k: np.ascontiguousarray(rows[k]) for k in KEYS}
-    # few forgeries, spread out, so the bisection prunes clean parts (no density probe with contexts)
+    # few forgeries, spread out: the density probe (with contexts) sees at most one, so the
+    # fallback is the bisection, which prunes the clean parts
     forged = np.sort(rng.choice(n, size=24, replace=False))
     for j, i in enumerate(forged):
         if j % 2:
@@ -322,3 +323,106 @@ def test_two_contexts_in_flight_on_one_gpu(gpu):
     for p, ok, st in out[1]:
         assert not ok and p == want
         assert np.array_equal(np.nonzero(st)[0], idx) and set(st[idx].tolist()) == {1}
+
+
+def test_partitioned_fallback_with_service_contexts(gpu):
+    """configs[4]'s density on batches shaped like the service's (every entry with a 32-byte
+    challenge id as transcript context, service.rs:512-517; batch.rs:262-268): 2^22 proofs,
+    0.1 % forged -- half s + 1, half a replayed context (the proof verified under another
+    challenge id).  The density probe samples the batch WITH its contexts (k_probe_gather), so
+    the fallback is the partitioned check: exact forged set, the C oracle's partial of the
+    forged entries (with their contexts), and no clean block verified per proof."""
+    torch = pytest.importorskip("torch")
+    n = 1 << 22
+    dev = "cuda:0"
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5151)
+    cb = torch.randint(0, 256, (32 * n,), dtype=torch.int32, device=dev, generator=gen).to(torch.uint8)
+    co = torch.arange(n + 1, dtype=torch.int64, device=dev) * 32
+    t = {k: torch.empty((n, 32), dtype=torch.uint8, device=dev) for k in KEYS}
+    gpu.prove_synthetic_device(n, SX, SK, t["y1"], t["y2"], t["r1"], t["r2"], t["s"], ctx_bytes=cb, ctx_off=co)
+    rng = np.random.default_rng(2222)
+    idx = np.sort(rng.choice(n, size=n // 1000, replace=False))
+    bump, replay = idx[0::2], idx[1::2]
+    sel = torch.from_numpy(bump.astype(np.int64)).to(dev)
+    rows = t["s"].index_select(0, sel).cpu().numpy()
+    for r in range(rows.shape[0]):
+        rows[r] = np.frombuffer(((_le(rows[r]) + 1) % O.L).to_bytes(32, "little"), np.uint8)
+    t["s"].index_copy_(0, sel, torch.from_numpy(rows).to(dev))
+    cbv = cb.view(n, 32)
+    rsel = torch.from_numpy(replay.astype(np.int64)).to(dev)
+    cbv.index_copy_(0, rsel, cbv.index_select(0, (rsel + 1) % n).clone())   # another entry's challenge id
+    allsel = torch.from_numpy(idx.astype(np.int64)).to(dev)
+    host = {k: t[k].index_select(0, allsel).cpu().numpy() for k in KEYS}
+    hctx = [bytes(r) for r in cbv.index_select(0, allsel).cpu().numpy()]
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    p, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED, fallback=True, ctx_bytes=cb, ctx_off=co)
+    stats = gpu.fallback_stats()
+    got = st.cpu().numpy()
+    assert not ok
+    assert np.array_equal(np.nonzero(got)[0], idx) and set(got[idx].tolist()) == {1}
+    assert stats["path"] == "partitioned", stats
+    dirty = _blocks_with(idx, n)
+    assert stats["blocks_failing"] == dirty.size and stats["per_proof"] == 256 * dirty.size, stats
+    want, live = C.rlc_partial(host, idx, WSEED, contexts=hctx, threads=_threads())
+    assert live == idx.size and p == want
+
+
+def test_partitioned_fallback_decode_failures_and_equations_only(gpu, golden):
+    """The partitioned check with entries whose decode-level status is non-zero:
+    an undecodable r1, s + l (non-canonical), zero s and an identity r1, placed in blocks that
+    are otherwise clean, in failing blocks and in the partial last block, beside 0.1 % s + 1 /
+    wrong-y1 forgeries.  Those entries carry zero weight and keep their decode-level status
+    (2, 3, 5, 4); the partial is the oracle's over the live forged entries.  Then the same batch
+    with commitment checks off: identity r1 and zero s are judged by the equations (status 1,
+    and they keep their weight), the others are unchanged."""
+    torch = pytest.importorskip("torch")
+    n = (1 << 21) + 77
+    t = _synthetic_device(gpu, torch, n)
+    rng = np.random.default_rng(9191)
+    idx = np.sort(rng.choice(n, size=n // 1000, replace=False))
+    host = _forge(t, torch, idx)
+    dirty = set(int(b) for b in _blocks_with(idx, n))
+    clean = [b for b in range(0, (n + 255) // 256, 97) if b not in dirty][:8]
+    last = (n - 1) // 256
+    spots = []   # (entry, kind): a few per kind in clean blocks, failing blocks and the last block
+    for j, b in enumerate(clean + sorted(dirty)[:8] + [last]):
+        e = min(n - 1, 256 * b + 17 + j) if b != last else n - 3
+        if e in set(idx.tolist()):
+            e = e - 1
+        spots.append((e, ("bad_point", "s_plus_l", "zero_s", "identity_r")[j % 4]))
+    bad_pt = np.frombuffer(bytes.fromhex(golden["rfc9496_bad"][0]), np.uint8)
+    for e, kind in spots:
+        if kind == "bad_point":
+            t["r1"][e] = torch.from_numpy(bad_pt.copy()).to("cuda:0")
+        elif kind == "identity_r":
+            t["r1"][e] = 0
+        elif kind == "zero_s":
+            t["s"][e] = 0
+        else:
+            v = _le(t["s"][e].cpu().numpy()) + O.L
+            t["s"][e] = torch.from_numpy(np.frombuffer(v.to_bytes(32, "little"), np.uint8).copy()).to("cuda:0")
+    code = {"bad_point": 2, "s_plus_l": 3, "zero_s": 5, "identity_r": 4}
+    st = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    p, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED, fallback=True)
+    assert gpu.fallback_stats()["path"] == "partitioned"
+    got = st.cpu().numpy()
+    want = np.zeros(n, np.uint8)
+    want[idx] = 1
+    for e, kind in spots:
+        want[e] = code[kind]
+    assert not ok and np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    assert p == _oracle_partial(host, idx)
+    gpu.set_commitment_checks(False)
+    try:
+        p2, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED, fallback=True)
+        stats = gpu.fallback_stats()
+    finally:
+        gpu.set_commitment_checks(True)
+    for e, kind in spots:
+        if kind in ("zero_s", "identity_r"):
+            want[e] = 1
+    got = st.cpu().numpy()
+    assert stats["path"] == "partitioned" and not ok
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    assert p2 != p   # the two equation-judged entries are weighted now

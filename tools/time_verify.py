@@ -9,6 +9,58 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "chaum-pedersen-zkp_amd"))
 
 
+def _clock_summary(w):
+    """Per-wave clock records (rows of 5 int64: shader ticks, 100 MHz ticks, 100 MHz start /
+    end, hw id) -> mean / p10 / p90 shader clock in GHz and the wave time in us."""
+    import numpy as np
+    w = w[w[:, 1] > 0]
+    ghz = w[:, 0] / (w[:, 1] / 100e6) / 1e9
+    us = w[:, 1] / 100.0
+    return {"waves": int(len(w)), "shader_clock_ghz": {"mean": round(float(ghz.mean()), 4),
+                                                        "p10": round(float(np.percentile(ghz, 10)), 4),
+                                                        "p90": round(float(np.percentile(ghz, 90)), 4)},
+            "wave_time_us": {"mean": round(float(us.mean()), 1), "p10": round(float(np.percentile(us, 10)), 1),
+                             "p90": round(float(np.percentile(us, 90)), 1)}}
+
+
+def rlc_probe(cp, gpu, t, status, steps):
+    """MODE=rlc: the RLC batch check of the same proofs; the last step's k_rlc_prepare and
+    k_rlc_bucket clock stamps (cpz_ctx_clock_probe, CPZ_CLOCK_PROBE builds) and their
+    HIP-event times per step."""
+    import ctypes
+    import json
+
+    import numpy as np
+    import torch
+    seed = bytes(range(32))
+    for _ in range(2):
+        gpu.verify_batch_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status, seed)
+    torch.cuda.synchronize()
+    gpu.set_timing(True)
+    gpu.stage_times()
+    for _ in range(steps):
+        _, ok = gpu.verify_batch_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status, seed)
+    torch.cuda.synchronize()
+    st = gpu.stage_times()
+    lib = cp._native.load()
+    fn = lib.cpz_ctx_clock_probe
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+    out = {"what": "k_rlc_prepare / k_rlc_bucket built with -DCPZ_CLOCK_PROBE -DCPZ_TIMING_ONLY (rlc_dev.h "
+                   "ClockStamp): per wave, s_memtime / s_memrealtime around its work; the last of %d RLC steps "
+                   "over 2^20 proofs (tools/time_verify.py MODE=rlc)" % steps, "batch_ok": bool(ok)}
+    for k, name, stage in ((0, "k_rlc_prepare", "rlc_prepare"), (1, "k_rlc_bucket", "rlc_bucket")):
+        got = ctypes.c_size_t(0)
+        buf = np.zeros((1 << 22) * 5, np.uint64)
+        cp._native.check(fn(gpu._h, k, buf.ctypes.data, 1 << 22, ctypes.byref(got)))
+        w = buf[:5 * min(got.value, 1 << 22)].reshape(-1, 5).astype(np.int64)
+        rec = _clock_summary(w)
+        ms, cnt = st.get(stage, (0.0, 1))
+        rec["kernel_ms_per_step"] = ms / max(cnt, 1)
+        out[name] = rec
+    print(json.dumps(out))
+
+
 def main():
     import torch
     import chaum_pedersen as cp
@@ -19,6 +71,8 @@ def main():
     t = {k: torch.empty((n, 32), dtype=torch.uint8, device=dev) for k in ("y1", "y2", "r1", "r2", "s")}
     status = torch.empty(n, dtype=torch.uint8, device=dev)
     gpu.prove_synthetic_device(n, bytes(32), bytes(range(32)), t["y1"], t["y2"], t["r1"], t["r2"], t["s"])
+    if os.environ.get("MODE") == "rlc":
+        return rlc_probe(cp, gpu, t, status, steps)
     for _ in range(2):
         gpu.verify_each_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], status)
     torch.cuda.synchronize()
