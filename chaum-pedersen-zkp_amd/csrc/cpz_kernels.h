@@ -106,9 +106,12 @@ struct VerifyArgs {
                                  // decode-level status is non-zero keep it
   int eq_only = 0;                  // commitment checks off: identity r1 / r2 and zero s are not
                                     // reported, the equations alone decide (verify_proof)
-  const uint32_t* blocks = nullptr; // k_verify_prepared: workgroup g verifies the kVerifyBlock
-                                    // proofs of block blocks[g] (the partitioned check's failing
-                                    // blocks); n bounds the global proof index
+  const uint32_t* blocks = nullptr; // k_verify_prepared: the partitioned check's failing blocks of
+                                    // block_proofs proofs each, nblocks of them; workgroup g takes
+                                    // kVerifyBlock / block_proofs consecutive listed blocks; n bounds
+                                    // the global proof index
+  int block_proofs = 0;
+  int64_t nblocks = 0;
 };
 
 struct ProveArgs {

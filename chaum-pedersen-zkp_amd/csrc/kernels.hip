@@ -351,7 +351,12 @@ __device__ __forceinline__ void verify_one_row(const VerifyArgs& a, int64_t i, c
 __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_prepared(VerifyArgs a) {
   const CombTable comb_g{a.comb}, comb_h{a.comb + kCombPerBase};
   const int64_t l = (int64_t)blockIdx.x * kVerifyBlock + threadIdx.x;  // this launch's thread: its slab slot
-  const int64_t i = a.blocks ? (int64_t)a.blocks[blockIdx.x] * kVerifyBlock + threadIdx.x : l;  // one proof per thread
+  int64_t i = l;  // one proof per thread
+  if (a.blocks) {
+    const int64_t lb = (int64_t)blockIdx.x * (kVerifyBlock / a.block_proofs) + threadIdx.x / a.block_proofs;
+    if (lb >= a.nblocks) return;
+    i = (int64_t)a.blocks[lb] * a.block_proofs + threadIdx.x % a.block_proofs;
+  }
   if (i >= a.n) return;
   const SlabTable tab{a.scratch, (uint32_t)l * (uint32_t)(kCachedEntries * sizeof(ge_cached))};
   __shared__ uint32_t dig[16 * kVerifyBlock];

@@ -58,23 +58,27 @@ __device__ __forceinline__ int digit16(const uint2& g, int q) {
 
 // ---------------------------------------------------------------------------------------
 // k_part_sort: thread t holds proof t's four points (prepared order -r1, -y1, -r2, -y2),
-// threads 0 / 1 also g / h with the block's weight sums (ids 1024 / 1025).
+// threads 0 / 1 also g / h with the block's weight sums (ids 4 kPartProofs, + 1).
 // ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_part_sort(PartArgs a) {
+__global__ void __launch_bounds__(kPartProofs) k_part_sort(PartArgs a) {
+  constexpr int kT = kPartProofs;  // threads: one per proof of the block
   __shared__ uint32_t cur[kPartWindows][kPartBuckets];
   __shared__ uint32_t wtot[kPartWindows];
   __shared__ uint32_t wbase[kPartWindows + 1];
   __shared__ uint32_t top_over;
   const int64_t b = blockIdx.x, gb = a.blk0 + b;
   const int t = threadIdx.x;
-  for (int i = t; i < kPartWindows * kPartBuckets; i += 256) (&cur[0][0])[i] = 0;
+  for (int i = t; i < kPartWindows * kPartBuckets; i += kT) (&cur[0][0])[i] = 0;
   if (t == 0) top_over = 0;
   const int64_t pi = kPartProofs * gb + t;
   const int64_t j0 = 4 * pi;
   const bool in = pi < a.n;  // past the batch's end (last block): no entries
   int16_t ex[kRlcWindows];
-  if (t < 2) {
-    const sc s = a.block_sums[2 * gb + t];
+  if (t < 2) {  // the block's sum of a s (t = 0) / b s (t = 1): its one or two block sums
+    constexpr int R = kPartProofs / kRlcSumBlock;
+    sc s = a.block_sums[2 * (R * gb) + t];
+#pragma unroll
+    for (int r = 1; r < R; r++) s = sc_add(s, a.block_sums[2 * (R * gb + r) + t]);
     recode16(ex, s.w);
   }
   __syncthreads();
@@ -103,11 +107,11 @@ __global__ void __launch_bounds__(256) k_part_sort(PartArgs a) {
   if (t >= kPartTopBuckets && t < kPartBuckets && cur[kPartWindows - 1][t] != 0) top_over = 1;
   __syncthreads();
   if (t == 0) a.fail[gb] = top_over ? 1 : 0;
-  // exclusive scan of each window's 128 counts: wave wv takes windows wv, wv + 4, ...; lane l
-  // buckets 2l and 2l + 1
+  // exclusive scan of each window's 128 counts: wave wv takes windows wv, wv + kT / 64, ...;
+  // lane l buckets 2l and 2l + 1
   {
     const int lane = t & 63, wv = t >> 6;
-    for (int v = wv; v < kPartWindows; v += 4) {
+    for (int v = wv; v < kPartWindows; v += kT / 64) {
       const uint32_t c0 = cur[v][2 * lane], c1 = cur[v][2 * lane + 1], s = c0 + c1;
       uint32_t x = s;
 #pragma unroll
@@ -131,7 +135,7 @@ __global__ void __launch_bounds__(256) k_part_sort(PartArgs a) {
   }
   __syncthreads();
   uint16_t* offs = a.offs + b * kPartOffs;
-  for (int i = t; i < kPartOffs; i += 256) {
+  for (int i = t; i < kPartOffs; i += kT) {
     const int v = i / (kPartBuckets + 1), k = i % (kPartBuckets + 1);
     offs[i] = (uint16_t)(k < kPartBuckets ? wbase[v] + cur[v][k] : wbase[v + 1]);
   }
@@ -165,7 +169,7 @@ __global__ void __launch_bounds__(256) k_part_sort(PartArgs a) {
     if (t < kPartUnits) a.assign[b * kPartUnits + t] = (uint16_t)(asg[0][t] | (asg[1][t] << 8));
   }
   __syncthreads();
-  for (int i = t; i < kPartWindows * kPartBuckets; i += 256) (&cur[0][0])[i] += wbase[i / kPartBuckets];
+  for (int i = t; i < kPartWindows * kPartBuckets; i += kT) (&cur[0][0])[i] += wbase[i / kPartBuckets];
   __syncthreads();
   uint16_t* list = a.lists + b * kPartListCap;
 #pragma unroll 1
@@ -442,7 +446,7 @@ __global__ void __launch_bounds__(64) k_part_sum2(const ge_p3* tmp, int64_t m, u
 
 hipError_t launch_part_msm(const PartArgs& a, hipStream_t st) {
   if (a.nblk <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_part_sort, dim3((unsigned)a.nblk), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_part_sort, dim3((unsigned)a.nblk), dim3(kPartProofs), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_part_acc, dim3((unsigned)((a.nblk + 3) / 4)), dim3(256), 0, st, a);

@@ -14,7 +14,8 @@ constexpr int kRlcBuckets = 1 << 15;     // |digit| in [1, 2^15]
 #define CPZ_RLC_SEGLEN 32
 #endif
 constexpr int kRlcSegLen = CPZ_RLC_SEGLEN;  // buckets per reduction segment
-constexpr int kRlcPrepBlock = 256;       // proofs per prepare block (= block_sums granule)
+constexpr int kRlcPrepBlock = 256;       // proofs per prepare workgroup (the bisection / shard / span granule)
+constexpr int kRlcSumBlock = 128;        // proofs per block sum (block_sums granule; kRlcPrepBlock / 2)
 #ifndef CPZ_RLC_PREP_WIDE_MAX
 #define CPZ_RLC_PREP_WIDE_MAX (1 << 15)
 #endif
@@ -47,7 +48,7 @@ struct RlcPrepArgs {
   ge_niels* pts;                 // 4 n (+2 extra) negated affine points
   int16_t* digits;               // [16][dstride] signed radix-2^16 digits
   int64_t dstride;
-  sc* block_sums;                // [ceil(n/256)][2]
+  sc* block_sums;                // [2 ceil(n/256)][2]: sum a s, sum b s per 128 proofs
   sc* quarter_sums = nullptr;    // [ceil(n/64)][2]: scratch of the four-lanes-per-proof prepare
   int* any_bad;                  // set to 1 if some proof has a non-zero decode-level status
   int eq_only = 0;               // commitment checks off: identity r1 / r2 keep their weight
@@ -90,7 +91,11 @@ struct RlcMsmArgs {
 // Pippenger MSM per block with signed 8-bit windows (the 16-bit digits of the prepare split in
 // two), giving every block's partial P_b = sum over its proofs of the RLC terms.  A block with
 // P_b the identity holds no forgery (w.o.p.); the others go to per-proof verification.
-constexpr int kPartProofs = kRlcPrepBlock;           // 256 proofs per block
+#ifndef CPZ_PART_PROOFS
+#define CPZ_PART_PROOFS 256
+#endif
+constexpr int kPartProofs = CPZ_PART_PROOFS;          // proofs per block (128 or 256)
+static_assert(kPartProofs == 128 || kPartProofs == 256, "partition blocks are one or two block sums");
 constexpr int kPartPoints = 4 * kPartProofs + 2;      // + g, h with the block's weight sums
 constexpr int kPartWindows = 2 * kRlcWindows;         // 32 signed radix-2^8 windows
 constexpr int kPartBuckets = 128;                     // |digit| in [1, 128]
@@ -108,7 +113,7 @@ struct PartArgs {
   const ge_niels* pts;           // prepared negated Niels points, 4 per proof
   const int16_t* digits;         // [16][dstride] signed radix-2^16 digits
   int64_t dstride;
-  const sc* block_sums;          // [blocks][2]: sum a s, sum b s per block
+  const sc* block_sums;          // [sum blocks][2]: sum a s, sum b s per kRlcSumBlock proofs
   const ge_niels* tab;           // g at tab[0], h at tab[kNielsEntriesRlc]
   uint16_t* lists;               // [nblk][kPartListCap] point ids (bit 15: negate) sorted by (window, bucket)
   uint16_t* offs;                // [nblk][kPartOffs] bucket starts per window (+ window end)

@@ -116,18 +116,20 @@ __global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_prepare(RlcPrepArgs a)
     }
   }
   clk.stop(a.clock_probe, i >> 6);
-  // block sums of a_i s_i, b_i s_i (mod l)
+  // block sums of a_i s_i, b_i s_i (mod l), one per kRlcSumBlock proofs (two per workgroup)
+  static_assert(kRlcPrepBlock == 2 * kRlcSumBlock, "two block sums per prepare workgroup");
   __syncthreads();
-  for (int off = kRlcPrepBlock / 2; off > 0; off >>= 1) {
-    if (threadIdx.x < off) {
+  for (int off = kRlcSumBlock / 2; off > 0; off >>= 1) {
+    if ((threadIdx.x % kRlcSumBlock) < off) {
       red_a[threadIdx.x] = sc_add(red_a[threadIdx.x], red_a[threadIdx.x + off]);
       red_b[threadIdx.x] = sc_add(red_b[threadIdx.x], red_b[threadIdx.x + off]);
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    a.block_sums[2 * blockIdx.x] = red_a[0];
-    a.block_sums[2 * blockIdx.x + 1] = red_b[0];
+  if (threadIdx.x % kRlcSumBlock == 0) {
+    const int64_t sb = 2 * (int64_t)blockIdx.x + threadIdx.x / kRlcSumBlock;
+    a.block_sums[2 * sb] = red_a[threadIdx.x];
+    a.block_sums[2 * sb + 1] = red_b[threadIdx.x];
   }
 }
 
@@ -214,9 +216,11 @@ __global__ void __launch_bounds__(256, 2) k_rlc_prepare4(RlcPrepArgs a) {
   }
 }
 
-// block_sums of a wide prepare: 256-proof block b is quarters 4 b .. 4 b + 3 (those that exist).
+// block_sums of a wide prepare: sum block b (kRlcSumBlock = 128 proofs) is quarters 2 b and
+// 2 b + 1 (those that exist).
 __global__ void __launch_bounds__(64) k_rlc_bsum4(const sc* __restrict__ quarter_sums, int64_t nq,
                                                   sc* __restrict__ block_sums, int64_t nb) {
+  static_assert(kRlcSumBlock == 128, "two 64-proof quarters per block sum");
   const int64_t t = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (t >= 2 * nb) return;
   const int64_t b = t >> 1;
@@ -224,12 +228,12 @@ __global__ void __launch_bounds__(64) k_rlc_bsum4(const sc* __restrict__ quarter
   sc acc;
 #pragma unroll
   for (int k = 0; k < 8; k++) acc.w[k] = 0;
-  for (int64_t k = 4 * b; k < 4 * b + 4 && k < nq; k++) acc = sc_add(acc, quarter_sums[2 * k + ab]);
+  for (int64_t k = 2 * b; k < 2 * b + 2 && k < nq; k++) acc = sc_add(acc, quarter_sums[2 * k + ab]);
   block_sums[2 * b + ab] = acc;
 }
 
 // ---------------------------------------------------------------------------------------
-// k_rlc_extra: g and h with scalars sum_{blocks in [b0, b1)} (a s), (b s).
+// k_rlc_extra: g and h with scalars sum_{sum blocks in [b0, b1)} (a s), (b s).
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_rlc_extra(RlcMsmArgs a, const sc* __restrict__ block_sums, int64_t b0,
                                                    int64_t b1, const ge_niels* __restrict__ tab) {
@@ -853,8 +857,8 @@ hipError_t launch_rlc_prepare(const RlcPrepArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_rlc_prepare4, dim3((unsigned)nq), dim3(256), 0, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_rlc_bsum4, dim3((unsigned)((2 * blocks + 63) / 64)), dim3(64), 0, st, a.quarter_sums, nq,
-                       a.block_sums, blocks);
+    hipLaunchKernelGGL(k_rlc_bsum4, dim3((unsigned)((4 * blocks + 63) / 64)), dim3(64), 0, st, a.quarter_sums, nq,
+                       a.block_sums, 2 * blocks);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_rlc_prepare, dim3((unsigned)blocks), dim3(kRlcPrepBlock), 0, st, a);

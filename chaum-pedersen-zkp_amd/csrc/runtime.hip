@@ -576,7 +576,7 @@ int rlc_reserve_prepared(RlcPrepared& P, int64_t n) {
   P.cap = 0;  // stays 0 unless every buffer is in place
   CPZ_HIP(P.pts.ensure((size_t)npts * sizeof(cpz::ge_niels)));
   CPZ_HIP(P.dig.ensure((size_t)rlc_dstride(n) * cpz::kRlcWindows * sizeof(int16_t)));
-  CPZ_HIP(P.bsum.ensure((size_t)nblk * 2 * sizeof(cpz::sc)));
+  CPZ_HIP(P.bsum.ensure((size_t)nblk * 2 * 2 * sizeof(cpz::sc)));  // two sum blocks per prepare block
   CPZ_HIP(P.qsum.ensure((size_t)((std::min(n, cpz::kRlcPrepWideMax) + 63) / 64) * 2 * sizeof(cpz::sc)));
   P.cap = n;
   return CPZ_OK;
@@ -661,6 +661,7 @@ int rlc_msm_args(const RlcPrepared& P, RlcMsmSet& S, int64_t lo, int64_t hi, cpz
 // one.  Synchronises; returns the partial encoding and identity flag.
 int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t partial[32], int* identity) {
   static_assert(CPZ_RLC_SPAN % cpz::kRlcPrepBlock == 0, "spans are whole weight blocks");
+  static_assert(cpz::kRlcPrepBlock % cpz::kRlcSumBlock == 0, "ranges are whole block sums");
   static_assert(4ll * CPZ_RLC_SPAN + 2 <= cpz::kRlcMaxMsmPoints, "a span's MSM exceeds the sort-entry format");
   RlcMsmSet& S = ctx->rl_msm;
   const int64_t nspan = (hi - lo + CPZ_RLC_SPAN - 1) / CPZ_RLC_SPAN;
@@ -673,8 +674,8 @@ int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t part
       m.total_first = j == 0;
       m.total_last = j == nspan - 1;
     }
-    const int64_t b0 = slo / cpz::kRlcPrepBlock;
-    const int64_t b1 = (shi + cpz::kRlcPrepBlock - 1) / cpz::kRlcPrepBlock;
+    const int64_t b0 = slo / cpz::kRlcSumBlock;
+    const int64_t b1 = (shi + cpz::kRlcSumBlock - 1) / cpz::kRlcSumBlock;
 #if defined(CPZ_CLOCK_PROBE)
     {  // k_rlc_bucket's grid: (ceil(chunks / 256), 16) blocks of 4 waves (launch_rlc_msm)
       const int64_t chunks = ((m.p1 - m.p0) + 2 + m.echunk - 1) / m.echunk;
@@ -885,17 +886,20 @@ int launch_probe(cpz_ctx* ctx, size_t n, const void* const rows[5], const void* 
   return kProbeChunks;
 }
 
-// Per-proof verification (k_verify_prepared) of the listed blocks of kVerifyBlock proofs of the
-// prepared batch: launches of at most half the occupancy grid, round-robin over the verify
-// streams and their scratch slabs (as launch_verify_chunks).
+// Per-proof verification (k_verify_prepared) of the listed partition blocks (kPartProofs proofs
+// each) of the prepared batch: a workgroup takes kVerifyBlock / kPartProofs consecutive listed
+// blocks; launches of at most half the occupancy grid, round-robin over the verify streams and
+// their scratch slabs (as launch_verify_chunks).
 int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* status, const uint32_t* d_blocks,
                            int64_t nb, hipStream_t st) {
-  static_assert(cpz::kVerifyBlock == cpz::kPartProofs, "a listed block is one verify workgroup");
+  static_assert(cpz::kVerifyBlock % cpz::kPartProofs == 0, "whole listed blocks per verify workgroup");
+  constexpr int64_t G = cpz::kVerifyBlock / cpz::kPartProofs;
   if (nb <= 0) return CPZ_OK;
   const int full = (occupancy_grid(ctx) + CPZ_VERIFY_CHUNK_DIV - 1) / CPZ_VERIFY_CHUNK_DIV;
   const size_t slab = (size_t)full * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached);
   CPZ_HIP(ctx->scratch.ensure((size_t)CPZ_VERIFY_STREAMS * slab));
-  const int64_t chunks = (nb + full - 1) / full;
+  const int64_t groups = (nb + G - 1) / G;
+  const int64_t chunks = (groups + full - 1) / full;
   const int nst = (int)std::min<int64_t>(CPZ_VERIFY_STREAMS, chunks);
   if (nst > 1) {
     if (!ctx->aux_start) CPZ_HIP(hipEventCreateWithFlags(&ctx->aux_start, hipEventDisableTiming));
@@ -914,11 +918,13 @@ int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* stat
   va.comb = static_cast<const cpz::ge_niels*>(ctx->gs->comb.p);
   va.pre = static_cast<const cpz::ge_niels*>(ctx->rl_prep.pts.p);
   va.eq_only = ctx->call_eq ? 1 : 0;
+  va.block_proofs = cpz::kPartProofs;
   for (int64_t c = 0; c < chunks; c++) {
     const int64_t g0 = c * full;
-    const int g = (int)std::min<int64_t>(full, nb - g0);
+    const int g = (int)std::min<int64_t>(full, groups - g0);
     cpz::VerifyArgs v = va;
-    v.blocks = d_blocks + g0;
+    v.blocks = d_blocks + g0 * G;
+    v.nblocks = std::min<int64_t>(nb - g0 * G, (int64_t)g * G);
     const int k = (int)(c % nst);
     v.scratch = static_cast<char*>(ctx->scratch.p) + (size_t)k * slab;
     hipStream_t sc = k == 0 ? st : ctx->aux_stream[k - 1];
@@ -935,15 +941,17 @@ int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* stat
 }
 
 // Blocks per launch of the partitioned MSM's sort and walk: 2^24 proofs, ~4.8 GB of lists and
-// offsets (~72 KB per block); the window sums, 40 KB per block, are kept for the whole batch so
-// that one combine launch covers every block.  Per 8192 blocks the launch tails cost C5 5 ms
-// (227.9 / 229.5 ms against 223.7 / 223.6 at 65536, 224.6 / 224.9 at 32768; A/B, one call).
-constexpr int64_t kPartChunkBlocks = 65536;
+// offsets (~72 KB per 256-proof block); the window sums, 40 KB per block, are kept for the whole
+// batch so that one combine launch covers every block.  Per 8192 blocks the launch tails cost C5
+// 5 ms (227.9 / 229.5 ms against 223.7 / 223.6 at 65536, 224.6 / 224.9 at 32768; A/B, one call).
+constexpr int64_t kPartChunkBlocks = (int64_t(1) << 24) / cpz::kPartProofs;
 // Density probe outcomes (invalid entries among the kProbeChunks x 256 sampled) for which the
-// partitioned check pays: its MSM costs ~0.3 of per-proof verification per proof, and a block
-// of 256 is clean with probability (1 - rho)^256; above ~12 sampled (rho > ~0.3 %) more than
-// half the blocks fail and plain per-proof verification is cheaper.
-constexpr int kPartMaxProbeBad = 12;
+// partitioned check pays.  Relative to per-proof verification its prepare costs ~0.19, its
+// block partials ~0.32 (256-proof blocks) or ~0.36 (128), and the per-proof pass over a failing
+// block's proofs ~0.83 (no decodes); a block of B proofs is clean with probability (1 - rho)^B.
+// So it pays while 1 - (1 - rho)^B < ~0.59 (B = 256: rho < ~0.35 %, ~14 sampled) or ~0.54
+// (B = 128: rho < ~0.6 %, ~25 sampled); the limits keep a margin.
+constexpr int kPartMaxProbeBad = cpz::kPartProofs == 128 ? 20 : 12;
 
 // Every buffer the partitioned check of n proofs uses: the prepared batch, the partial / flag
 // words of an MSM set, one chunk's sorted lists / assignment / offsets, and the whole batch's

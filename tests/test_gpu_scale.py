@@ -247,15 +247,24 @@ def test_spans_forged_only_in_a_later_span(gpu):
     assert ok and p == bytes(32)
 
 
-def _blocks_with(idx, n):
-    return np.unique(np.asarray(idx) // 256)
+def _part_block(n, stats):
+    """The partitioned check's block size (128 or 256 proofs), from the blocks it checked."""
+    b = 1
+    while b * stats["blocks_checked"] < n:
+        b <<= 1
+    assert b in (128, 256) and -(-n // b) == stats["blocks_checked"], (n, stats)
+    return b
+
+
+def _blocks_with(idx, b):
+    return np.unique(np.asarray(idx) // b)
 
 
 @pytest.mark.parametrize("n", [1 << 22, (1 << 20) + 77])
 def test_partitioned_fallback_at_c5_density(gpu, n):
     """configs[4]'s density (0.1 % forged, half s + 1, half wrong y1) through the batch check
     with its fallback: the density probe sees a few invalid samples, so the fallback is the
-    partitioned check -- every 256-proof block's RLC partial, then per-proof verification of
+    partitioned check -- every block's RLC partial (128 or 256 proofs), then per-proof verification of
     the failing blocks ONLY.  Checked: the exact forged set (statuses 1 there, 0 elsewhere);
     the batch partial equals the C oracle's partial of the forged entries alone; the path
     taken; the failing blocks are exactly the blocks holding a forgery; and no entry of a
@@ -274,10 +283,10 @@ def test_partitioned_fallback_at_c5_density(gpu, n):
     assert not ok
     assert np.array_equal(np.nonzero(got)[0], idx) and set(got[idx].tolist()) == {1}
     assert stats["path"] == "partitioned", stats
-    dirty = _blocks_with(idx, n)
-    nblk = (n + 255) // 256
-    assert stats["blocks_checked"] == nblk and stats["blocks_failing"] == dirty.size, (stats, dirty.size)
-    want_pp = sum(min(256, n - 256 * int(b)) for b in dirty)
+    B = _part_block(n, stats)
+    dirty = _blocks_with(idx, B)
+    assert stats["blocks_failing"] == dirty.size, (stats, dirty.size)
+    want_pp = sum(min(B, n - B * int(b)) for b in dirty)
     assert stats["per_proof"] == want_pp
     assert p == _oracle_partial(host, idx)
 
@@ -362,8 +371,9 @@ def test_partitioned_fallback_with_service_contexts(gpu):
     assert not ok
     assert np.array_equal(np.nonzero(got)[0], idx) and set(got[idx].tolist()) == {1}
     assert stats["path"] == "partitioned", stats
-    dirty = _blocks_with(idx, n)
-    assert stats["blocks_failing"] == dirty.size and stats["per_proof"] == 256 * dirty.size, stats
+    B = _part_block(n, stats)
+    dirty = _blocks_with(idx, B)
+    assert stats["blocks_failing"] == dirty.size and stats["per_proof"] == B * dirty.size, stats
     want, live = C.rlc_partial(host, idx, WSEED, contexts=hctx, threads=_threads())
     assert live == idx.size and p == want
 
@@ -382,12 +392,14 @@ def test_partitioned_fallback_decode_failures_and_equations_only(gpu, golden):
     rng = np.random.default_rng(9191)
     idx = np.sort(rng.choice(n, size=n // 1000, replace=False))
     host = _forge(t, torch, idx)
-    dirty = set(int(b) for b in _blocks_with(idx, n))
-    clean = [b for b in range(0, (n + 255) // 256, 97) if b not in dirty][:8]
-    last = (n - 1) // 256
+    B = 128   # spots placed per 128 proofs: inside one block whether blocks are 128 or 256 proofs
+    dirty256 = set(int(b) for b in _blocks_with(idx, 256))
+    dirty = set(int(b) for b in _blocks_with(idx, B))
+    clean = [b for b in range(0, (n + B - 1) // B, 97) if b // 2 not in dirty256][:8]
+    last = (n - 1) // B
     spots = []   # (entry, kind): a few per kind in clean blocks, failing blocks and the last block
     for j, b in enumerate(clean + sorted(dirty)[:8] + [last]):
-        e = min(n - 1, 256 * b + 17 + j) if b != last else n - 3
+        e = min(n - 1, B * b + 17 + j) if b != last else n - 3
         if e in set(idx.tolist()):
             e = e - 1
         spots.append((e, ("bad_point", "s_plus_l", "zero_s", "identity_r")[j % 4]))
