@@ -91,8 +91,12 @@ struct RlcMsmArgs {
 // Pippenger MSM per block with signed 8-bit windows (the 16-bit digits of the prepare split in
 // two), giving every block's partial P_b = sum over its proofs of the RLC terms.  A block with
 // P_b the identity holds no forgery (w.o.p.); the others go to per-proof verification.
+// 128: C5 210.8 / 210.0 ms against 221.3 / 221.8 ms with 256-proof blocks (A/B, one call): the
+// failing blocks' per-proof pass halves (12 % of the proofs at 0.1 % forged instead of 23 %),
+// the block partials cost 16 % more per proof (98 -> 114 ms: the 32 x 128 bucket boundaries per
+// block are spread over half the entries).
 #ifndef CPZ_PART_PROOFS
-#define CPZ_PART_PROOFS 256
+#define CPZ_PART_PROOFS 128
 #endif
 constexpr int kPartProofs = CPZ_PART_PROOFS;          // proofs per block (128 or 256)
 static_assert(kPartProofs == 128 || kPartProofs == 256, "partition blocks are one or two block sums");

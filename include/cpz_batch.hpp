@@ -48,8 +48,11 @@ constexpr std::size_t MAX_BATCH_SIZE = 1000;  // batch.rs:48
 
 // Smallest Parameters group that takes the RLC batch check rather than per-proof
 // verification (both return verify_one's outcome per entry).  The same threshold as
-// rust/reference-patch/gpu.rs (RLC_MIN_GROUP); measured in profiles/r04_small_batch.json.
-constexpr std::size_t RLC_MIN_GROUP = 2;
+// rust/reference-patch/gpu.rs (RLC_MIN_GROUP), from the per-call latency table
+// profiles/r04_small_batch.json: one synchronous host-buffer call takes 0.78-0.83 ms through
+// the RLC check and 1.26-1.68 ms per proof at every n from 1 to 1000, so every group of a
+// multi-entry batch takes the RLC check (a one-entry batch is verify_one, batch.rs:178-180).
+constexpr std::size_t RLC_MIN_GROUP = 1;
 
 using Bytes32 = std::array<uint8_t, 32>;
 

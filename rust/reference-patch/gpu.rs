@@ -55,8 +55,10 @@ const CONTEXTS_PER_DEVICE: usize = 2;
 /// Smallest `Parameters` group sent to the RLC batch check; smaller groups are verified per
 /// proof (cpz_verify_each).  Both return `verify_one`'s outcome; the threshold only picks the
 /// faster entry point at the batch sizes this API carries (n <= 1000, batch.rs:48), from the
-/// per-call latency table profiles/r04_small_batch.json (bench.py small_batch).
-const RLC_MIN_GROUP: usize = 2;
+/// per-call latency table profiles/r04_small_batch.json (bench.py small_batch): 0.78-0.83 ms
+/// per RLC call against 1.26-1.68 ms per-proof at every n from 1 to 1000, so every group of a
+/// multi-entry batch takes the RLC check.
+const RLC_MIN_GROUP: usize = 1;
 
 /// The process's verifier contexts (see above).
 struct Pool {
