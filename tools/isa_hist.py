@@ -25,11 +25,11 @@ def kernel_lines(path, name):
     return out
 
 
-def main():
-    path, name = sys.argv[1], sys.argv[2]
+def parse(path, name):
+    """(instructions [(mnemonic, text)], loops [(first, last, label)] innermost first)."""
     lines = kernel_lines(path, name)
     labels = {}
-    insts = []  # (index, mnemonic, text)
+    insts = []
     for ln in lines:
         s = ln.strip()
         if not s or s.startswith(";") or s.startswith("."):
@@ -37,10 +37,7 @@ def main():
             if m:
                 labels[m.group(1)] = len(insts)
             continue
-        mn = s.split()[0]
-        insts.append((mn, s))
-    total = collections.Counter(mn for mn, _ in insts)
-    print("kernel %s: %d instructions" % (name, len(insts)))
+        insts.append((s.split()[0], s))
     loops = []
     for idx, (mn, s) in enumerate(insts):
         if mn.startswith("s_cbranch") or mn == "s_branch":
@@ -48,6 +45,20 @@ def main():
             if tgt in labels and labels[tgt] <= idx:
                 loops.append((labels[tgt], idx, tgt))
     loops.sort(key=lambda t: t[1] - t[0])
+    return insts, loops
+
+
+def loop_bodies(path, name):
+    """[(label, Counter of mnemonics)] per loop body, innermost first."""
+    insts, loops = parse(path, name)
+    return [(tgt, collections.Counter(mn for mn, _ in insts[lo:hi + 1])) for lo, hi, tgt in loops]
+
+
+def main():
+    path, name = sys.argv[1], sys.argv[2]
+    insts, loops = parse(path, name)
+    total = collections.Counter(mn for mn, _ in insts)
+    print("kernel %s: %d instructions" % (name, len(insts)))
     for lo, hi, tgt in loops:
         body = collections.Counter(mn for mn, _ in insts[lo:hi + 1])
         n = hi + 1 - lo
