@@ -347,7 +347,8 @@ class Gpu:
         _native.check(self._lib.cpz_ctx_fallback_stats(self._h, out))
         return {"path": _native.FALLBACK_PATHS.get(int(out[0]), str(out[0])), "probe_invalid": int(out[1]),
                 "blocks_checked": int(out[2]), "blocks_failing": int(out[3]), "per_proof": int(out[4]),
-                "bisection_msms": int(out[5])}
+                "bisection_msms": int(out[5]), "blocks_indexed": int(out[6]),
+                "blocks_located": int(out[7])}
 
     # -- commitment checks (cpz_ctx_set_commitment_checks) ------------------------------------
     def set_commitment_checks(self, enable: bool) -> None:

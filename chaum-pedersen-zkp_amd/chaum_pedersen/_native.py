@@ -38,9 +38,9 @@ EXPORTED = (
 )
 CALL_EQUATIONS_ONLY = 1   # CPZ_CALL_EQUATIONS_ONLY: commitment checks off for one call
 NUM_STAGES = 16
-FALLBACK_STATS = 6
+FALLBACK_STATS = 8
 FALLBACK_PATHS = {0: "none", 1: "bisection", 2: "partitioned", 3: "per_proof"}
-ABI_VERSION = 4     # CPZ_ABI_VERSION of the cpz.h these declarations follow
+ABI_VERSION = 5     # CPZ_ABI_VERSION of the cpz.h these declarations follow
 
 
 class CpzError(RuntimeError):

@@ -1,18 +1,18 @@
 // Partitioned batch check on gfx950: the random-linear-combination partial of every block of
-// 256 proofs, so that a failing batch goes to per-proof verification only where a block
-// fails -- the fallback of verify_batch (batch.rs:262-268) / verify_individually
-// (batch.rs:314-318) at forgery densities where bisection cannot prune (configs[4]: 0.1 %
-// forged leaves ~77 % of 256-proof blocks clean, but every range of a few thousand proofs
-// dirty).
+// kPartProofs (128) proofs, so that a failing batch goes to per-proof verification only where a
+// block fails, and within a failing block holding one forgery only to that entry -- the
+// fallback of verify_batch (batch.rs:262-268) / verify_individually (batch.rs:314-318) at
+// forgery densities where bisection cannot prune (configs[4]: 0.1 % forged leaves ~88 % of
+// 128-proof blocks clean, but every range of a few thousand proofs dirty).
 //
 // Block b's partial is the corrected batch equation over its own proofs (rlc.hip header):
 //   P_b = sum_{i in b} [a_i s_i] g - [a_i] r1_i - [a_i c_i] y1_i + [b_i s_i] h - [b_i] r2_i - [b_i c_i] y2_i
 // with the same 128-bit weights, so sum_b P_b is the batch's partial, and P_b is the identity
 // iff every proof of b satisfies both equations (except with probability 2^-128 per forged
-// proof).  It is one Pippenger MSM per block over 1026 points (the block's 4 x 256 prepared
-// points and g, h with the block's weight sums): signed radix-2^8 digits (each radix-2^16
-// digit d of the prepare split as d = lo + 2^8 hi, lo in [-128, 128), hi in [-128, 128]),
-// 32 windows of 128 buckets.
+// proof).  It is one Pippenger MSM per block over kPartPoints points (the block's 4 x kPartProofs
+// prepared points and g, h with the block's weight sums): signed radix-2^8 digits (each
+// radix-2^16 digit d of the prepare split as d = lo + 2^8 hi, lo in [-128, 128), hi in
+// [-128, 128]), 32 windows of 128 buckets.
 //   k_part_sort     1 workgroup / block: LDS counting sort of the block's entries by (window,
 //                   bucket) -> a list of 16-bit point ids and per-window bucket offsets.
 //   k_part_acc      1 wave / block; a lane walks two units -- (window v, share h): buckets
@@ -25,8 +25,11 @@
 //                   selected operands, so lanes at different buckets never diverge.
 //   k_part_combine  1 quad / block (16 blocks per wave): T_v = sum_d d B_d from the four lanes'
 //                   (acc, run), P_b = sum_v 2^(8 v) T_v by Horner, quad-cooperative; P_b and its
-//                   identity flag.
+//                   flags.
 //   k_part_sum1/2   sum_b P_b -> the batch partial (encoded only when it is not the identity).
+// The locate pass over the failing blocks (rlc.h): k_part_index_digits (the same scalars times
+// j_t = kPartLocJ0 - 2 t), the same sort / walk (on the prepared points, through PartArgs::pmap)
+// / combine -> P'_b, and k_part_locate (the one t with P'_b = [j_t] P_b, if there is one).
 #include <hip/hip_runtime.h>
 
 #include "rlc.h"
@@ -106,7 +109,7 @@ __global__ void __launch_bounds__(kPartProofs) k_part_sort(PartArgs a) {
   // miss the entry (k_part_combine ORs its identity test into this flag).
   if (t >= kPartTopBuckets && t < kPartBuckets && cur[kPartWindows - 1][t] != 0) top_over = 1;
   __syncthreads();
-  if (t == 0) a.fail[gb] = top_over ? 1 : 0;
+  if (t == 0) a.fail[gb] = top_over ? 2 : 0;
   // exclusive scan of each window's 128 counts: wave wv takes windows wv, wv + kT / 64, ...;
   // lane l buckets 2l and 2l + 1
   {
@@ -268,7 +271,7 @@ __global__ void __launch_bounds__(256, 2) k_part_acc(PartArgs a) {
   int v = (units & 0xff) >> 2, h = units & 3;
   const uint16_t* list = a.lists + b * kPartListCap;
   const uint16_t* ob = a.offs + b * kPartOffs;
-  const ge_niels* P = a.pts + (int64_t)4 * kPartProofs * gb;
+  const ge_niels* P = a.pts + (int64_t)4 * kPartProofs * (a.pmap ? (int64_t)a.pmap[gb] : gb);
   ge_p3* ws = a.wsum + gb * kPartWsum;  // indexed by the global block: one combine pass for all chunks
   uint4 (*slot)[64] = lds[wv];
   int width = part_width(v), klo = width * h, k = klo;
@@ -401,7 +404,7 @@ __global__ void __launch_bounds__(64) k_part_combine(PartArgs a) {
   }
   if (live && q == 0) {
     store_p3(a.part + a.blk0 + b, P);
-    a.fail[a.blk0 + b] = (a.fail[a.blk0 + b] || !ristretto_is_identity(P)) ? 1 : 0;  // k_part_sort's flag
+    a.fail[a.blk0 + b] = a.fail[a.blk0 + b] | (ristretto_is_identity(P) ? 0 : 1);  // k_part_sort's bit 1
   }
 }
 
@@ -442,6 +445,156 @@ __global__ void __launch_bounds__(64) k_part_sum2(const ge_p3* tmp, int64_t m, u
       identity_out[0] = id ? 1 : 0;
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Locating the forged entry of a failing block (rlc.h: P'_b = sum_i j_i E_i, j = kPartLocJ0 - 2 t).
+// k_part_index_digits: listed block b, thread t = proof kPartProofs * blocks[b] + t of the
+// prepared batch: the first pass's scalars (weights from the same ChaCha20 block, rlc.hip
+// k_rlc_prepare) times j -- the r-points' j a_i as an integer (nine signed radix-2^16 digits;
+// j < 2^16 - 256 keeps |digit 8| < 2^15 - 128), j a_i c_i mod l and j b_i c_i mod l recoded, and
+// the block sums of j a_i s_i, j b_i s_i.  Zero digits and sum terms where the prepare gave zero
+// weight.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void index_weight_digits(int16_t d[kRlcWindows], const uint32_t u[4], int64_t j) {
+  int64_t carry = 0;
+#pragma unroll
+  for (int w = 0; w < 8; w++) {
+    const int64_t chunk = j * (int64_t)(int16_t)(u[w >> 1] >> (16 * (w & 1))) + carry;  // |chunk| < 2^31
+    const int64_t lo = ((chunk + 0x8000) & 0xffff) - 0x8000;
+    d[w] = (int16_t)lo;
+    carry = (chunk - lo) >> 16;
+  }
+  d[8] = (int16_t)carry;
+#pragma unroll
+  for (int w = 9; w < kRlcWindows; w++) d[w] = 0;
+}
+
+__global__ void __launch_bounds__(kPartProofs) k_part_index_digits(PartIdxArgs a) {
+  static_assert(kPartLocJ0 < (1 << 16) - 256 && kPartLocJ0 - 2 * (kPartProofs - 1) > (1 << 15),
+                "index multipliers: digit 8 of j a below 2^15 - 128, and above 2^15 so that it spreads");
+  __shared__ sc red_a[kPartProofs];
+  __shared__ sc red_b[kPartProofs];
+  const int64_t b = blockIdx.x;
+  const int t = threadIdx.x;
+  const int64_t i = (int64_t)a.blocks[b] * kPartProofs + t;  // proof of the prepared batch
+  const int64_t o = b * kPartProofs + t;                      // its compact slot
+  const int64_t j = kPartLocJ0 - 2 * t;
+  sc zero;
+#pragma unroll
+  for (int k = 0; k < 8; k++) zero.w[k] = 0;
+  red_a[t] = zero;
+  red_b[t] = zero;
+  const bool live = i < a.n && a.status[i] == kStOk;
+  uint32_t blk[16];
+  if (live) chacha20_block(blk, a.seed, a.first_index + (uint64_t)i, 0);
+  sc J = zero;
+  J.w[0] = (uint32_t)j;
+#pragma unroll 1
+  for (int q = 0; q < 4; q++) {
+    int16_t d[kRlcWindows];
+#pragma unroll
+    for (int w = 0; w < kRlcWindows; w++) d[w] = 0;
+    if (live) {
+      const uint32_t* u = q < 2 ? blk : blk + 4;
+      if (q & 1) {
+        sc c;
+        rlc_load8(c.w, a.c, i);
+        recode16(d, sc_mul(J, sc_mul(rlc_weight(u), c)).w);
+      } else {
+        index_weight_digits(d, u, j);
+        sc sv;
+        rlc_load8(sv.w, a.s, i);
+        (q == 0 ? red_a : red_b)[t] = sc_mul(J, sc_mul(rlc_weight(u), sv));
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < kRlcWindows; w++) a.digits[(int64_t)w * a.dstride + 4 * o + q] = d[w];
+  }
+  __syncthreads();
+  for (int off = kRlcSumBlock / 2; off > 0; off >>= 1) {
+    if ((t % kRlcSumBlock) < off) {
+      red_a[t] = sc_add(red_a[t], red_a[t + off]);
+      red_b[t] = sc_add(red_b[t], red_b[t + off]);
+    }
+    __syncthreads();
+  }
+  if (t % kRlcSumBlock == 0) {  // kPartProofs / kRlcSumBlock sums per listed block (k_part_sort adds them)
+    const int64_t sb = b * (kPartProofs / kRlcSumBlock) + t / kRlcSumBlock;
+    a.block_sums[2 * sb] = red_a[t];
+    a.block_sums[2 * sb + 1] = red_b[t];
+  }
+}
+
+// [k] P for a small k > 0 (double and add from the top bit).
+__device__ __forceinline__ ge_p3 p3_mul_small(const ge_p3& P, uint32_t k) {
+  ge_p3 R = P;
+#pragma unroll 1
+  for (int bit = 30 - __builtin_clz(k); bit >= 0; bit--) {
+    R = p1p1_to_p3(p3_dbl(R));
+    if ((k >> bit) & 1u) R = ge_add(R, P);
+  }
+  return R;
+}
+
+// k_part_locate: kPartLocLanes lanes per listed block; lane q tests the proofs t = q, q + L, ...
+// (L = kPartLocLanes), i.e. j = J0 - 2 q, J0 - 2 q - 2 L, ..., against P'_b by ristretto
+// equality, stepping by -[2 L] P_b.  The block is located iff exactly one j matches (and
+// neither partial is incomplete nor P_b the identity).
+__global__ void __launch_bounds__(256) k_part_locate(PartLocArgs a) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t b = g / kPartLocLanes;
+  const int q = (int)(g % kPartLocLanes);
+  const bool live = b < a.nblk;
+  const int64_t bb = live ? b : a.nblk - 1;  // dead lanes: any block, dropped (whole groups)
+  const ge_p3 P = load_p3(a.part + a.blocks[bb]);
+  const ge_p3 Pl = load_p3(a.lpart + bb);
+  const bool usable = !(a.lfail[bb] & 2) && !ristretto_is_identity(P);
+  ge_p3 Q = p3_mul_small(P, (uint32_t)(kPartLocJ0 - 2 * q));
+  const ge_p3 step = ge_neg(p3_mul_small(P, 2u * kPartLocLanes));
+  int hits = 0, found = 0;
+#pragma unroll 1
+  for (int t = q; t < kPartProofs; t += kPartLocLanes) {
+    if (ristretto_equal(Q, Pl)) {
+      hits++;
+      found = t;
+    }
+    Q = ge_add(Q, step);
+  }
+  // the block's lanes are consecutive lanes of one wave
+#pragma unroll
+  for (int m = 1; m < kPartLocLanes; m <<= 1) {
+    const int oh = __shfl_xor(hits, m), of = __shfl_xor(found, m);
+    found = of > found ? of : found;
+    hits += oh;
+  }
+  if (live && q == 0) a.loc[b] = (usable && hits == 1) ? (uint16_t)found : kPartNoLoc;
+}
+
+__global__ void __launch_bounds__(256) k_gather_status(const uint8_t* status, const uint32_t* idx, int64_t m,
+                                                       uint8_t* out) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < m) out[k] = status[idx[k]];
+}
+
+hipError_t launch_part_index_digits(const PartIdxArgs& a, hipStream_t st) {
+  if (a.nblk <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_part_index_digits, dim3((unsigned)a.nblk), dim3(kPartProofs), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_part_locate(const PartLocArgs& a, hipStream_t st) {
+  if (a.nblk <= 0) return hipSuccess;
+  static_assert(64 % kPartLocLanes == 0 && kPartProofs % kPartLocLanes == 0, "a block's lanes in one wave");
+  const int64_t threads = a.nblk * kPartLocLanes;
+  hipLaunchKernelGGL(k_part_locate, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_status(const uint8_t* status, const uint32_t* idx, int64_t m, uint8_t* out, hipStream_t st) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_status, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, status, idx, m, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_part_msm(const PartArgs& a, hipStream_t st) {

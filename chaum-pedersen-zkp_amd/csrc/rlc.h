@@ -124,9 +124,57 @@ struct PartArgs {
   ge_p3* wsum;                   // [blocks][kPartWsum] (indexed by the global block)
   uint16_t* assign;              // [nblk][kPartUnits] lane -> (unit of windows 0..15, unit of 16..31)
   ge_p3* part;                   // [blocks] P_b (indexed by the global block)
-  uint8_t* fail;                 // [blocks] 1 iff P_b is not the identity (or a top-window digit
-                                 // exceeded kPartTopBuckets: the block is verified per proof)
+  uint8_t* fail;                 // [blocks] bit 0: P_b is not the identity; bit 1: a top-window
+                                 // digit exceeded kPartTopBuckets (the block is verified per proof)
+  const uint32_t* pmap = nullptr;  // locate pass: listed block b's points are those of prepared
+                                   // block pmap[b] (digits, sums and outputs are compact)
 };
+
+// ---- locating a failing block's forged entry (part.hip) ----------------------------------
+// A failing block's second partial with the weights of its proof t multiplied by
+// j_t = kPartLocJ0 - 2 t:  P'_b = sum_i j_i E_i  where  P_b = sum_i E_i  (E_i proof i's weighted
+// terms; the identity, up to 4-torsion, for a valid proof).  With one forged proof f,
+// P'_b = [j_f] P_b; with more, no j satisfies it except with probability ~2^-121 per block (128
+// candidate j against 128-bit weights).  The r-points' scalars j a_i are kept as integers (signed
+// radix-2^16 digits with a ninth digit), the others reduced mod l, so the pass has the first's
+// window structure.  The j lie just below 2^16 so that the ninth digit spreads over its range:
+// with j = t + 1 or 2 t + 1 the r-points' ninth digits were small and piled into the lowest
+// buckets of 8-bit windows 16 / 17, and the walk waited for the lane holding them (C5's 15,776
+// failing blocks: 18.1 - 20.9 ms, against 13.4 ms for the same walk with j = 1).
+constexpr int64_t kPartLocJ0 = (1 << 16) - 257;
+#ifndef CPZ_PART_LOCATE
+#define CPZ_PART_LOCATE 1
+#endif
+constexpr int kPartLocLanes = 8;     // lanes per block in k_part_locate (t = q, q + 8, ...)
+constexpr uint16_t kPartNoLoc = 0xffff;
+
+struct PartIdxArgs {
+  int64_t nblk;                  // listed blocks
+  int64_t n;                     // proofs of the prepared batch
+  const uint32_t* blocks;        // [nblk] prepared block of each listed block
+  uint64_t first_index;          // the prepare's weight keys
+  uint32_t seed[8];
+  const uint32_t* s;
+  const uint32_t* c;
+  const uint8_t* status;         // decode-level statuses of the prepare (non-zero: zero weight)
+  int16_t* digits;               // [16][dstride] compact: listed block b's proof t at 4 (kPartProofs b + t)
+  int64_t dstride;
+  sc* block_sums;                // [nblk * kPartProofs / kRlcSumBlock][2], compact
+};
+
+struct PartLocArgs {
+  int64_t nblk;
+  const uint32_t* blocks;        // [nblk] prepared block of each listed block
+  const ge_p3* part;             // [prepared blocks] P_b of the first pass
+  const ge_p3* lpart;            // [nblk] P'_b of the index-weighted pass
+  const uint8_t* lfail;          // [nblk] its flags (bit 1: incomplete partial)
+  uint16_t* loc;                 // [nblk] out: the forged proof's index in the block, or kPartNoLoc
+};
+
+hipError_t launch_part_index_digits(const PartIdxArgs& a, hipStream_t st);
+hipError_t launch_part_locate(const PartLocArgs& a, hipStream_t st);
+// out[k] = status[idx[k]] for k < m
+hipError_t launch_gather_status(const uint8_t* status, const uint32_t* idx, int64_t m, uint8_t* out, hipStream_t st);
 
 hipError_t launch_part_msm(const PartArgs& a, hipStream_t st);      // sort + walk of [blk0, blk0 + nblk)
 hipError_t launch_part_combine(const PartArgs& a, hipStream_t st);  // P_b and fail flags of [blk0, blk0 + nblk)

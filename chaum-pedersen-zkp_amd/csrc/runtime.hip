@@ -210,6 +210,7 @@ struct cpz_ctx {
   // partitioned batch check (part.hip): sorted lists / offsets / window sums of one chunk of
   // blocks, every block's partial and fail flag, the sum's scratch, the failing-block list
   DevBuf pt_lists, pt_offs, pt_wsum, pt_part, pt_fail, pt_tmp, pt_blocks, pt_assign;
+  DevBuf pt_ldig, pt_lsum, pt_lpart, pt_lfail, pt_loc;  // the locate pass over failing blocks
   // what the last batch call's fallback did (cpz_ctx_fallback_stats)
   uint64_t fb_stats[CPZ_FALLBACK_STATS] = {};
   // commitment checks (statuses 4 and 5: the Proof::from_bytes rejections); off = equations only.
@@ -891,9 +892,9 @@ int launch_probe(cpz_ctx* ctx, size_t n, const void* const rows[5], const void* 
 // blocks; launches of at most half the occupancy grid, round-robin over the verify streams and
 // their scratch slabs (as launch_verify_chunks).
 int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* status, const uint32_t* d_blocks,
-                           int64_t nb, hipStream_t st) {
-  static_assert(cpz::kVerifyBlock % cpz::kPartProofs == 0, "whole listed blocks per verify workgroup");
-  constexpr int64_t G = cpz::kVerifyBlock / cpz::kPartProofs;
+                           int64_t nb, int block_proofs, hipStream_t st) {
+  if (block_proofs <= 0 || cpz::kVerifyBlock % block_proofs != 0) return CPZ_EINVAL;
+  const int64_t G = cpz::kVerifyBlock / block_proofs;
   if (nb <= 0) return CPZ_OK;
   const int full = (occupancy_grid(ctx) + CPZ_VERIFY_CHUNK_DIV - 1) / CPZ_VERIFY_CHUNK_DIV;
   const size_t slab = (size_t)full * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached);
@@ -918,7 +919,7 @@ int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* stat
   va.comb = static_cast<const cpz::ge_niels*>(ctx->gs->comb.p);
   va.pre = static_cast<const cpz::ge_niels*>(ctx->rl_prep.pts.p);
   va.eq_only = ctx->call_eq ? 1 : 0;
-  va.block_proofs = cpz::kPartProofs;
+  va.block_proofs = block_proofs;
   for (int64_t c = 0; c < chunks; c++) {
     const int64_t g0 = c * full;
     const int g = (int)std::min<int64_t>(full, groups - g0);
@@ -947,10 +948,11 @@ int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* stat
 constexpr int64_t kPartChunkBlocks = (int64_t(1) << 24) / cpz::kPartProofs;
 // Density probe outcomes (invalid entries among the kProbeChunks x 256 sampled) for which the
 // partitioned check pays.  Relative to per-proof verification its prepare costs ~0.19, its
-// block partials ~0.32 (256-proof blocks) or ~0.36 (128), and the per-proof pass over a failing
-// block's proofs ~0.83 (no decodes); a block of B proofs is clean with probability (1 - rho)^B.
-// So it pays while 1 - (1 - rho)^B < ~0.59 (B = 256: rho < ~0.35 %, ~14 sampled) or ~0.54
-// (B = 128: rho < ~0.6 %, ~25 sampled); the limits keep a margin.
+// block partials ~0.32 (256-proof blocks) or ~0.36 (128), the locate pass ~0.5 per failing
+// fraction, and the per-proof pass over a block holding two or more forgeries ~0.83 (no
+// decodes); a block of B proofs is clean with probability (1 - rho)^B.  At B = 128 it pays up
+// to rho ~ 0.65 % (~27 sampled; ~0.6 % without the locate pass), at 256 up to ~0.35 % (~14);
+// the limits keep a margin.
 constexpr int kPartMaxProbeBad = cpz::kPartProofs == 128 ? 20 : 12;
 
 // Every buffer the partitioned check of n proofs uses: the prepared batch, the partial / flag
@@ -970,23 +972,132 @@ int part_reserve(cpz_ctx* ctx, int64_t n) {
   CPZ_HIP(ctx->pt_part.ensure((size_t)nblk * sizeof(cpz::ge_p3)));
   CPZ_HIP(ctx->pt_fail.ensure((size_t)nblk));
   CPZ_HIP(ctx->pt_tmp.ensure((size_t)((nblk + 63) / 64 + 16) * sizeof(cpz::ge_p3)));
-  CPZ_HIP(ctx->pt_blocks.ensure((size_t)nblk * sizeof(uint32_t)));
+  CPZ_HIP(ctx->pt_blocks.ensure((size_t)2 * nblk * sizeof(uint32_t)));  // failing blocks, then the per-proof lists
   return CPZ_OK;
 }
 
 void part_release(cpz_ctx* ctx) {
   for (DevBuf* b : {&ctx->pt_lists, &ctx->pt_offs, &ctx->pt_wsum, &ctx->pt_part, &ctx->pt_fail, &ctx->pt_tmp,
-                    &ctx->pt_blocks, &ctx->pt_assign})
+                    &ctx->pt_blocks, &ctx->pt_assign, &ctx->pt_ldig, &ctx->pt_lsum, &ctx->pt_lpart, &ctx->pt_lfail,
+                    &ctx->pt_loc})
     b->release();
   ctx->rl_prep.release();
   (void)hipGetLastError();
 }
 
+// The locate pass (rlc.h, part.hip) over the failing blocks listed in pt_blocks: their
+// index-weighted partials P'_b, then per block the one j with P'_b = [j] P_b if there is one.
+// Fills `cand` with the located proofs and leaves in `whole` the blocks to verify per proof.
+// Its buffers (16 KB of digits per failing block) are taken on demand; if they do not fit,
+// every failing block is verified per proof, as without the pass.
+int part_locate(cpz_ctx* ctx, int64_t n, const void* s, const uint8_t* d_status, const uint8_t seed[32],
+                uint64_t first_index, const std::vector<uint32_t>& blocks, std::vector<uint32_t>& whole,
+                std::vector<uint32_t>& cand, hipStream_t st) {
+  const int64_t nf = (int64_t)blocks.size();
+  const int64_t dstride = ((4 * cpz::kPartProofs * nf) + 7) & ~(int64_t)7;
+  const int64_t nsum = nf * (cpz::kPartProofs / cpz::kRlcSumBlock);
+  if (ctx->pt_ldig.ensure((size_t)cpz::kRlcWindows * dstride * sizeof(int16_t)) != hipSuccess ||
+      ctx->pt_lsum.ensure((size_t)2 * nsum * sizeof(cpz::sc)) != hipSuccess ||
+      ctx->pt_lpart.ensure((size_t)nf * sizeof(cpz::ge_p3)) != hipSuccess ||
+      ctx->pt_lfail.ensure((size_t)nf) != hipSuccess || ctx->pt_loc.ensure((size_t)nf * sizeof(uint16_t)) != hipSuccess) {
+    for (DevBuf* b : {&ctx->pt_ldig, &ctx->pt_lsum, &ctx->pt_lpart, &ctx->pt_lfail, &ctx->pt_loc}) b->release();
+    (void)hipGetLastError();
+    return CPZ_OK;  // `whole` keeps every failing block
+  }
+  const uint32_t* d_blocks = static_cast<const uint32_t*>(ctx->pt_blocks.p);
+  {
+    StageTimer t(ctx, 3, st);
+    cpz::PartIdxArgs ia;
+    ia.nblk = nf;
+    ia.n = n;
+    ia.blocks = d_blocks;
+    ia.first_index = first_index;
+    std::memcpy(ia.seed, seed, 32);
+    ia.s = static_cast<const uint32_t*>(s);
+    ia.c = static_cast<const uint32_t*>(ctx->c.p);
+    ia.status = d_status;
+    ia.digits = static_cast<int16_t*>(ctx->pt_ldig.p);
+    ia.dstride = dstride;
+    ia.block_sums = static_cast<cpz::sc*>(ctx->pt_lsum.p);
+    CPZ_HIP(cpz::launch_part_index_digits(ia, st));
+    cpz::PartArgs pa;
+    pa.n = nf * cpz::kPartProofs;  // compact; proofs past the batch's end have zero digits
+    pa.pts = static_cast<const cpz::ge_niels*>(ctx->rl_prep.pts.p);
+    pa.pmap = d_blocks;
+    pa.digits = ia.digits;
+    pa.dstride = dstride;
+    pa.block_sums = ia.block_sums;
+    pa.tab = static_cast<const cpz::ge_niels*>(ctx->gs->tab.p);
+    pa.lists = static_cast<uint16_t*>(ctx->pt_lists.p);
+    pa.assign = static_cast<uint16_t*>(ctx->pt_assign.p);
+    pa.offs = static_cast<uint16_t*>(ctx->pt_offs.p);
+    pa.wsum = static_cast<cpz::ge_p3*>(ctx->pt_wsum.p);  // the first pass's window sums are spent
+    pa.part = static_cast<cpz::ge_p3*>(ctx->pt_lpart.p);
+    pa.fail = static_cast<uint8_t*>(ctx->pt_lfail.p);
+    const int64_t chunk = std::min<int64_t>(nf, kPartChunkBlocks);
+    for (int64_t b0 = 0; b0 < nf; b0 += chunk) {
+      pa.blk0 = b0;
+      pa.nblk = std::min<int64_t>(chunk, nf - b0);
+      CPZ_HIP(cpz::launch_part_msm(pa, st));
+    }
+    pa.blk0 = 0;
+    pa.nblk = nf;
+    CPZ_HIP(cpz::launch_part_combine(pa, st));
+    cpz::PartLocArgs la;
+    la.nblk = nf;
+    la.blocks = d_blocks;
+    la.part = static_cast<const cpz::ge_p3*>(ctx->pt_part.p);
+    la.lpart = pa.part;
+    la.lfail = pa.fail;
+    la.loc = static_cast<uint16_t*>(ctx->pt_loc.p);
+    CPZ_HIP(cpz::launch_part_locate(la, st));
+  }
+  std::vector<uint16_t> loc((size_t)nf);
+  CPZ_HIP(hipMemcpyAsync(loc.data(), ctx->pt_loc.p, (size_t)nf * sizeof(uint16_t), hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipStreamSynchronize(st));
+  ctx->fb_stats[6] = (uint64_t)nf;
+  whole.clear();
+  for (int64_t k = 0; k < nf; k++) {
+    if (loc[(size_t)k] == cpz::kPartNoLoc) whole.push_back(blocks[(size_t)k]);
+    else cand.push_back(blocks[(size_t)k] * (uint32_t)cpz::kPartProofs + loc[(size_t)k]);
+  }
+  ctx->fb_stats[7] = (uint64_t)cand.size();
+  return CPZ_OK;
+}
+
+// Per-proof verification (k_verify_prepared) of the located proofs alone and of the `whole`
+// blocks.  A located proof that verifies (a 2^-121 event: the locate pass accepted its block's
+// other proofs on P'_b = [j] P_b) sends its block to per-proof verification as well.
+int part_verify_lists(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, const std::vector<uint32_t>& blocks,
+                      std::vector<uint32_t> whole, const std::vector<uint32_t>& cand, hipStream_t st) {
+  uint32_t* d_list = static_cast<uint32_t*>(ctx->pt_blocks.p) + blocks.size();  // after the failing blocks
+  StageTimer span(ctx, 4, st);  // wall time of the per-proof pass; launches timed as verify_each
+  if (!cand.empty()) {
+    ctx->fb_stats[4] += (uint64_t)cand.size();
+    CPZ_HIP(hipMemcpyAsync(d_list, cand.data(), cand.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    if (int rc = verify_prepared_blocks(ctx, n, s, d_status, d_list, (int64_t)cand.size(), 1, st)) return rc;
+    std::vector<uint8_t> cst(cand.size());
+    uint8_t* d_cst = static_cast<uint8_t*>(ctx->pt_lfail.p);  // |cand| <= failing blocks bytes, spent
+    CPZ_HIP(cpz::launch_gather_status(d_status, d_list, (int64_t)cand.size(), d_cst, st));
+    CPZ_HIP(hipMemcpyAsync(cst.data(), d_cst, cand.size(), hipMemcpyDeviceToHost, st));
+    CPZ_HIP(hipStreamSynchronize(st));
+    for (size_t k = 0; k < cand.size(); k++)
+      if (cst[k] == cpz::kStatusOk) whole.push_back(cand[k] / (uint32_t)cpz::kPartProofs);
+  }
+  if (whole.empty()) return CPZ_OK;
+  for (uint32_t b : whole) ctx->fb_stats[4] += (uint64_t)std::min<int64_t>(cpz::kPartProofs, n - (int64_t)b * cpz::kPartProofs);
+  CPZ_HIP(hipMemcpyAsync(d_list, whole.data(), whole.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  if (int rc = verify_prepared_blocks(ctx, n, s, d_status, d_list, (int64_t)whole.size(), cpz::kPartProofs, st))
+    return rc;
+  CPZ_HIP(hipStreamSynchronize(st));  // the host lists are pageable memory read by the copies above
+  return CPZ_OK;
+}
+
 // The partitioned fallback over the prepared batch (buffers from part_reserve): every block's
 // partial (k_part_*), the batch partial as their sum, and per-proof verification of the
 // failing blocks only.
-int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, uint8_t partial[32], int* identity,
-                  hipStream_t st) {
+int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, const uint8_t seed[32],
+                  uint64_t first_index, uint8_t partial[32], int* identity, hipStream_t st) {
   const int64_t nblk = (n + cpz::kPartProofs - 1) / cpz::kPartProofs;
   const int64_t chunk = std::min<int64_t>(nblk, kPartChunkBlocks);
   {
@@ -1028,15 +1139,15 @@ int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, uin
     if (dirty[(size_t)b]) blocks.push_back((uint32_t)b);
   ctx->fb_stats[2] = (uint64_t)nblk;
   ctx->fb_stats[3] = blocks.size();
-  for (uint32_t b : blocks) ctx->fb_stats[4] += (uint64_t)std::min<int64_t>(cpz::kPartProofs, n - (int64_t)b * cpz::kPartProofs);
   if (blocks.empty()) return CPZ_OK;
   CPZ_HIP(hipMemcpyAsync(ctx->pt_blocks.p, blocks.data(), blocks.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-  StageTimer span(ctx, 4, st);  // wall time of the per-proof pass; launches timed as verify_each
-  int rc = verify_prepared_blocks(ctx, n, s, d_status, static_cast<const uint32_t*>(ctx->pt_blocks.p),
-                                  (int64_t)blocks.size(), st);
-  if (rc) return rc;
-  CPZ_HIP(hipStreamSynchronize(st));  // `blocks` is pageable host memory read by the copy above
-  return CPZ_OK;
+  std::vector<uint32_t> whole = blocks;  // blocks verified per proof
+  std::vector<uint32_t> cand;            // located forged proofs, verified alone
+  if (CPZ_PART_LOCATE) {
+    int rc = part_locate(ctx, n, s, d_status, seed, first_index, blocks, whole, cand, st);
+    if (rc) return rc;
+  }
+  return part_verify_lists(ctx, n, s, d_status, blocks, whole, cand, st);
 }
 
 int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
@@ -1085,7 +1196,7 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
       if ((rc = rlc_prepare_points(ctx, n, y1, y2, r1, r2, s, d_status, seed, first_index, st, false))) return rc;
       uint8_t part[32];
       int ident = 0;
-      if ((rc = part_fallback(ctx, (int64_t)n, s, d_status, part, &ident, st))) return rc;
+      if ((rc = part_fallback(ctx, (int64_t)n, s, d_status, seed, first_index, part, &ident, st))) return rc;
       if (partial_out) std::memcpy(partial_out, part, 32);
       if (batch_ok) *batch_ok = 0;  // the probe saw invalid entries
       if (host_status) {
@@ -1579,7 +1690,8 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->rl_prep.release();
   ctx->rl_msm.release();
   for (DevBuf* b : {&ctx->pt_lists, &ctx->pt_offs, &ctx->pt_wsum, &ctx->pt_part, &ctx->pt_fail, &ctx->pt_tmp,
-                    &ctx->pt_blocks, &ctx->pt_assign})
+                    &ctx->pt_blocks, &ctx->pt_assign, &ctx->pt_ldig, &ctx->pt_lsum, &ctx->pt_lpart, &ctx->pt_lfail,
+                    &ctx->pt_loc})
     b->release();
   ctx->rl_flags.release();
   ctx->rl_parts.release();

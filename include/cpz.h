@@ -55,8 +55,9 @@ extern "C" {
  * an array size it writes changes, so that callers built against another header can refuse
  * to run instead of passing wrongly sized buffers.  3: CPZ_NUM_STAGES = 16,
  * cpz_ctx_stage_times_n, cpz_ctx_set_commitment_checks.  4: per-call flags (the _ex entry
- * points, CPZ_CALL_EQUATIONS_ONLY), stage 7 (generator tables), density probe with contexts. */
-#define CPZ_ABI_VERSION 4
+ * points, CPZ_CALL_EQUATIONS_ONLY), stage 7 (generator tables), density probe with contexts.
+ * 5: CPZ_FALLBACK_STATS = 8 (the partitioned check's locate pass). */
+#define CPZ_ABI_VERSION 5
 
 typedef struct cpz_ctx cpz_ctx;
 
@@ -215,14 +216,18 @@ int cpz_verify_batch_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[3
 /* What the last cpz_verify_batch[_device] call on the context did to locate invalid entries
  * (fallback != 0), for tests and benchmarks:
  *   out[0]  path: CPZ_FALLBACK_NONE (the batch passed, or no fallback), _BISECTION (sub-range
- *           RLC partials, per-proof leaves), _PARTITIONED (every 256-proof block's partial,
- *           per-proof verification of the failing blocks), _PER_PROOF (dense: everything)
+ *           RLC partials, per-proof leaves), _PARTITIONED (every 128-proof block's partial, the
+ *           failing blocks' index-weighted partials, per-proof verification of the located
+ *           entries and of the blocks not located), _PER_PROOF (dense: everything)
  *   out[1]  invalid entries the density probe saw (0 without a probe)
  *   out[2]  blocks whose partial the partitioned check computed
  *   out[3]  blocks whose partial was not the identity
  *   out[4]  entries the fallback verified per proof
- *   out[5]  sub-range MSMs the bisection ran */
-#define CPZ_FALLBACK_STATS 6
+ *   out[5]  sub-range MSMs the bisection ran
+ *   out[6]  failing blocks whose index-weighted partial the locate pass computed
+ *   out[7]  of those, blocks whose one invalid entry it located (verified alone; the rest of
+ *           such a block is accepted on P'_b = [j] P_b, error <= ~2^-121 per block) */
+#define CPZ_FALLBACK_STATS 8
 #define CPZ_FALLBACK_NONE 0
 #define CPZ_FALLBACK_BISECTION 1
 #define CPZ_FALLBACK_PARTITIONED 2

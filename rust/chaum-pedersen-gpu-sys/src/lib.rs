@@ -46,9 +46,9 @@ pub const CPZ_PARSE_IDENTITY: u8 = 19;
 pub const CPZ_PARSE_ZERO_S: u8 = 20;
 
 pub const CPZ_NUM_STAGES: usize = 16;
-pub const CPZ_ABI_VERSION: c_int = 4;
+pub const CPZ_ABI_VERSION: c_int = 5;
 pub const CPZ_CALL_EQUATIONS_ONLY: u32 = 1;
-pub const CPZ_FALLBACK_STATS: usize = 6;
+pub const CPZ_FALLBACK_STATS: usize = 8;
 pub const CPZ_FALLBACK_NONE: u64 = 0;
 pub const CPZ_FALLBACK_BISECTION: u64 = 1;
 pub const CPZ_FALLBACK_PARTITIONED: u64 = 2;

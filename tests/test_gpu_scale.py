@@ -260,6 +260,16 @@ def _blocks_with(idx, b):
     return np.unique(np.asarray(idx) // b)
 
 
+def _locate_expect(idx, b, n):
+    """(failing blocks, blocks the locate pass finds, entries verified per proof): a failing
+    block with exactly one forged entry is located and that entry alone verified per proof;
+    a block with more is verified whole (rlc.h, the index-weighted partial)."""
+    blocks, counts = np.unique(np.asarray(idx) // b, return_counts=True)
+    one = int((counts == 1).sum())
+    whole = sum(min(b, n - b * int(k)) for k, c in zip(blocks, counts) if c > 1)
+    return blocks.size, one, one + whole
+
+
 @pytest.mark.parametrize("n", [1 << 22, (1 << 20) + 77])
 def test_partitioned_fallback_at_c5_density(gpu, n):
     """configs[4]'s density (0.1 % forged, half s + 1, half wrong y1) through the batch check
@@ -268,8 +278,9 @@ def test_partitioned_fallback_at_c5_density(gpu, n):
     the failing blocks ONLY.  Checked: the exact forged set (statuses 1 there, 0 elsewhere);
     the batch partial equals the C oracle's partial of the forged entries alone; the path
     taken; the failing blocks are exactly the blocks holding a forgery; and no entry of a
-    clean block is verified per proof (per_proof == the failing blocks' proofs).  The ragged
-    size puts a forgery in the partial last block."""
+    clean block is verified per proof: a failing block holding one forgery is located by its
+    index-weighted partial and only that entry is verified per proof, a block holding more is
+    verified whole.  The ragged size puts a forgery in the partial last block."""
     torch = pytest.importorskip("torch")
     t = _synthetic_device(gpu, torch, n)
     rng = np.random.default_rng(4242 + n)
@@ -286,8 +297,9 @@ def test_partitioned_fallback_at_c5_density(gpu, n):
     B = _part_block(n, stats)
     dirty = _blocks_with(idx, B)
     assert stats["blocks_failing"] == dirty.size, (stats, dirty.size)
-    want_pp = sum(min(B, n - B * int(b)) for b in dirty)
-    assert stats["per_proof"] == want_pp
+    nfail, one, want_pp = _locate_expect(idx, B, n)
+    assert stats["blocks_indexed"] == nfail and stats["blocks_located"] == one, stats
+    assert stats["per_proof"] == want_pp, stats
     assert p == _oracle_partial(host, idx)
 
 
@@ -373,9 +385,41 @@ def test_partitioned_fallback_with_service_contexts(gpu):
     assert stats["path"] == "partitioned", stats
     B = _part_block(n, stats)
     dirty = _blocks_with(idx, B)
-    assert stats["blocks_failing"] == dirty.size and stats["per_proof"] == B * dirty.size, stats
+    nfail, one, want_pp = _locate_expect(idx, B, n)
+    assert stats["blocks_failing"] == dirty.size == nfail, stats
+    assert stats["blocks_located"] == one and stats["per_proof"] == want_pp, stats
     want, live = C.rlc_partial(host, idx, WSEED, contexts=hctx, threads=_threads())
     assert live == idx.size and p == want
+
+
+def test_partitioned_locate_edges(gpu):
+    """The locate pass at its edges (2^20 + 77 proofs, 0.1 % s + 1 / wrong-y1 forgeries plus
+    placed ones): a block whose one forgery is its first entry (j = 1) and one whose forgery is
+    its last (j = 128 or 256), a block with two and one with three forgeries (no j matches:
+    verified whole), and the batch's last entry, in the partial last block.  Exact set, the
+    oracle's partial, and the stats' located / whole split."""
+    torch = pytest.importorskip("torch")
+    n = (1 << 20) + 77
+    t = _synthetic_device(gpu, torch, n)
+    rng = np.random.default_rng(6060)
+    idx = rng.choice(n, size=n // 1000, replace=False)
+    B = 256   # placed so that they hold for 128- and 256-proof blocks alike
+    free = [b for b in range(64, n // B - 64, 37) if not np.any(idx // B == b)]
+    b1, b2, b3, b4 = free[:4]
+    placed = [B * b1, B * b2 + B - 1, B * b3 + 5, B * b3 + 9, B * b4 + 100, B * b4 + 101, B * b4 + 200, n - 1]
+    idx = np.union1d(idx, placed)
+    host = _forge(t, torch, idx)
+    st = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    p, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED, fallback=True)
+    stats = gpu.fallback_stats()
+    got = st.cpu().numpy()
+    assert not ok and stats["path"] == "partitioned", stats
+    assert np.array_equal(np.nonzero(got)[0], idx) and set(got[idx].tolist()) == {1}
+    blk = _part_block(n, stats)
+    nfail, one, want_pp = _locate_expect(idx, blk, n)
+    assert stats["blocks_failing"] == stats["blocks_indexed"] == nfail, stats
+    assert stats["blocks_located"] == one and stats["per_proof"] == want_pp, stats
+    assert p == _oracle_partial(host, idx)
 
 
 def test_partitioned_fallback_decode_failures_and_equations_only(gpu, golden):
