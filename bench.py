@@ -345,8 +345,9 @@ def c5_extra(gpu, torch, dev, stream, n5, ctx_len):
     ms = {k: v[0] for k, v in c_st.items()}
     out = {"workload": "configs[4]: %d proofs%s, %d forged (half s+1, half %s), RLC batch check + fallback "
                        "(density probe beside the challenges; at this density the partitioned check: every "
-                       "256-proof block's RLC partial, per-proof verification of the failing blocks only) -> "
-                       "exact invalid set" % (n5, (" with %d-byte contexts" % ctx_len) if ctx_len else "", nf,
+                       "128-proof block's RLC partial, the failing blocks' index-weighted partials locating a "
+                       "single forgery, per-proof verification of the located entries and of the blocks holding "
+                       "more) -> exact invalid set" % (n5, (" with %d-byte contexts" % ctx_len) if ctx_len else "", nf,
                                               "a replayed context" if ctx_len else "wrong y1"),
            "proofs": n5, "forged": nf, "ms": c_el * 1e3, "proofs_per_s": n5 / c_el, "exact_set": True,
            "phase_ms": {"challenge": ms.get("challenge", 0.0), "rlc_prepare": ms.get("rlc_prepare", 0.0),
@@ -356,7 +357,8 @@ def c5_extra(gpu, torch, dev, stream, n5, ctx_len):
            "ratio_to_per_proof": c_el / p_el,
            "partial": partial.hex(),
            "note": "per_proof_only_ms: cpz_verify_each of the same batch (same statuses); rlc_msm is the "
-                   "partitioned MSM (k_part_*), fallback_per_proof the per-proof pass over the failing blocks"}
+                   "partitioned MSMs (k_part_*: every block's partial, then the failing blocks' index-weighted "
+                   "partials and the locate step), fallback_per_proof the per-proof pass"}
     del t5, st5, cx
     torch.cuda.empty_cache()
     return out
