@@ -954,6 +954,12 @@ constexpr int64_t kPartChunkBlocks = (int64_t(1) << 24) / cpz::kPartProofs;
 // to rho ~ 0.65 % (~27 sampled; ~0.6 % without the locate pass), at 256 up to ~0.35 % (~14);
 // the limits keep a margin.
 constexpr int kPartMaxProbeBad = cpz::kPartProofs == 128 ? 20 : 12;
+// A batch of at least this many proofs whose RLC check failed with the density probe seeing at
+// most one invalid sample (or without a probe) takes the partitioned check instead of bisection.
+#ifndef CPZ_SPARSE_PARTITIONED
+#define CPZ_SPARSE_PARTITIONED 1
+#endif
+constexpr int64_t kPartSparseMin = 1 << 19;
 
 // Every buffer the partitioned check of n proofs uses: the prepared batch, the partial / flag
 // words of an MSM set, one chunk's sorted lists / assignment / offsets, and the whole batch's
@@ -976,11 +982,17 @@ int part_reserve(cpz_ctx* ctx, int64_t n) {
   return CPZ_OK;
 }
 
-void part_release(cpz_ctx* ctx) {
+// The partitioned check's own buffers (not the prepared batch).
+void part_release_blocks(cpz_ctx* ctx) {
   for (DevBuf* b : {&ctx->pt_lists, &ctx->pt_offs, &ctx->pt_wsum, &ctx->pt_part, &ctx->pt_fail, &ctx->pt_tmp,
                     &ctx->pt_blocks, &ctx->pt_assign, &ctx->pt_ldig, &ctx->pt_lsum, &ctx->pt_lpart, &ctx->pt_lfail,
                     &ctx->pt_loc})
     b->release();
+  (void)hipGetLastError();
+}
+
+void part_release(cpz_ctx* ctx) {
+  part_release_blocks(ctx);
   ctx->rl_prep.release();
   (void)hipGetLastError();
 }
@@ -1143,7 +1155,9 @@ int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, con
   CPZ_HIP(hipMemcpyAsync(ctx->pt_blocks.p, blocks.data(), blocks.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   std::vector<uint32_t> whole = blocks;  // blocks verified per proof
   std::vector<uint32_t> cand;            // located forged proofs, verified alone
-  if (CPZ_PART_LOCATE) {
+  // The locate pass pays while most failing blocks hold one forgery; with more than half of the
+  // blocks failing (density above ~0.5 %) the failing blocks are verified whole.
+  if (CPZ_PART_LOCATE && 2 * (int64_t)blocks.size() <= nblk) {
     int rc = part_locate(ctx, n, s, d_status, seed, first_index, blocks, whole, cand, st);
     if (rc) return rc;
   }
@@ -1247,9 +1261,22 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
   const bool all_live = any_bad == 0;
   if (batch_ok) *batch_ok = (ident && all_live) ? 1 : 0;
   if (!ident && fallback) {
-    ctx->fb_stats[0] = CPZ_FALLBACK_BISECTION;
-    rc = rlc_fallback(ctx, 0, (int64_t)n, y1, y2, r1, r2, s, d_status, st, 0);
-    if (rc) return rc;
+    // A large batch that failed: every block's partial over the points just prepared, then
+    // the locate pass and per-proof verification of what it leaves (part_fallback) -- at 2^20
+    // cheaper than bisection from one forged entry up (sub-range MSMs of 1/8 of the range, each
+    // with the whole MSM's sort and tails).  Smaller batches, or no room for the block buffers:
+    // bisection.
+    if (CPZ_SPARSE_PARTITIONED && (int64_t)n >= kPartSparseMin && part_reserve(ctx, (int64_t)n) == CPZ_OK) {
+      ctx->fb_stats[0] = CPZ_FALLBACK_PARTITIONED;
+      uint8_t part2[32];
+      int ident2 = 0;
+      if ((rc = part_fallback(ctx, (int64_t)n, s, d_status, seed, first_index, part2, &ident2, st))) return rc;
+    } else {
+      part_release_blocks(ctx);
+      ctx->fb_stats[0] = CPZ_FALLBACK_BISECTION;
+      rc = rlc_fallback(ctx, 0, (int64_t)n, y1, y2, r1, r2, s, d_status, st, 0);
+      if (rc) return rc;
+    }
     CPZ_HIP(hipStreamSynchronize(st));  // statuses complete on return (documented)
   }
   if (host_status) {

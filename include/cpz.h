@@ -216,9 +216,11 @@ int cpz_verify_batch_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[3
 /* What the last cpz_verify_batch[_device] call on the context did to locate invalid entries
  * (fallback != 0), for tests and benchmarks:
  *   out[0]  path: CPZ_FALLBACK_NONE (the batch passed, or no fallback), _BISECTION (sub-range
- *           RLC partials, per-proof leaves), _PARTITIONED (every 128-proof block's partial, the
- *           failing blocks' index-weighted partials, per-proof verification of the located
- *           entries and of the blocks not located), _PER_PROOF (dense: everything)
+ *           RLC partials, per-proof leaves: a failed batch below 2^19 proofs), _PARTITIONED
+ *           (every 128-proof block's partial, the failing blocks' index-weighted partials,
+ *           per-proof verification of the located entries and of the blocks not located: the
+ *           density probe's moderate densities, and a failed batch of 2^19 proofs or more),
+ *           _PER_PROOF (dense: everything)
  *   out[1]  invalid entries the density probe saw (0 without a probe)
  *   out[2]  blocks whose partial the partitioned check computed
  *   out[3]  blocks whose partial was not the identity

@@ -9,7 +9,8 @@ checker; test infrastructure only):
 * C3 (configs[2]) shaped like the reference service's batches (service.rs:512-517: every entry
   carries its 32-byte challenge id as transcript context): 2^20 proofs, s + 1 and wrong-context
   forgeries; the batch partial equals the oracle's partial of the forged entries alone and the
-  fallback's bisection returns exactly the forged set.
+  fallback (the failed MSM, then the partitioned check with its locate pass) returns exactly the
+  forged set.
 * C5 (configs[4]) and C4 (configs[3]): the RLC partial of a forged batch -- whole batch and
   every shard, weights keyed by the global index -- equals, byte for byte, the oracle's
   partial computed from the forged entries ALONE (valid entries contribute the identity, so
@@ -128,14 +129,15 @@ def _oracle_partial(host, gidx, lo=None, hi=None):
     return enc
 
 
-def test_c3_service_contexts_partial_and_bisection(gpu):
+def test_c3_service_contexts_partial_and_located_set(gpu):
     n = 1 << 20
     rng = np.random.default_rng(33)
     ctxs = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(n)]
     rows = gpu.prove_synthetic(n, SX, SK, contexts=ctxs)
     rows = {k: np.ascontiguousarray(rows[k]) for k in KEYS}
     # few forgeries, spread out: the density probe (with contexts) sees at most one, so the
-    # fallback is the bisection, which prunes the clean parts
+    # batch MSM runs first; it fails, and the fallback is the partitioned check (every block's
+    # partial over the points just prepared, each failing block's one forgery located)
     forged = np.sort(rng.choice(n, size=24, replace=False))
     for j, i in enumerate(forged):
         if j % 2:
@@ -143,8 +145,13 @@ def test_c3_service_contexts_partial_and_bisection(gpu):
         else:
             rows["s"][i] = np.frombuffer(((_le(rows["s"][i]) + 1) % O.L).to_bytes(32, "little"), np.uint8)
     partial, ok, st = gpu.verify_batch(*(rows[k] for k in KEYS), seed=WSEED, contexts=ctxs)
+    stats = gpu.fallback_stats()
     assert not ok
     assert np.array_equal(np.nonzero(st)[0], forged) and set(st[forged].tolist()) == {1}
+    assert stats["path"] == "partitioned" and stats["probe_invalid"] <= 1, stats
+    blk = _part_block(n, stats)
+    nfail, one, want_pp = _locate_expect(forged, blk, n)
+    assert stats["blocks_failing"] == nfail and stats["blocks_located"] == one and stats["per_proof"] == want_pp
     sub = {k: rows[k][forged] for k in KEYS}
     want, live = C.rlc_partial(sub, forged, WSEED, contexts=[ctxs[i] for i in forged], threads=_threads())
     assert live == forged.size
@@ -193,9 +200,9 @@ def test_c4_shard_partials_from_forged_entries_alone(gpu):
 
 def test_fallback_probe_sparse_and_dense(gpu):
     """Fallback-enabled batch checks of 2^21 proofs: three forgeries (the density probe sees
-    none -> MSM + bisection: exact set, and the partial equals the oracle's partial of the
-    three), then 1 % forged (the probe sees several -> MSM skipped: exact set, partial_out
-    0xff...ff, batch not ok)."""
+    none -> MSM, which fails, then the partitioned check with the locate pass: exact set, and
+    the partial equals the oracle's partial of the three), then 1 % forged (the probe sees
+    several -> MSM skipped: exact set, partial_out 0xff...ff, batch not ok)."""
     torch = pytest.importorskip("torch")
     n = 1 << 21
     t = _synthetic_device(gpu, torch, n)
@@ -203,9 +210,11 @@ def test_fallback_probe_sparse_and_dense(gpu):
     sparse = np.array([12345, 1_000_001, n - 2])
     host = _forge(t, torch, sparse)
     p, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED, fallback=True)
+    stats = gpu.fallback_stats()
     assert not ok and p == _oracle_partial(host, sparse)
     got = st.cpu().numpy()
     assert np.array_equal(np.nonzero(got)[0], sparse) and set(got[sparse].tolist()) == {1}
+    assert stats["path"] == "partitioned" and stats["blocks_located"] == 3 and stats["per_proof"] == 3, stats
     dense = np.sort(np.random.default_rng(7).choice(np.setdiff1d(np.arange(n), sparse), n // 100, replace=False))
     _forge(t, torch, dense)
     p, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED, fallback=True)
