@@ -30,6 +30,10 @@ constexpr int kNielsEntriesRlc = kTableB;
 constexpr int kRlcChunk = 64;            // sorted entries per bucket-accumulation thread (at most)
 constexpr int kRlcMinChunk = 4;          // ... and at least (small MSMs, rlc_sort_geometry)
 constexpr int64_t kRlcMinHeads = 2048;   // head slots per window whatever the MSM's size
+#ifndef CPZ_RLC_SPARSE
+#define CPZ_RLC_SPARSE 1
+#endif
+constexpr int kRlcSparsePts = 2048;      // MSMs of at most this many points reduce their non-empty buckets only
 // Points of one MSM (its flat positions t, incl. the two extras): the 32-bit entries hold t
 // in 24 bits and all-ones is their empty marker.
 constexpr int64_t kRlcMaxMsmPoints = (1ll << 24) - 1;
@@ -67,6 +71,8 @@ struct RlcMsmArgs {
   int groups;                    // sort blocks per window
   int64_t chunk;                 // points per sort block
   int echunk = kRlcChunk;        // sorted entries per k_rlc_bucket thread (rlc_sort_geometry)
+  int sparse = 0;                // set by launch_rlc_msm: small MSM, non-empty buckets reduced alone ...
+  int sgroups = 4;               // ... by this many workgroups per window
   uint32_t* idx;                 // [16][istride]
   uint32_t* inter;               // [16][istride] coarse-sorted entries (32-bit)
   int64_t istride;

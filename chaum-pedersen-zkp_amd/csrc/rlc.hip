@@ -31,6 +31,7 @@
 //   k_rlc_final     2^(16w) combine, encode -> 32-byte partial + identity flag.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 
 #include "rlc.h"
@@ -659,7 +660,7 @@ __global__ void __launch_bounds__(256, CPZ_RLC_FIX_WAVES) k_rlc_bucket_fix(RlcMs
   const uint32_t s = off[b], e = off[b + 1];
   ge_cached* dst = reinterpret_cast<ge_cached*>(a.buckets + t);
   if (s == e) {
-    store_cached(dst, ge_cached_identity());
+    if (!a.sparse) store_cached(dst, ge_cached_identity());  // the sparse reduction reads non-empty buckets only
     return;
   }
   const uint32_t c0 = s / (uint32_t)a.echunk, c1 = (e - 1) / (uint32_t)a.echunk;
@@ -769,6 +770,99 @@ __global__ void __launch_bounds__(4 * kRlcWinQuads) k_rlc_window(RlcMsmArgs a) {
     r = ge_add_quad(r, lds_w[0], q);
     if (q == 0) store_p3(a.win + w, r);
   }
+}
+
+// Small MSMs (at most kRlcSparsePts points, BatchVerifier-sized batches): a window holds at
+// most that many non-empty buckets, so T_w = sum_b b B_b is formed from them alone -- one
+// double-and-add [b] B_b per non-empty bucket on a quad -- instead of the running sums over
+// all 2^15 buckets (k_rlc_segment + k_rlc_window: 0.095 + 0.130 ms at n = 10, whatever the
+// size).  A synchronous batch check of n = 1 .. 100 proofs: 0.63-0.68 ms against 0.77-0.81 ms;
+// at n = 1000 (4002 points) it measured 0.84 against 0.82-0.83 ms, hence the 2048-point limit
+// (profiles/r04_small_batch_sparse_ab.json).  G = RlcMsmArgs::sgroups workgroups per window (4 .. 32, ~2 buckets per quad) each
+// take every G-th non-empty bucket (each workgroup lists the window's non-empty buckets itself
+// from the offsets), reduce their quads' sums in LDS and write a partial; k_rlc_window_sum adds
+// a window's partials.
+constexpr int kRlcSparseMaxGroups = 32;
+__global__ void __launch_bounds__(256) k_rlc_window_sparse(RlcMsmArgs a) {
+  __shared__ uint32_t cnt[256];
+  __shared__ uint16_t list[kRlcSparsePts + 2];
+  __shared__ ge_p3 red[64];
+  __builtin_amdgcn_s_setprio(3);
+  const int w = blockIdx.y, g = blockIdx.x, t = threadIdx.x;
+  const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
+  constexpr int per = kRlcBuckets / 256;
+  uint32_t mine = 0;
+  for (int k = 0; k < per; k++) mine += off[t * per + k + 1] > off[t * per + k] ? 1u : 0u;
+  cnt[t] = mine;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {  // inclusive scan of the per-thread counts
+    const uint32_t v = t >= d ? cnt[t - d] : 0u;
+    __syncthreads();
+    cnt[t] += v;
+    __syncthreads();
+  }
+  const uint32_t K = cnt[255];  // non-empty buckets of the window (<= its entries <= the MSM's points)
+  uint32_t pos = cnt[t] - mine;
+  for (int k = 0; k < per && pos < (uint32_t)(kRlcSparsePts + 2); k++) {
+    const int b = t * per + k;
+    if (off[b + 1] > off[b]) list[pos++] = (uint16_t)b;
+  }
+  __syncthreads();
+  const int u = t >> 2, q = t & 3;
+  const ge_cached* B = reinterpret_cast<const ge_cached*>(a.buckets + (int64_t)w * kRlcBuckets);
+  ge_p3 acc = ge_identity();
+#pragma unroll 1
+  for (uint32_t i = (uint32_t)(g * 64 + u); i < K; i += 64 * (uint32_t)a.sgroups) {  // uniform per quad
+    const int b = list[i];
+    const uint32_t v = (uint32_t)b + 1;  // bucket index b holds the digit magnitude b + 1
+    const ge_cached Bc = load_cached(B + b);
+    const ge_cached Z = ge_cached_identity();
+    ge_p3 R = ge_identity();
+#pragma unroll 1
+    for (int bit = 15; bit >= 0; bit--) {  // branch-free: every quad of the wave adds
+      R = p3_dbl_n_quad(R, 1, q);
+      const bool on = (v >> bit) & 1u;
+      ge_cached c;
+      c.YpX = fe_select(Z.YpX, Bc.YpX, on);
+      c.YmX = fe_select(Z.YmX, Bc.YmX, on);
+      c.Z = fe_select(Z.Z, Bc.Z, on);
+      c.T2d = fe_select(Z.T2d, Bc.T2d, on);
+      R = ge_add_quad(R, c, q);
+    }
+    acc = ge_add_quad(acc, R, q);
+  }
+  if (q == 0) red[u] = acc;
+  __syncthreads();
+#pragma unroll 1
+  for (int o = 32; o > 0; o >>= 1) {
+    ge_p3 x;
+    if (u < o) x = ge_add_quad(red[u], red[u + o], q);
+    __syncthreads();
+    if (u < o && q == 0) red[u] = x;
+    __syncthreads();
+  }
+  if (t == 0) store_p3(a.seg_s + (int64_t)w * kRlcSparseMaxGroups + g, red[0]);
+}
+
+// 8 quads per window: quad k adds partials k, k + 8, ..., then a 3-level LDS tree.
+__global__ void __launch_bounds__(512) k_rlc_window_sum(RlcMsmArgs a) {
+  __shared__ ge_p3 red[kRlcWindows][8];
+  const int w = threadIdx.x >> 5, k = (threadIdx.x >> 2) & 7, q = threadIdx.x & 3;
+  const ge_p3* part = a.seg_s + (int64_t)w * kRlcSparseMaxGroups;
+  ge_p3 r = ge_identity();
+#pragma unroll 1
+  for (int g = k; g < a.sgroups; g += 8) r = ge_add_quad(r, load_p3(part + g), q);
+  if (q == 0) red[w][k] = r;
+  __syncthreads();
+#pragma unroll 1
+  for (int o = 4; o > 0; o >>= 1) {
+    ge_p3 x;
+    if (k < o) x = ge_add_quad(red[w][k], red[w][k + o], q);
+    __syncthreads();
+    if (k < o && q == 0) red[w][k] = x;
+    __syncthreads();
+  }
+  if (k == 0 && q == 0) store_p3(a.win + w, red[w][0]);
 }
 
 // P = sum_w 2^(16 w) T_w by a tree on one wave: quad j owns window j; at level `span` the
@@ -917,16 +1011,26 @@ hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0,
   hipLaunchKernelGGL(k_rlc_bucket, dim3((unsigned)((chunks + 255) / 256), kRlcWindows), dim3(256), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = mark(2)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rlc_bucket_fix, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, a);
+  RlcMsmArgs a2 = a;
+  a2.sparse = CPZ_RLC_SPARSE && (a.p1 - a.p0) + 2 <= kRlcSparsePts ? 1 : 0;
+  a2.sgroups = (int)std::min<int64_t>(kRlcSparseMaxGroups, std::max<int64_t>(4, ((a.p1 - a.p0) + 2 + 127) / 128));
+  hipLaunchKernelGGL(k_rlc_bucket_fix, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, a2);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = mark(3)) != hipSuccess) return e;
-  const int64_t ns = (int64_t)kRlcWindows * (kRlcBuckets / kRlcSegLen);
-  hipLaunchKernelGGL(k_rlc_segment, dim3((unsigned)((4 * ns + 255) / 256)), dim3(256), 0, st, a);  // a quad each
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rlc_window, dim3(kRlcWindows), dim3(4 * kRlcWinQuads), 0, st, a);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (a2.sparse) {
+    hipLaunchKernelGGL(k_rlc_window_sparse, dim3((unsigned)a2.sgroups, kRlcWindows), dim3(256), 0, st, a2);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_rlc_window_sum, dim3(1), dim3(32 * kRlcWindows), 0, st, a2);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  } else {
+    const int64_t ns = (int64_t)kRlcWindows * (kRlcBuckets / kRlcSegLen);
+    hipLaunchKernelGGL(k_rlc_segment, dim3((unsigned)((4 * ns + 255) / 256)), dim3(256), 0, st, a2);  // a quad each
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_rlc_window, dim3(kRlcWindows), dim3(4 * kRlcWinQuads), 0, st, a2);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   if ((e = mark(4)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rlc_final, dim3(1), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(k_rlc_final, dim3(1), dim3(64), 0, st, a2);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   return mark(5);
 }

@@ -8,6 +8,7 @@ import hashlib
 import numpy as np
 import pytest
 
+import coracle as C
 import pyoracle as O
 
 pytestmark = pytest.mark.gpu
@@ -55,6 +56,29 @@ def _bump_s(t, torch, idx):
         v = (int.from_bytes(s_host[i].tobytes(), "little") + 1) % O.L
         s_host[i] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)
     t["s"].copy_(torch.from_numpy(s_host))
+
+
+@pytest.mark.parametrize("n", [3, 100, 511, 512])
+def test_small_msm_sparse_reduction_partials(gpu, n):
+    """MSMs of at most 2048 points (n <= 511 proofs) form each window's sum from its non-empty
+    buckets alone (k_rlc_window_sparse + k_rlc_window_sum); larger ones run the running sums over
+    all 2^15 buckets (k_rlc_segment + k_rlc_window).  On both sides of the threshold: a valid
+    batch gives the identity; with s + 1 forgeries (first, middle, last entry) the partial equals
+    the C oracle's partial of the forged entries alone, at a non-zero first index."""
+    torch = pytest.importorskip("torch")
+    first = 12_345
+    seed = hashlib.sha256(b"cpz-sparse-msm").digest()
+    t = _synthetic(gpu, torch, n, first=first)
+    st = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    p, ok = gpu.verify_batch_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], st, seed, first_index=first)
+    assert ok and p == bytes(32)
+    idx = np.unique(np.array([0, n // 2, n - 1]))
+    _bump_s(t, torch, idx.tolist())
+    p, ok = gpu.verify_batch_device(t["y1"], t["y2"], t["r1"], t["r2"], t["s"], st, seed, first_index=first)
+    sel = torch.from_numpy(idx.astype(np.int64)).to("cuda:0")
+    host = {k: t[k].index_select(0, sel).cpu().numpy() for k in ("y1", "y2", "r1", "r2", "s")}
+    want, live = C.rlc_partial(host, idx + first, seed)
+    assert live == idx.size and not ok and p == want
 
 
 def test_rlc_scale_valid_forged_fallback_and_shards(gpu):
