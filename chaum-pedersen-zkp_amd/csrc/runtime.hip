@@ -1070,8 +1070,9 @@ int part_locate(cpz_ctx* ctx, int64_t n, const void* s, const uint8_t* d_status,
   ctx->fb_stats[6] = (uint64_t)nf;
   whole.clear();
   for (int64_t k = 0; k < nf; k++) {
-    if (loc[(size_t)k] == cpz::kPartNoLoc) whole.push_back(blocks[(size_t)k]);
-    else cand.push_back(blocks[(size_t)k] * (uint32_t)cpz::kPartProofs + loc[(size_t)k]);
+    const int64_t e = (int64_t)blocks[(size_t)k] * cpz::kPartProofs + loc[(size_t)k];
+    if (loc[(size_t)k] == cpz::kPartNoLoc || e >= n) whole.push_back(blocks[(size_t)k]);  // (past the end: w.o.p. never)
+    else cand.push_back((uint32_t)e);
   }
   ctx->fb_stats[7] = (uint64_t)cand.size();
   return CPZ_OK;
