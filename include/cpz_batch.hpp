@@ -49,9 +49,9 @@ constexpr std::size_t MAX_BATCH_SIZE = 1000;  // batch.rs:48
 // Smallest Parameters group that takes the RLC batch check rather than per-proof
 // verification (both return verify_one's outcome per entry).  The same threshold as
 // rust/reference-patch/gpu.rs (RLC_MIN_GROUP), from the per-call latency table
-// profiles/r04_small_batch.json: one synchronous host-buffer call takes 0.78-0.83 ms through
-// the RLC check and 1.26-1.68 ms per proof at every n from 1 to 1000, so every group of a
-// multi-entry batch takes the RLC check (a one-entry batch is verify_one, batch.rs:178-180).
+// profiles/r04_small_batch.json: one synchronous host-buffer call takes 0.62-0.68 ms through
+// the RLC check at n = 1 .. 100 and 0.83 ms at 1000, against 1.26-1.68 ms per proof, so every
+// group takes the RLC check (a one-entry batch keyed by the OS's randomness, not the caller's).
 constexpr std::size_t RLC_MIN_GROUP = 1;
 
 using Bytes32 = std::array<uint8_t, 32>;
@@ -313,7 +313,10 @@ class BatchVerifier {
       if (k == groups.size()) groups.push_back({entries_[i].params, {}});
       groups[k].second.push_back(i);
     }
-    const bool single = entries_.size() == 1;  // batch.rs:178-180: verify_one, no randomness
+    // batch.rs:178-180: a one-entry batch is verify_one and draws nothing from the caller's rng;
+    // its RLC check (0.65 against 1.46 ms per proof, profiles/r04_small_batch.json) is keyed by
+    // a seed from the OS entropy source.
+    const bool single = entries_.size() == 1;
     Bytes32 seed{};
     bool have_seed = false;
     uint64_t first_index = 0;
@@ -346,9 +349,10 @@ class BatchVerifier {
       d.entries = n;
       d.first_index = first_index;
       int rc;
-      if (!single && n >= rlc_min_group_) {
+      if (n >= rlc_min_group_) {
         if (!have_seed) {  // drawn once per verify, as the reference draws its weights (batch.rs:240)
-          rng(seed.data(), seed.size());
+          if (single) os_rng(seed.data(), seed.size());
+          else rng(seed.data(), seed.size());
           have_seed = true;
         }
         d.rlc = true;

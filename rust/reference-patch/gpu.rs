@@ -8,8 +8,9 @@
 //!
 //! What the GPU computes, per `Parameters` group of entries (groups in order of first
 //! appearance):
-//!   * n == 1 (batch.rs:178-180): `verify_one` -- cpz_verify_each; `rng` is not touched,
-//!     as in the reference.
+//!   * n == 1 (batch.rs:178-180): `verify_one`; `rng` is not touched, as in the reference.
+//!     The entry's RLC check (0.65 against 1.46 ms per proof, profiles/r04_small_batch.json)
+//!     is keyed by a seed from the OS (`OsRng`), and a failing check verifies it per proof.
 //!   * n >= 2 (batch.rs:233-269): a 32-byte seed drawn once from `rng` (the reference draws
 //!     its weights from it, batch.rs:240) keys the random-linear-combination check of every
 //!     group of at least RLC_MIN_GROUP entries (cpz_verify_batch: the batch equation with the
@@ -42,7 +43,7 @@ use std::sync::atomic::{AtomicUsize, Ordering};
 use std::sync::{Mutex, MutexGuard, OnceLock, TryLockError};
 
 use chaum_pedersen_gpu::{device_count, Entry, EntryError, Gpu, EQUATIONS_ONLY};
-use rand_core::CryptoRngCore;
+use rand_core::{CryptoRngCore, OsRng, RngCore};
 
 use super::{BatchEntry, BatchVerifier};
 use crate::{Element, Error, Parameters, Ristretto255, Result};
@@ -55,9 +56,9 @@ const CONTEXTS_PER_DEVICE: usize = 2;
 /// Smallest `Parameters` group sent to the RLC batch check; smaller groups are verified per
 /// proof (cpz_verify_each).  Both return `verify_one`'s outcome; the threshold only picks the
 /// faster entry point at the batch sizes this API carries (n <= 1000, batch.rs:48), from the
-/// per-call latency table profiles/r04_small_batch.json (bench.py small_batch): 0.78-0.83 ms
-/// per RLC call against 1.26-1.68 ms per-proof at every n from 1 to 1000, so every group of a
-/// multi-entry batch takes the RLC check.
+/// per-call latency table profiles/r04_small_batch.json (bench.py small_batch): 0.62-0.68 ms
+/// per RLC call at n = 1 .. 100 and 0.83 ms at 1000, against 1.26-1.68 ms per proof, so every
+/// group takes the RLC check.
 const RLC_MIN_GROUP: usize = 1;
 
 /// The process's verifier contexts (see above).
@@ -185,12 +186,16 @@ pub(super) fn verify<R: CryptoRngCore + ?Sized>(batch: &BatchVerifier, rng: &mut
     for grp in &groups {
         let rows = group_rows(entries, &grp.idx);
         let (g, h) = &grp.enc;
-        let status = if entries.len() == 1 || rows.len() < RLC_MIN_GROUP {
+        let status = if rows.len() < RLC_MIN_GROUP {
             gpu.verify_each_with(EQUATIONS_ONLY, g, h, &rows).map_err(|e| Error::InvalidParams(e.to_string()))?
         } else {
             let seed = seed.get_or_insert_with(|| {
                 let mut s = [0u8; 32];
-                rng.fill_bytes(&mut s);
+                if entries.len() == 1 {
+                    OsRng.fill_bytes(&mut s); // verify_one draws nothing from the caller's rng
+                } else {
+                    rng.fill_bytes(&mut s);
+                }
                 s
             });
             let (_partial, _ok, st) = gpu

@@ -4,7 +4,8 @@ the call sequence rust/reference-patch/gpu.rs issues, exercised through its C++ 
 
   * entries grouped by Parameters in order of first appearance (two interleaved groups here:
     the default generators and the golden custom pair);
-  * a one-entry batch -> cpz_verify_each_ex (batch.rs:178-180), the rng untouched;
+  * a one-entry batch (verify_one, batch.rs:178-180) leaves the rng untouched: its RLC check
+    is keyed by a seed from the OS entropy source;
   * otherwise one 32-byte seed drawn from the caller's rng keys every group's RLC check,
     groups take consecutive weight indices (first_index = entries of the earlier groups),
     groups of >= rlc_min_group entries run cpz_verify_batch_ex, smaller ones
@@ -140,15 +141,18 @@ def test_dropin_call_sequence_matches_verify_one(gpu, golden, tmp_path, n, rlc_m
     for g, d in zip(order, disp):
         assert d["first_index"] == fi
         idx = np.nonzero(groups == g)[0]
-        want_rlc = n > 1 and len(idx) >= rlc_min
+        want_rlc = len(idx) >= rlc_min
         assert d["rlc"] == want_rlc
         if want_rlc:
-            assert d["seed"] == SEED
+            if n > 1:
+                assert d["seed"] == SEED
+            else:   # the OS's seed, not the caller's rng
+                assert d["seed"] != SEED
             p = params[g]
             sub = {q: rows[q][idx] for q in rows}
-            part, _ = coracle.rlc_partial(sub, np.arange(fi, fi + len(idx)), SEED,
+            part, _ = coracle.rlc_partial(sub, np.arange(fi, fi + len(idx)), d["seed"],
                                           contexts=[ctxs[i] for i in idx], g=p.g, h=p.h)
             assert d["partial"] == part, (g, len(idx))
             assert d["batch_ok"] == all(exp[i] == 0 for i in idx)
         fi += len(idx)
-    assert draws == (1 if any(d["rlc"] for d in disp) else 0)
+    assert draws == (1 if n > 1 and any(d["rlc"] for d in disp) else 0)

@@ -136,7 +136,8 @@ def test_patch_draws_the_seed_from_rng_and_uses_the_batch_check():
     assert "gpu.verify_each_with(EQUATIONS_ONLY," in g   # Proof::new entries: equations only, per call
     assert ".verify_batch_with(EQUATIONS_ONLY," in g
     assert "set_commitment_checks" not in g              # never the shared context mode
-    assert "entries.len() == 1 || rows.len() < RLC_MIN_GROUP" in g   # n == 1 -> verify_one, rng untouched
+    assert "if rows.len() < RLC_MIN_GROUP {" in g
+    assert "if entries.len() == 1 {" in g and "OsRng.fill_bytes(&mut s)" in g   # n == 1: rng untouched
     assert "first_index += rows.len() as u64;" in g      # consecutive weight indices, every group
 
 
