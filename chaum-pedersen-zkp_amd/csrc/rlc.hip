@@ -780,8 +780,8 @@ __global__ void __launch_bounds__(4 * kRlcWinQuads) k_rlc_window(RlcMsmArgs a) {
 // at n = 1000 (4002 points) it measured 0.84 against 0.82-0.83 ms, hence the 2048-point limit
 // (profiles/r04_small_batch_sparse_ab.json).  G = RlcMsmArgs::sgroups workgroups per window (4 .. 32, ~2 buckets per quad) each
 // take every G-th non-empty bucket (each workgroup lists the window's non-empty buckets itself
-// from the offsets), reduce their quads' sums in LDS and write a partial; k_rlc_window_sum adds
-// a window's partials.
+// from the offsets), reduce their quads' sums in LDS and write a partial; k_rlc_final adds a
+// window's partials as it loads the window sums (a separate summing launch cost ~20 us).
 constexpr int kRlcSparseMaxGroups = 32;
 __global__ void __launch_bounds__(256) k_rlc_window_sparse(RlcMsmArgs a) {
   __shared__ uint32_t cnt[256];
@@ -790,9 +790,9 @@ __global__ void __launch_bounds__(256) k_rlc_window_sparse(RlcMsmArgs a) {
   __builtin_amdgcn_s_setprio(3);
   const int w = blockIdx.y, g = blockIdx.x, t = threadIdx.x;
   const uint32_t* off = a.offsets + (int64_t)w * (kRlcBuckets + 1);
-  constexpr int per = kRlcBuckets / 256;
+  constexpr int per = kRlcBuckets / 256;  // thread t scans buckets t, t + 256, ... (coalesced)
   uint32_t mine = 0;
-  for (int k = 0; k < per; k++) mine += off[t * per + k + 1] > off[t * per + k] ? 1u : 0u;
+  for (int k = 0; k < per; k++) mine += off[k * 256 + t + 1] > off[k * 256 + t] ? 1u : 0u;
   cnt[t] = mine;
   __syncthreads();
   for (int d = 1; d < 256; d <<= 1) {  // inclusive scan of the per-thread counts
@@ -804,7 +804,7 @@ __global__ void __launch_bounds__(256) k_rlc_window_sparse(RlcMsmArgs a) {
   const uint32_t K = cnt[255];  // non-empty buckets of the window (<= its entries <= the MSM's points)
   uint32_t pos = cnt[t] - mine;
   for (int k = 0; k < per && pos < (uint32_t)(kRlcSparsePts + 2); k++) {
-    const int b = t * per + k;
+    const int b = k * 256 + t;
     if (off[b + 1] > off[b]) list[pos++] = (uint16_t)b;
   }
   __syncthreads();
@@ -844,27 +844,6 @@ __global__ void __launch_bounds__(256) k_rlc_window_sparse(RlcMsmArgs a) {
   if (t == 0) store_p3(a.seg_s + (int64_t)w * kRlcSparseMaxGroups + g, red[0]);
 }
 
-// 8 quads per window: quad k adds partials k, k + 8, ..., then a 3-level LDS tree.
-__global__ void __launch_bounds__(512) k_rlc_window_sum(RlcMsmArgs a) {
-  __shared__ ge_p3 red[kRlcWindows][8];
-  const int w = threadIdx.x >> 5, k = (threadIdx.x >> 2) & 7, q = threadIdx.x & 3;
-  const ge_p3* part = a.seg_s + (int64_t)w * kRlcSparseMaxGroups;
-  ge_p3 r = ge_identity();
-#pragma unroll 1
-  for (int g = k; g < a.sgroups; g += 8) r = ge_add_quad(r, load_p3(part + g), q);
-  if (q == 0) red[w][k] = r;
-  __syncthreads();
-#pragma unroll 1
-  for (int o = 4; o > 0; o >>= 1) {
-    ge_p3 x;
-    if (k < o) x = ge_add_quad(red[w][k], red[w][k + o], q);
-    __syncthreads();
-    if (k < o && q == 0) red[w][k] = x;
-    __syncthreads();
-  }
-  if (k == 0 && q == 0) store_p3(a.win + w, red[w][0]);
-}
-
 // P = sum_w 2^(16 w) T_w by a tree on one wave: quad j owns window j; at level `span` the
 // active quads double their upper partner 16 span times and add it to their own (240
 // doublings deep), then the partial is encoded with its identity flag -- or, for one span of
@@ -873,7 +852,15 @@ __global__ void __launch_bounds__(64) k_rlc_final(RlcMsmArgs a) {
   __shared__ ge_p3 lds[kRlcWindows];
   __builtin_amdgcn_s_setprio(3);
   const int j = threadIdx.x >> 2, q = threadIdx.x & 3;
-  if (q == 0) lds[j] = load_p3(a.win + j);
+  if (a.sparse) {  // window j's sum from its k_rlc_window_sparse partials
+    const ge_p3* part = a.seg_s + (int64_t)j * kRlcSparseMaxGroups;
+    ge_p3 T = load_p3(part);
+#pragma unroll 1
+    for (int g = 1; g < a.sgroups; g++) T = ge_add_quad(T, load_p3(part + g), q);
+    if (q == 0) lds[j] = T;
+  } else if (q == 0) {
+    lds[j] = load_p3(a.win + j);
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   for (int span = 1; span < kRlcWindows; span <<= 1) {  // one wave: LDS traffic stays in program order
@@ -1019,8 +1006,6 @@ hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0,
   if ((e = mark(3)) != hipSuccess) return e;
   if (a2.sparse) {
     hipLaunchKernelGGL(k_rlc_window_sparse, dim3((unsigned)a2.sgroups, kRlcWindows), dim3(256), 0, st, a2);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_rlc_window_sum, dim3(1), dim3(32 * kRlcWindows), 0, st, a2);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   } else {
     const int64_t ns = (int64_t)kRlcWindows * (kRlcBuckets / kRlcSegLen);

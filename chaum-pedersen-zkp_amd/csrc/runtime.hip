@@ -69,6 +69,29 @@ struct DevBuf {
   }
 };
 
+// Page-locked host memory (hipHostMalloc), grown on demand.
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) {
+      hipError_t e = hipHostFree(p);
+      p = nullptr;
+      cap = 0;
+      if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
 // A stream on a hardware queue of its own.  HIP maps plain streams onto at most
 // GPU_MAX_HW_QUEUES (4 by default) queues per process, reusing the least-used one beyond that,
 // and two streams on one queue run one after the other: two torch streams created after the
@@ -187,6 +210,11 @@ struct cpz_ctx {
   // host-API staging (y1, y2, r1, r2, s, and challenges / witnesses / nonces)
   DevBuf in[7];
   DevBuf ctxb, ctxo, ctxp;
+  // small host-buffer calls: inputs packed into one page-locked block and one copy (`in_all`),
+  // and the RLC check's partial, flags and statuses read back with one synchronisation (`pin`
+  // from kPinMail on; the mailbox words at its start)
+  DevBuf in_all;
+  PinnedBuf pin;
   // host-buffer pipeline (cpz_verify_each): H2D copies of chunk j+1 on their own stream
   // while chunk j verifies on `stream`
   hipStream_t copy_stream = nullptr;
@@ -522,9 +550,46 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
 }
 
 // Stage host inputs on the device.  Returns device pointers through out[].
+// Host-buffer calls of up to kPinStageMax input bytes: the rows (and transcript contexts) are
+// packed into page-locked memory and sent with one copy.  A BatchVerifier-sized call made five
+// to eight pageable copies, ~10 us of host round trip each (rocprofv3 timeline, n = 10).
+constexpr size_t kPinMail = 256;                  // mailbox bytes at the start of ctx->pin
+constexpr size_t kPinStageMax = size_t(8) << 20;  // larger inputs: one pageable copy per row
+inline size_t pad16(size_t x) { return (x + 15) & ~size_t(15); }
+
 int stage_inputs(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], int count, const uint8_t* ctx_bytes,
                  const uint64_t* ctx_off, const uint8_t* ctx_present, const void* dev[5], const void** dcb,
                  const uint64_t** dco, const uint8_t** dcp) {
+  if (ctx_off)
+    for (size_t i = 0; i < n; i++)
+      if (ctx_off[i + 1] < ctx_off[i]) return fail(CPZ_EINVAL, "ctx_off must be non-decreasing");
+  const size_t nbytes = ctx_off ? (size_t)(ctx_off[n] - ctx_off[0]) : 0;
+  const size_t rows = (size_t)count * n * 32;
+  const size_t o_off = rows, o_pres = pad16(o_off + (ctx_off ? (n + 1) * 8 : 0));
+  const size_t o_ctx = pad16(o_pres + (ctx_off && ctx_present ? n : 0));
+  const size_t total = pad16(o_ctx + (ctx_off ? std::max<size_t>(nbytes, 1) : 0));
+  if (total <= kPinStageMax && ctx->pin.ensure(kPinMail + total + pad16(n)) == hipSuccess &&
+      ctx->in_all.ensure(total) == hipSuccess) {
+    // no copy of an earlier call may still read the block (host-buffer calls return
+    // synchronised; this covers one that failed part-way)
+    CPZ_HIP(hipStreamSynchronize(ctx->stream));
+    uint8_t* h = static_cast<uint8_t*>(ctx->pin.p) + kPinMail;
+    for (int k = 0; k < count; k++) std::memcpy(h + (size_t)k * n * 32, host[k], n * 32);
+    if (ctx_off) {
+      uint64_t* rel = reinterpret_cast<uint64_t*>(h + o_off);
+      for (size_t i = 0; i <= n; i++) rel[i] = ctx_off[i] - ctx_off[0];
+      if (ctx_present) std::memcpy(h + o_pres, ctx_present, n);
+      if (nbytes) std::memcpy(h + o_ctx, ctx_bytes + ctx_off[0], nbytes);
+    }
+    CPZ_HIP(hipMemcpyAsync(ctx->in_all.p, h, total, hipMemcpyHostToDevice, ctx->stream));
+    uint8_t* d = static_cast<uint8_t*>(ctx->in_all.p);
+    for (int k = 0; k < count; k++) dev[k] = d + (size_t)k * n * 32;
+    *dcb = ctx_off ? d + o_ctx : nullptr;
+    *dco = ctx_off ? reinterpret_cast<const uint64_t*>(d + o_off) : nullptr;
+    *dcp = ctx_off && ctx_present ? d + o_pres : nullptr;
+    return CPZ_OK;
+  }
+  (void)hipGetLastError();
   for (int k = 0; k < count; k++) {
     CPZ_HIP(ctx->in[k].ensure(n * 32));
     CPZ_HIP(hipMemcpyAsync(ctx->in[k].p, host[k], n * 32, hipMemcpyHostToDevice, ctx->stream));
@@ -534,9 +599,6 @@ int stage_inputs(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], int count
   *dco = nullptr;
   *dcp = nullptr;
   if (ctx_off) {
-    const size_t nbytes = ctx_off[n] - ctx_off[0];
-    for (size_t i = 0; i < n; i++)
-      if (ctx_off[i + 1] < ctx_off[i]) return fail(CPZ_EINVAL, "ctx_off must be non-decreasing");
     std::vector<uint64_t> rel(n + 1);
     for (size_t i = 0; i <= n; i++) rel[i] = ctx_off[i] - ctx_off[0];
     CPZ_HIP(ctx->ctxb.ensure(nbytes ? nbytes : 1));
@@ -660,7 +722,7 @@ int rlc_msm_args(const RlcPrepared& P, RlcMsmSet& S, int64_t lo, int64_t hi, cpz
 // but ~1.8 TB/s over 4 GiB (translation misses, tools/ubench/gather_bytes.hip), so a
 // 2^26-proof MSM over one 32 GiB points array spent 2.8x the per-entry bucket time of a 2^20
 // one.  Synchronises; returns the partial encoding and identity flag.
-int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t partial[32], int* identity) {
+int rlc_range_launch(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st) {
   static_assert(CPZ_RLC_SPAN % cpz::kRlcPrepBlock == 0, "spans are whole weight blocks");
   static_assert(cpz::kRlcPrepBlock % cpz::kRlcSumBlock == 0, "ranges are whole block sums");
   static_assert(4ll * CPZ_RLC_SPAN + 2 <= cpz::kRlcMaxMsmPoints, "a span's MSM exceeds the sort-entry format");
@@ -700,6 +762,13 @@ int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t part
     if (timed)
       for (int k = 0; k + 1 < cpz::kRlcMsmMarks; k++) ctx->marks.push_back({8 + k, marks[k], marks[k + 1]});
   }
+  return CPZ_OK;
+}
+
+// rlc_range_launch, then the partial and identity flag read back (synchronises).
+int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t partial[32], int* identity) {
+  if (int rc = rlc_range_launch(ctx, lo, hi, st)) return rc;
+  RlcMsmSet& S = ctx->rl_msm;
   int flags[1];
   CPZ_HIP(hipMemcpyAsync(partial, S.partial.p, 32, hipMemcpyDeviceToHost, st));
   CPZ_HIP(hipMemcpyAsync(flags, S.flags.p, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -1250,15 +1319,27 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
     }
   }
   if ((rc = rlc_prepare_points(ctx, n, y1, y2, r1, r2, s, d_status, seed, first_index, st))) return rc;
-  uint8_t part[32];
-  int ident = 0;
-  rc = rlc_range(ctx, 0, (int64_t)n, st, part, &ident);
-  if (rc) return rc;
-  if (partial_out) std::memcpy(partial_out, part, 32);
+  // The partial, its identity flag, the any-bad word and (host-buffer calls) the statuses come
+  // back with one synchronisation, into page-locked memory when it is there: a valid batch
+  // needs no second round trip.  A failing one re-reads the statuses after its fallback.
+  if ((rc = rlc_range_launch(ctx, 0, (int64_t)n, st))) return rc;
+  const bool stage_st = host_status && n <= kPinStageMax;  // (the staged inputs there are spent)
+  const bool pinned = ctx->pin.ensure(kPinMail + (stage_st ? pad16(n) : 0)) == hipSuccess;
+  (void)hipGetLastError();
+  uint8_t part_buf[32];
+  int word_buf[2] = {0, 0};
+  uint8_t* part = pinned ? static_cast<uint8_t*>(ctx->pin.p) : part_buf;
+  int* words = pinned ? reinterpret_cast<int*>(static_cast<uint8_t*>(ctx->pin.p) + 32) : word_buf;
+  uint8_t* st_stage = pinned && stage_st ? static_cast<uint8_t*>(ctx->pin.p) + kPinMail : host_status;
+  CPZ_HIP(hipMemcpyAsync(part, ctx->rl_msm.partial.p, 32, hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipMemcpyAsync(&words[0], ctx->rl_msm.flags.p, sizeof(int), hipMemcpyDeviceToHost, st));
   // every entry must also have decoded (zero-weight entries are not "verified")
-  int any_bad = 0;
-  CPZ_HIP(hipMemcpyAsync(&any_bad, static_cast<int*>(ctx->rl_flags.p) + 3, sizeof(int), hipMemcpyDeviceToHost, st));
+  CPZ_HIP(hipMemcpyAsync(&words[1], static_cast<int*>(ctx->rl_flags.p) + 3, sizeof(int), hipMemcpyDeviceToHost, st));
+  if (host_status) CPZ_HIP(hipMemcpyAsync(st_stage, d_status, n, hipMemcpyDeviceToHost, st));
   CPZ_HIP(hipStreamSynchronize(st));
+  const int ident = words[0];
+  const int any_bad = words[1];
+  if (partial_out) std::memcpy(partial_out, part, 32);
   const bool all_live = any_bad == 0;
   if (batch_ok) *batch_ok = (ident && all_live) ? 1 : 0;
   if (!ident && fallback) {
@@ -1279,11 +1360,13 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
       if (rc) return rc;
     }
     CPZ_HIP(hipStreamSynchronize(st));  // statuses complete on return (documented)
+    if (host_status) {
+      CPZ_HIP(hipMemcpyAsync(host_status, d_status, n, hipMemcpyDeviceToHost, st));
+      CPZ_HIP(hipStreamSynchronize(st));
+    }
+    return CPZ_OK;
   }
-  if (host_status) {
-    CPZ_HIP(hipMemcpyAsync(host_status, d_status, n, hipMemcpyDeviceToHost, st));
-    CPZ_HIP(hipStreamSynchronize(st));
-  }
+  if (host_status && st_stage != host_status) std::memcpy(host_status, st_stage, n);
   return CPZ_OK;
 }
 
@@ -1692,6 +1775,8 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->st.release();
   ctx->scratch.release();
   for (auto& b : ctx->in) b.release();
+  ctx->in_all.release();
+  ctx->pin.release();
   ctx->ctxb.release();
   ctx->ctxo.release();
   ctx->ctxp.release();
