@@ -39,7 +39,7 @@ __all__ = [
 MAX_BATCH_SIZE = 1000          # batch.rs:48
 # Smallest Parameters group that BatchVerifier.verify sends to the RLC batch check (smaller
 # groups: per-proof verification); rust/reference-patch/gpu.rs RLC_MIN_GROUP, cpz_batch.hpp.
-RLC_MIN_GROUP = 1
+RLC_MIN_GROUP = 1001
 PROTOCOL_VERSION = 1           # gadgets.rs:12
 L = 2**252 + 27742317777372353535851937790883648493   # group order (ristretto.rs scalars)
 

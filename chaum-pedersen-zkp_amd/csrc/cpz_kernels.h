@@ -90,6 +90,21 @@ struct ProbeGatherArgs {
   uint8_t* out_present;
 };
 
+// Launches of at most kQuadVerifyMax proofs are verified on eight lanes per proof
+// (k_verify_quad), larger ones on one lane per proof (k_verify_each).  cpz_verify_each_device
+// per call (tools/quad_crossover.py): eight lanes 0.39 / 0.40 / 0.41 / 0.42 / 0.78 / 1.52 ms at
+// 1K / 2K / 4K / 8K / 16K / 32K proofs, one lane 1.26-1.31 ms at all of them.  The scratch slab
+// holds kQuadProofScratch bytes of tables per proof for them (VerifyArgs::quad_max).
+#ifndef CPZ_VERIFY_QUAD
+#define CPZ_VERIFY_QUAD 1
+#endif
+#ifndef CPZ_QUAD_MAX
+#define CPZ_QUAD_MAX 16384
+#endif
+constexpr int64_t kQuadVerifyMax = CPZ_QUAD_MAX;
+constexpr int kQuadTableInts = 2 * 9 * 40;  // per quad: two tables of 9 entries of 4 x 10 limbs
+constexpr int64_t kQuadProofScratch = 2 * kQuadTableInts * 4;
+
 struct VerifyArgs {
   int64_t n;
   const uint32_t* y1;
@@ -112,6 +127,8 @@ struct VerifyArgs {
                                     // the global proof index
   int block_proofs = 0;
   int64_t nblocks = 0;
+  int64_t quad_max = 0;             // launches of at most this many proofs use k_verify_quad (the
+                                    // runtime: kQuadVerifyMax, bounded by the slab's size)
 };
 
 struct ProveArgs {

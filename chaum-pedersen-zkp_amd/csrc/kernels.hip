@@ -32,6 +32,7 @@
 #include "transcript.h"
 #include "scalarmul.h"
 #include "verify.h"
+#include "rlc_dev.h"
 
 namespace cpz {
 
@@ -588,8 +589,204 @@ int verify_each_blocks_per_cu() {
   return nb;
 }
 
+// ---------------------------------------------------------------------------------------
+// Small batches: one proof on eight lanes, a quad per equation (rlc_dev.h's quad-cooperative
+// point arithmetic: the four lanes hold the same point, each computes one of a round's four
+// products).  k_verify_each gives every proof one lane, so a batch of a few proofs waits for
+// one lane's whole verification (~1.1 ms: 31 x 4 doublings and 64 additions per equation
+// issued one instruction per ~10 cycles by a lone wave); here the two equations run side by
+// side and every point operation takes two product latencies instead of eight.  Lanes 0 / 1
+// of a quad decode Y / R of its equation; the quad's tables (cached multiples 0..8 of -Y and
+// of -R, or R when v < 0) live in the scratch slab, 160 bytes per entry, lane q storing and
+// loading only field q (Y+X, Y-X, 2dT, Z: the operand fe_sel4 hands it), so a negative digit
+// is lanes 0 / 1 swapping fields and lane 2 negating its own.  Same statuses as verify_proof.
+// ---------------------------------------------------------------------------------------
+
+__device__ __forceinline__ void fe_store_limbs(int32_t* dst, const fe& f) {
+  uint2* d = reinterpret_cast<uint2*>(dst);
+#pragma unroll
+  for (int k = 0; k < 5; k++) d[k] = make_uint2((uint32_t)f.v[2 * k], (uint32_t)f.v[2 * k + 1]);
+}
+
+__device__ __forceinline__ fe fe_load_limbs(const int32_t* src) {
+  const uint2* d = reinterpret_cast<const uint2*>(src);
+  fe f;
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    const uint2 v = d[k];
+    f.v[2 * k] = (int32_t)v.x;
+    f.v[2 * k + 1] = (int32_t)v.y;
+  }
+  return f;
+}
+
+// field q of the cached form, in fe_sel4 order (Y+X, Y-X, 2dT, Z)
+__device__ __forceinline__ fe cached_field(const ge_cached& c, int q) { return fe_sel4(q, c.YpX, c.YmX, c.T2d, c.Z); }
+
+__device__ __forceinline__ ge_cached cached_of_field(const fe& x) {
+  ge_cached c;
+  c.YpX = x;
+  c.YmX = x;
+  c.T2d = x;
+  c.Z = x;
+  return c;
+}
+
+// entries 0..8 of the quad's table of P (lane q writes field q)
+__device__ __forceinline__ void quad_table(int32_t* tab, const ge_p3& P, int q) {
+  fe_store_limbs(tab + q * 10, cached_field(ge_cached_identity(), q));
+  const ge_cached c1 = p3_to_cached(P);
+  fe_store_limbs(tab + 40 + q * 10, cached_field(c1, q));
+  ge_p3 acc = p3_dbl_n_quad(P, 1, q);
+  fe_store_limbs(tab + 80 + q * 10, cached_field(p3_to_cached(acc), q));
+#pragma unroll 1
+  for (int k = 3; k <= 8; k++) {
+    acc = ge_add_quad(acc, c1, q);
+    fe_store_limbs(tab + 40 * k + q * 10, cached_field(p3_to_cached(acc), q));
+  }
+}
+
+// lane q's operand of signed digit d: entry |d|; a negative digit swaps Y+X / Y-X and
+// negates 2dT
+__device__ __forceinline__ fe quad_lookup(const int32_t* tab, int d, int q) {
+  const bool neg = d < 0;
+  const int mag = neg ? -d : d;
+  const int f = (neg && q < 2) ? 1 - q : q;
+  const fe x = fe_load_limbs(tab + 40 * mag + 10 * f);
+  return (neg && q == 2) ? fe_neg(x) : x;
+}
+
+__device__ __forceinline__ ge_p3 p3_bcast(const ge_p3& P, int from) {
+  ge_p3 r;
+  if (from == 0) {
+    r.X = fe_quad_bcast<0>(P.X); r.Y = fe_quad_bcast<0>(P.Y); r.Z = fe_quad_bcast<0>(P.Z); r.T = fe_quad_bcast<0>(P.T);
+  } else {
+    r.X = fe_quad_bcast<1>(P.X); r.Y = fe_quad_bcast<1>(P.Y); r.Z = fe_quad_bcast<1>(P.Z); r.T = fe_quad_bcast<1>(P.T);
+  }
+  return r;
+}
+
+template <bool kPre>
+__global__ void __launch_bounds__(256) k_verify_quad(VerifyArgs a) {
+  const int t = threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * 32 + (t >> 3);
+  const int e = (t >> 2) & 1, q = t & 3;
+  if (i >= a.n) return;                          // a proof's eight lanes together
+  if (kPre && a.status[i] != kStOk) return;      // decode-level rejection: already final
+  const CombTable comb{a.comb + (e ? kCombPerBase : 0)};
+  int32_t* tab = reinterpret_cast<int32_t*>(a.scratch) + ((int64_t)blockIdx.x * 64 + (t >> 2)) * kQuadTableInts;
+  uint32_t sw[8], cw[8];
+  load_words8(sw, a.s, i);
+  load_words8(cw, a.c, i);
+  const uint8_t st_s = kPre ? kStOk : a.status[i];
+  // challenge split and digits, identical on every lane (verify_proof)
+  uint32_t ud[4], vd[4], sd[8];
+  bool vneg;
+  {
+    uint32_t u[4], va[4];
+    sc_half_split(cw, u, va, vneg);
+    sc_recode_radix16_half(ud, u);
+    sc_recode_radix16_half(vd, va);
+    sc vs, ss;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      vs.w[k] = k < 4 ? va[k] : 0u;
+      ss.w[k] = sw[k];
+    }
+    sc sp = sc_mul(vs, ss);
+    if (vneg) sp = sc_neg(sp);
+    sc_recode_radix65536(sd, sp.w);
+  }
+  // lane 0 decodes this equation's Y, lane 1 its R
+  ge_p3 P = ge_identity();
+  bool ok = true;
+  if (q < 2) {
+    if constexpr (kPre) {
+      P = affine_from_neg_niels(niels_load(a.pre + 4 * i + (q == 0 ? 1 + 2 * e : 2 * e)));
+    } else {
+      uint32_t enc[8];
+      load_words8(enc, q == 0 ? (e ? a.y2 : a.y1) : (e ? a.r2 : a.r1), i);
+      ok = ristretto_decode(P, enc);
+    }
+  }
+  ge_p3 Y = p3_bcast(P, 0), R = p3_bcast(P, 1);
+  Y = ge_neg(Y);
+  if (!vneg) R = ge_neg(R);
+  quad_table(tab, Y, q);
+  quad_table(tab + kQuadTableInts / 2, R, q);
+  __threadfence_block();  // the quad's other lanes' fields (a negative digit reads them)
+  // Q = [u] Y' + [|v|] R' + [s'] B: identity (mod E[4]) iff the equation holds
+  ge_p3 acc = ge_identity();
+#pragma unroll 1
+  for (int j = 0; j < 4; j++) {
+    const uint32_t wu = ud[3], wv = vd[3];
+#pragma unroll
+    for (int k = 3; k > 0; k--) {
+      ud[k] = ud[k - 1];
+      vd[k] = vd[k - 1];
+    }
+#pragma unroll 1
+    for (int m = 7; m >= 0; m--) {
+      const int du = ((int32_t)(wu << (28 - 4 * m))) >> 28;
+      const int dv = ((int32_t)(wv << (28 - 4 * m))) >> 28;
+      const fe ey = quad_lookup(tab, du, q), er = quad_lookup(tab + kQuadTableInts / 2, dv, q);
+      if (j != 0 || m != 7) acc = p3_dbl_n_quad(acc, 4, q);
+      acc = ge_add_quad(acc, cached_of_field(ey), q);
+      acc = ge_add_quad(acc, cached_of_field(er), q);
+    }
+  }
+#pragma unroll 1
+  for (int j = 0; j < 8; j++) {
+    const uint32_t w = sd[0];
+#pragma unroll
+    for (int k = 0; k < 7; k++) sd[k] = sd[k + 1];
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+      const int d = (int32_t)(w << (16 - 16 * m)) >> 16;
+      const ge_niels nl = comb.lookup(2 * j + m, d);
+      ge_cached c;
+      c.YpX = nl.ypx;
+      c.YmX = nl.ymx;
+      c.T2d = nl.xy2d;
+      c.Z = fe_one();
+      acc = ge_add_quad(acc, c, q);
+    }
+  }
+  // the proof's verdict from its two quads (lane 0 of quad e = 0 writes it)
+  int eq = ristretto_is_identity(acc) ? 1 : 0;
+  eq &= __shfl_xor(eq, 4);
+  int bad = ok ? 0 : 1;
+  bad |= __shfl_xor(bad, 1);
+  bad |= __shfl_xor(bad, 2);
+  bad |= __shfl_xor(bad, 4);
+  if ((t & 7) != 0) return;
+  bool rid = false;
+  if constexpr (!kPre) {
+    uint32_t w1[8], w2[8];
+    load_words8(w1, a.r1, i);
+    load_words8(w2, a.r2, i);
+    rid = words8_zero(w1) || words8_zero(w2);
+  }
+  uint8_t st;
+  if (bad) st = kStBadPoint;
+  else if (st_s == kStBadScalar) st = kStBadScalar;
+  else if (rid && !a.eq_only) st = kStIdentity;
+  else if (st_s == kStZeroS) st = kStZeroS;
+  else if (st_s == kStBadChallenge) st = kStBadScalar;
+  else st = eq ? kStOk : kStEqFail;
+  a.status[i] = st;
+}
+
 hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
+  if (CPZ_VERIFY_QUAD && !a.blocks && a.n <= a.quad_max) {  // small batches: eight lanes per proof
+    const unsigned g = (unsigned)((a.n + 31) / 32);
+    if (a.pre)
+      hipLaunchKernelGGL(k_verify_quad<true>, dim3(g), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL(k_verify_quad<false>, dim3(g), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
   if (a.pre)
     hipLaunchKernelGGL(k_verify_prepared, dim3(grid), dim3(kVerifyBlock), 0, st, a);
   else

@@ -481,6 +481,7 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
     v.c = va.c + 8 * a;
     if (va.pre) v.pre = va.pre + 4 * a;
     v.status = va.status + a;
+    v.quad_max = std::min<int64_t>(cpz::kQuadVerifyMax, (int64_t)(slab / cpz::kQuadProofScratch));
     const int k = (int)((rr ? rr->next++ : c) % nst);  // stream k owns scratch slab k
     v.scratch = static_cast<char*>(ctx->scratch.p) + (size_t)k * slab;
     hipStream_t sc = k == 0 ? st : ctx->aux_stream[k - 1];
@@ -1921,8 +1922,12 @@ int cpz_verify_each_ex(cpz_ctx* ctx, uint32_t flags, const uint8_t g[32], const 
   rc = enqueue_verify(ctx, n, dev[0], dev[1], dev[2], dev[3], dev[4], dcb, dco, dcp,
                       static_cast<uint8_t*>(ctx->st.p), ctx->stream);
   if (rc) return rc;
-  CPZ_HIP(hipMemcpyAsync(status_out, ctx->st.p, n, hipMemcpyDeviceToHost, ctx->stream));
+  // statuses through the page-locked block when stage_inputs used it (its inputs are spent)
+  const bool pinned = ctx->pin.cap >= kPinMail + pad16(n);
+  uint8_t* dst = pinned ? static_cast<uint8_t*>(ctx->pin.p) + kPinMail : status_out;
+  CPZ_HIP(hipMemcpyAsync(dst, ctx->st.p, n, hipMemcpyDeviceToHost, ctx->stream));
   CPZ_HIP(hipStreamSynchronize(ctx->stream));
+  if (pinned) std::memcpy(status_out, dst, n);
   return CPZ_OK;
 }
 

@@ -49,10 +49,12 @@ constexpr std::size_t MAX_BATCH_SIZE = 1000;  // batch.rs:48
 // Smallest Parameters group that takes the RLC batch check rather than per-proof
 // verification (both return verify_one's outcome per entry).  The same threshold as
 // rust/reference-patch/gpu.rs (RLC_MIN_GROUP), from the per-call latency table
-// profiles/r04_small_batch.json: one synchronous host-buffer call takes 0.62-0.68 ms through
-// the RLC check at n = 1 .. 100 and 0.83 ms at 1000, against 1.26-1.68 ms per proof, so every
-// group takes the RLC check (a one-entry batch keyed by the OS's randomness, not the caller's).
-constexpr std::size_t RLC_MIN_GROUP = 1;
+// profiles/r04_small_batch.json: one synchronous host-buffer call takes 0.39-0.48 ms per proof
+// (eight lanes each, k_verify_quad) at every n from 1 to 1000, against 0.54-0.59 ms through the
+// RLC check at n <= 100 and 0.74 ms at 1000, so no group of at most MAX_BATCH_SIZE entries takes
+// the RLC check (set_rlc_min_group lowers it; a one-entry batch is then keyed by the OS's
+// randomness, not the caller's).
+constexpr std::size_t RLC_MIN_GROUP = 1001;
 
 using Bytes32 = std::array<uint8_t, 32>;
 

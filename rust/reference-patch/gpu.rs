@@ -56,10 +56,11 @@ const CONTEXTS_PER_DEVICE: usize = 2;
 /// Smallest `Parameters` group sent to the RLC batch check; smaller groups are verified per
 /// proof (cpz_verify_each).  Both return `verify_one`'s outcome; the threshold only picks the
 /// faster entry point at the batch sizes this API carries (n <= 1000, batch.rs:48), from the
-/// per-call latency table profiles/r04_small_batch.json (bench.py small_batch): 0.62-0.68 ms
-/// per RLC call at n = 1 .. 100 and 0.83 ms at 1000, against 1.26-1.68 ms per proof, so every
-/// group takes the RLC check.
-const RLC_MIN_GROUP: usize = 1;
+/// per-call latency table profiles/r04_small_batch.json (bench.py small_batch): per proof on
+/// eight lanes each (k_verify_quad) 0.39-0.48 ms at every n from 1 to 1000, the RLC check
+/// 0.54-0.59 ms at n <= 100 and 0.74 ms at 1000, so no group of this API (at most 1000
+/// entries, batch.rs:48) takes the RLC check; the path stays for callers that lower it.
+const RLC_MIN_GROUP: usize = 1001;
 
 /// The process's verifier contexts (see above).
 struct Pool {

@@ -45,12 +45,24 @@ def _le(b):
 
 
 def test_c2_sample_every_forgery_kind(gpu, golden):
-    n = 1 << 20
-    rng = np.random.default_rng(20)
+    _every_forgery_kind(gpu, golden, 1 << 20, 1 << 16, 20)
+
+
+@pytest.mark.parametrize("n", [2047, 2048, 2049])
+def test_small_batch_eight_lanes_every_forgery_kind(gpu, golden, n):
+    """Batches of at most 2048 proofs are verified on eight lanes per proof (k_verify_quad,
+    a quad per equation), larger ones on one lane per proof (k_verify_each): on both sides of
+    the limit every entry's status and challenge equal the C oracle's, with a quarter of the
+    entries carrying one of the seven forgery / malformation kinds."""
+    _every_forgery_kind(gpu, golden, n, n, 7 + n)
+
+
+def _every_forgery_kind(gpu, golden, n, nsample, seed):
+    rng = np.random.default_rng(seed)
     ctxs = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() if i % 4 == 0 else None for i in range(n)]
     rows = gpu.prove_synthetic(n, SX, SK, contexts=ctxs)
     rows = {k: np.ascontiguousarray(rows[k]) for k in KEYS}
-    sample = np.sort(rng.choice(n, size=1 << 16, replace=False))
+    sample = np.sort(rng.choice(n, size=nsample, replace=False))
     forged = sample[rng.random(sample.size) < 0.25]
     kinds = ("s_plus_1", "wrong_y1", "wrong_context", "bad_point", "s_plus_l", "zero_s", "identity_r")
     bad_pts = [bytes.fromhex(e) for e in golden["rfc9496_bad"]]
