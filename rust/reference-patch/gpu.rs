@@ -8,16 +8,16 @@
 //!
 //! What the GPU computes, per `Parameters` group of entries (groups in order of first
 //! appearance):
-//!   * n == 1 (batch.rs:178-180): `verify_one`; `rng` is not touched, as in the reference.
-//!     The entry's RLC check (0.65 against 1.46 ms per proof, profiles/r04_small_batch.json)
-//!     is keyed by a seed from the OS (`OsRng`), and a failing check verifies it per proof.
-//!   * n >= 2 (batch.rs:233-269): a 32-byte seed drawn once from `rng` (the reference draws
-//!     its weights from it, batch.rs:240) keys the random-linear-combination check of every
-//!     group of at least RLC_MIN_GROUP entries (cpz_verify_batch: the batch equation with the
-//!     weights on every term, one Pippenger MSM); a failing batch runs the fallback search,
-//!     which returns exactly `verify_one`'s outcome per entry (verify_individually,
-//!     batch.rs:262-268, 314-318).  A smaller group runs cpz_verify_each, which returns the
-//!     same outcome.  Groups take consecutive weight indices (`first_index`).
+//!   * a group of fewer than RLC_MIN_GROUP entries -- every group of this API's batches (at
+//!     most 1000 entries), from the measured latencies -- runs cpz_verify_each: `verify_one`
+//!     per entry (batch.rs:185-231), eight GPU lanes per proof;
+//!   * a larger group takes the random-linear-combination check (cpz_verify_batch: the batch
+//!     equation with the weights on every term, one Pippenger MSM), keyed by a 32-byte seed
+//!     drawn once from `rng` (the reference draws its weights from it, batch.rs:240) -- or,
+//!     for a one-entry batch, which the reference verifies with `verify_one` without touching
+//!     `rng` (batch.rs:178-180), from the OS (`OsRng`); a failing check runs the fallback
+//!     search, which returns exactly `verify_one`'s outcome per entry (verify_individually,
+//!     batch.rs:262-268, 314-318).  Groups take consecutive weight indices (`first_index`).
 //! Every call passes EQUATIONS_ONLY: a `Proof` may have been built with `Proof::new` (no
 //! identity / zero-s checks, gadgets.rs:252, 278, 317), and `verify_one` judges it by the
 //! two equations alone -- so the result vector is the reference's for every batch, not only

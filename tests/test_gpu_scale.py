@@ -48,9 +48,9 @@ def test_c2_sample_every_forgery_kind(gpu, golden):
     _every_forgery_kind(gpu, golden, 1 << 20, 1 << 16, 20)
 
 
-@pytest.mark.parametrize("n", [2047, 2048, 2049])
+@pytest.mark.parametrize("n", [16383, 16384, 16385])
 def test_small_batch_eight_lanes_every_forgery_kind(gpu, golden, n):
-    """Batches of at most 2048 proofs are verified on eight lanes per proof (k_verify_quad,
+    """Launches of at most 16384 proofs are verified on eight lanes per proof (k_verify_quad,
     a quad per equation), larger ones on one lane per proof (k_verify_each): on both sides of
     the limit every entry's status and challenge equal the C oracle's, with a quarter of the
     entries carrying one of the seven forgery / malformation kinds."""
