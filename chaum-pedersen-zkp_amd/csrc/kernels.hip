@@ -669,12 +669,17 @@ __device__ __forceinline__ ge_p3 p3_bcast(const ge_p3& P, int from) {
 template <bool kPre>
 __global__ void __launch_bounds__(256) k_verify_quad(VerifyArgs a) {
   const int t = threadIdx.x;
-  const int64_t i = (int64_t)blockIdx.x * 32 + (t >> 3);
+  int64_t i = (int64_t)blockIdx.x * 32 + (t >> 3);
   const int e = (t >> 2) & 1, q = t & 3;
+  if (a.blocks) {  // listed blocks of block_proofs proofs (the partitioned check's per-proof passes)
+    const int64_t lb = i / a.block_proofs;
+    if (lb >= a.nblocks) return;
+    i = (int64_t)a.blocks[lb] * a.block_proofs + i % a.block_proofs;
+  }
   if (i >= a.n) return;                          // a proof's eight lanes together
   if (kPre && a.status[i] != kStOk) return;      // decode-level rejection: already final
   const CombTable comb{a.comb + (e ? kCombPerBase : 0)};
-  int32_t* tab = reinterpret_cast<int32_t*>(a.scratch) + ((int64_t)blockIdx.x * 64 + (t >> 2)) * kQuadTableInts;
+  int32_t* tab = reinterpret_cast<int32_t*>(a.scratch) + ((int64_t)blockIdx.x * 64 + (t >> 2)) * kQuadTableInts;  // by slot
   uint32_t sw[8], cw[8];
   load_words8(sw, a.s, i);
   load_words8(cw, a.c, i);
@@ -779,8 +784,9 @@ __global__ void __launch_bounds__(256) k_verify_quad(VerifyArgs a) {
 
 hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
-  if (CPZ_VERIFY_QUAD && !a.blocks && a.n <= a.quad_max) {  // small batches: eight lanes per proof
-    const unsigned g = (unsigned)((a.n + 31) / 32);
+  const int64_t slots = a.blocks ? a.nblocks * (int64_t)a.block_proofs : a.n;
+  if (CPZ_VERIFY_QUAD && slots <= a.quad_max) {  // small batches: eight lanes per proof
+    const unsigned g = (unsigned)((slots + 31) / 32);
     if (a.pre)
       hipLaunchKernelGGL(k_verify_quad<true>, dim3(g), dim3(256), 0, st, a);
     else

@@ -969,6 +969,25 @@ int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* stat
   const int full = (occupancy_grid(ctx) + CPZ_VERIFY_CHUNK_DIV - 1) / CPZ_VERIFY_CHUNK_DIV;
   const size_t slab = (size_t)full * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached);
   CPZ_HIP(ctx->scratch.ensure((size_t)CPZ_VERIFY_STREAMS * slab));
+  const int64_t quad_max = std::min<int64_t>(cpz::kQuadVerifyMax, (int64_t)(slab / cpz::kQuadProofScratch));
+  if (CPZ_VERIFY_QUAD && nb * block_proofs <= quad_max) {  // one eight-lanes-per-proof launch (k_verify_quad)
+    cpz::VerifyArgs v;
+    v.n = n;
+    v.s = static_cast<const uint32_t*>(s);
+    v.c = static_cast<const uint32_t*>(ctx->c.p);
+    v.status = status;
+    v.comb = static_cast<const cpz::ge_niels*>(ctx->gs->comb.p);
+    v.pre = static_cast<const cpz::ge_niels*>(ctx->rl_prep.pts.p);
+    v.eq_only = ctx->call_eq ? 1 : 0;
+    v.scratch = static_cast<char*>(ctx->scratch.p);
+    v.blocks = d_blocks;
+    v.block_proofs = block_proofs;
+    v.nblocks = nb;
+    v.quad_max = quad_max;
+    StageTimer t(ctx, 1, st);
+    CPZ_HIP(cpz::launch_verify_each(v, 0, st));
+    return CPZ_OK;
+  }
   const int64_t groups = (nb + G - 1) / G;
   const int64_t chunks = (groups + full - 1) / full;
   const int nst = (int)std::min<int64_t>(CPZ_VERIFY_STREAMS, chunks);
