@@ -408,6 +408,54 @@ __global__ void __launch_bounds__(64) k_part_combine(PartArgs a) {
   }
 }
 
+// The same per block for very few blocks (the locate pass of a sparse failure: each wave of
+// k_part_combine runs ~800 dependent quad operations, 1.7 ms, whatever the block count): one
+// workgroup of 32 quads per block, quad v forming T_v, then P_b = sum_v 2^(8 v) T_v by a tree
+// (depth 8 + 16 + 32 + 64 + 128 doublings).  Its upper levels leave most quads of a wave idle,
+// so at scale it costs far more than the packed chain (C5's 15,776-block locate pass: 202 ms
+// against 197.5; every size: 245 ms), hence kPartTreeMaxBlocks.
+__device__ __forceinline__ ge_p3 part_window_sum(const ge_p3* ws, int v, int q) {
+  const ge_p3* w = ws + v * kPartQuarters * 2;
+  const ge_p3 U = load_p3(w + 7);
+  const ge_p3 V = ge_add_quad(load_p3(w + 5), U, q);
+  const ge_p3 X = ge_add_quad(load_p3(w + 3), V, q);
+  const ge_p3 Stot = ge_add_quad(X, load_p3(w + 1), q);
+  const ge_p3 Sw = ge_add_quad(ge_add_quad(U, V, q), X, q);
+  ge_p3 At = ge_identity();  // the A_h are stored in cached form
+#pragma unroll 1
+  for (int hh = 0; hh < kPartQuarters; hh++) {
+    const ge_p3 c = load_p3(w + 2 * hh);
+    At = ge_add_quad(At, *reinterpret_cast<const ge_cached*>(&c), q);
+  }
+  ge_p3 T = p3_dbl_n_quad(ge_add_quad(Stot, Sw, q), __builtin_ctz(part_width(v)), q);
+  T = ge_add_quad(T, Stot, q);
+  return ge_add_quad(T, ge_neg(At), q);
+}
+
+__global__ void __launch_bounds__(4 * kPartWindows) k_part_combine_tree(PartArgs a) {
+  __shared__ ge_p3 lds[kPartWindows];
+  const int v = threadIdx.x >> 2, q = threadIdx.x & 3;
+  const int64_t b = blockIdx.x;
+  const ge_p3* ws = a.wsum + (a.blk0 + b) * kPartWsum;
+  const ge_p3 T = part_window_sum(ws, v, q);
+  if (q == 0) lds[v] = T;
+  __syncthreads();
+#pragma unroll 1
+  for (int span = 1; span < kPartWindows; span <<= 1) {
+    ge_p3 r;
+    const bool act = (v % (2 * span)) == 0;
+    if (act) r = ge_add_quad(lds[v], p3_dbl_n_quad(lds[v + span], 8 * span, q), q);
+    __syncthreads();
+    if (act && q == 0) lds[v] = r;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const ge_p3 P = lds[0];
+    store_p3(a.part + a.blk0 + b, P);
+    a.fail[a.blk0 + b] = a.fail[a.blk0 + b] | (ristretto_is_identity(P) ? 0 : 1);  // k_part_sort's bit 1
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // sum_b P_b: quads add 64 consecutive entries each, then one wave adds those.
 // ---------------------------------------------------------------------------------------
@@ -611,7 +659,10 @@ hipError_t launch_part_msm(const PartArgs& a, hipStream_t st) {
 // 8192-block chunk it was 512 waves, 0.95 ms each, 7.6 ms per 2^24 proofs.
 hipError_t launch_part_combine(const PartArgs& a, hipStream_t st) {
   if (a.nblk <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_part_combine, dim3((unsigned)((a.nblk + 15) / 16)), dim3(64), 0, st, a);
+  if (CPZ_PART_COMBINE_TREE && a.nblk <= kPartTreeMaxBlocks)
+    hipLaunchKernelGGL(k_part_combine_tree, dim3((unsigned)a.nblk), dim3(4 * kPartWindows), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_part_combine, dim3((unsigned)((a.nblk + 15) / 16)), dim3(64), 0, st, a);
   return hipGetLastError();
 }
 

@@ -115,6 +115,14 @@ constexpr int kPartListCap = kPartWindows * kPartPoints;  // sorted entries per 
 constexpr int kPartOffs = kPartWindows * (kPartBuckets + 1);
 constexpr int kPartWsum = kPartWindows * kPartQuarters * 2;  // (W, S) per window and quarter
 constexpr int kPartUnits = kPartWindows * kPartQuarters / 2;  // walk units per half (64 = lanes)
+// Combines of at most this many blocks run one workgroup per block (k_part_combine_tree).
+#ifndef CPZ_PART_COMBINE_TREE
+#define CPZ_PART_COMBINE_TREE 1
+#endif
+#ifndef CPZ_PART_TREE_MAX
+#define CPZ_PART_TREE_MAX 256
+#endif
+constexpr int64_t kPartTreeMaxBlocks = CPZ_PART_TREE_MAX;
 
 struct PartArgs {
   int64_t nblk;                  // blocks of this launch: [blk0, blk0 + nblk) of the prepared set
