@@ -569,11 +569,11 @@ int stage_inputs(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], int count
   const size_t o_off = rows, o_pres = pad16(o_off + (ctx_off ? (n + 1) * 8 : 0));
   const size_t o_ctx = pad16(o_pres + (ctx_off && ctx_present ? n : 0));
   const size_t total = pad16(o_ctx + (ctx_off ? std::max<size_t>(nbytes, 1) : 0));
+  // no copy of an earlier call may still read the block when it is rewritten or regrown
+  // (host-buffer calls return synchronised; this covers one that failed part-way)
+  if (total <= kPinStageMax) CPZ_HIP(hipStreamSynchronize(ctx->stream));
   if (total <= kPinStageMax && ctx->pin.ensure(kPinMail + total + pad16(n)) == hipSuccess &&
       ctx->in_all.ensure(total) == hipSuccess) {
-    // no copy of an earlier call may still read the block (host-buffer calls return
-    // synchronised; this covers one that failed part-way)
-    CPZ_HIP(hipStreamSynchronize(ctx->stream));
     uint8_t* h = static_cast<uint8_t*>(ctx->pin.p) + kPinMail;
     for (int k = 0; k < count; k++) std::memcpy(h + (size_t)k * n * 32, host[k], n * 32);
     if (ctx_off) {
