@@ -582,7 +582,7 @@ int stage_inputs(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], int count
       if (ctx_present) std::memcpy(h + o_pres, ctx_present, n);
       if (nbytes) std::memcpy(h + o_ctx, ctx_bytes + ctx_off[0], nbytes);
     }
-    CPZ_HIP(hipMemcpyAsync(ctx->in_all.p, h, total, hipMemcpyHostToDevice, ctx->stream));
+    if (total) CPZ_HIP(hipMemcpyAsync(ctx->in_all.p, h, total, hipMemcpyHostToDevice, ctx->stream));
     uint8_t* d = static_cast<uint8_t*>(ctx->in_all.p);
     for (int k = 0; k < count; k++) dev[k] = d + (size_t)k * n * 32;
     *dcb = ctx_off ? d + o_ctx : nullptr;
