@@ -91,21 +91,28 @@ def mad_peak_at_kernel_clock(oc, kernel="k_verify_each"):
             "sources": ["profiles/" + cr_name, "profiles/" + pr_name]}
 
 
+def _cgroup_cpu_quota():
+    """CPUs' worth of the cgroup v2 CPU quota (cpu.max 'quota period'), or None if unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else int(q) / int(p)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_threads(requested: int) -> dict:
-    """Threads for the CPU baseline: the CPUs this process may run on (sched_getaffinity),
-    capped by OMP_NUM_THREADS when the environment sets it (the GPU box's CPU share)."""
+    """Threads for the CPU baseline: every CPU this process may run on (sched_getaffinity),
+    whatever OMP_NUM_THREADS says; the cgroup quota (the box's CPU share, which bounds what
+    those threads can get) is reported beside it."""
     try:
         aff = len(os.sched_getaffinity(0))
     except AttributeError:
         aff = os.cpu_count() or 1
     omp = os.environ.get("OMP_NUM_THREADS")
-    if requested:
-        t = requested
-    elif omp and omp.isdigit():
-        t = min(aff, int(omp))
-    else:
-        t = aff
-    return {"threads": max(1, t), "affinity_cpus": aff, "omp_num_threads": omp}
+    t = requested or aff
+    return {"threads": max(1, t), "affinity_cpus": aff, "omp_num_threads": omp,
+            "cgroup_cpu_quota": _cgroup_cpu_quota()}
 
 
 def cpu_baseline(host_rows, seconds: float, threads: int):
@@ -364,6 +371,32 @@ def c5_extra(gpu, torch, dev, stream, n5, ctx_len):
     return out
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch_ranks(n: int) -> int:
+    """Run this same command as n ranks under torch.distributed.run (one process per GPU,
+    rendezvous on 127.0.0.1) in a child process and return its exit code.  Only rank 0 prints
+    the JSON line; the children's stdout/stderr are inherited, so the line reaches our stdout
+    unchanged.  The parent imports neither torch nor HIP: the GPU is touched only by the
+    ranks."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    try:
+        rc = subprocess.run(cmd, env=env).returncode
+    except KeyboardInterrupt:
+        return 130
+    return 128 - rc if rc < 0 else rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -374,7 +407,7 @@ def main():
                     help="proofs of the whole job, split over the ranks (strong scaling; configs[3] = 67108864)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="CPU baseline threads (0: the affinity CPUs, capped by OMP_NUM_THREADS if set)")
+                    help="CPU baseline threads (0: every CPU in the process's affinity set)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("each", "rlc"), default="each",
                     help="each: per-proof verification (configs[1], the headline); rlc: random-linear-"
@@ -399,6 +432,16 @@ def main():
                     help="rehearsal on a 1-GPU box: every rank uses cuda:0 (with --backend gloo); not a measurement")
     args = ap.parse_args()
     extra = lambda v: args.extras if v is None else v
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # `bench.py --gpus N` without a launcher: start one rank per GPU as a CHILD process
+        # group (torch.distributed.run), before anything here imports torch or touches HIP,
+        # relay its output and exit with its code.  Never exec.
+        sys.exit(_launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit("bench: --gpus %d but WORLD_SIZE=%s; refusing to report a line for the wrong N"
+                 % (args.gpus, env_world))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -632,6 +675,15 @@ def main():
         if cpu:
             cpu["affinity_cpus"] = th["affinity_cpus"]
             cpu["omp_num_threads"] = th["omp_num_threads"]
+            cpu["cgroup_cpu_quota"] = th["cgroup_cpu_quota"]
+            omp = th["omp_num_threads"]
+            if cpu.get("value") and omp and omp.isdigit() and 1 < int(omp) < th["threads"]:
+                # the box's per-job CPU share (OMP_NUM_THREADS) beside the all-core figure
+                sys.path.insert(0, os.path.join(ROOT, "oracle"))
+                import coracle  # CPU baseline only (test infrastructure)
+                sub = coracle.time_verify(rows, seconds=max(2.0, args.cpu_seconds / 4), threads=int(omp))
+                cpu["at_omp_threads"] = {"threads": int(omp), "value": sub.get("value"),
+                                         "verify_one_value": sub.get("verify_one_value")}
 
     if rank == 0:
         if args.mode == "each":

@@ -766,17 +766,24 @@ class BatchVerifier:
     def verify(self, rng=None, rlc_min_group: Optional[int] = None) -> List[VerifyResult]:
         """batch.rs:171-183, through the call sequence of the Rust drop-in
         (rust/reference-patch/gpu.rs; C++ mirror: include/cpz_batch.hpp): entries grouped by
-        Parameters in order of first appearance; a one-entry batch is verify_one
-        (batch.rs:178-180) and draws nothing from `rng`: its RLC check (0.65 against 1.46 ms per
-        proof, profiles/r04_small_batch.json) is keyed by a seed from os.urandom; otherwise one
-        32-byte seed from `rng` (an object with randbytes(), e.g. random.Random /
-        secrets.SystemRandom; None: os.urandom) keys every group's RLC check, groups take
-        consecutive weight indices, and a group of at least rlc_min_group entries (default
-        RLC_MIN_GROUP) runs the RLC batch check with its exact fallback (cpz_verify_batch), a
-        smaller one cpz_verify_each.  Entries
-        are `Proof` values, which may have been built with Proof(...) (Proof::new: no identity /
-        zero-s checks), so every call is equations-only: verify_one's equations alone decide
-        (batch.rs:185-231).  Either entry point returns exactly verify_one's outcome per entry."""
+        Parameters in order of first appearance; groups take consecutive weight indices, and a
+        group of at least rlc_min_group entries (default RLC_MIN_GROUP) runs the RLC batch check
+        with its exact fallback (cpz_verify_batch), a smaller one cpz_verify_each.
+
+        `rng` is drawn exactly as the reference draws it: nothing for a one-entry batch
+        (verify_one, batch.rs:178-180), otherwise one 64-byte random_scalar per entry
+        (batch.rs:239-240), whatever entry point each group takes -- so a caller that keeps
+        using a seeded rng sees the reference's stream.  The first draw's first 32 bytes key
+        the RLC weights, so `rng` must be a CSPRNG (the reference requires CryptoRngCore):
+        secrets.SystemRandom(), or None for os.urandom.  A predictable rng (random.Random)
+        would let forgeries be built whose weighted errors cancel, and is refused whenever a
+        group takes the RLC check.  A one-entry batch's RLC check (threshold lowered to 1) is
+        keyed by os.urandom.  Entries are `Proof` values, which may have been built with
+        Proof(...) (Proof::new: no identity / zero-s checks), so every call is equations-only:
+        verify_one's equations alone decide (batch.rs:185-231).  Either entry point returns
+        exactly verify_one's outcome per entry."""
+        import os
+        import random
         if not self._entries:
             raise InvalidParams("Cannot verify empty batch")
         gpu = self._gpu or _gpu()
@@ -785,8 +792,17 @@ class BatchVerifier:
         groups = {}   # insertion order = order of first appearance
         for i, e in enumerate(self._entries):
             groups.setdefault((e.params.g, e.params.h), []).append(i)
-        single = len(self._entries) == 1
+        n = len(self._entries)
+        uses_rlc = any(len(idx) >= rlc_min for idx in groups.values())
+        if uses_rlc and n > 1 and isinstance(rng, random.Random) and not isinstance(rng, random.SystemRandom):
+            raise InvalidParams("BatchVerifier.verify: the RLC weights need a cryptographic rng "
+                                "(secrets.SystemRandom() or None), not random.Random")
         seed = None
+        if n > 1:   # one random_scalar (64 bytes) per entry, batch.rs:239-240
+            draws = [(rng.randbytes(64) if rng is not None else os.urandom(64)) for _ in range(n)]
+            seed = draws[0][:32]
+        elif uses_rlc:
+            seed = os.urandom(32)
         first_index = 0
         for (g, h), idx in groups.items():
             ents = [self._entries[i] for i in idx]
@@ -794,9 +810,6 @@ class BatchVerifier:
                                   np.uint8).reshape(-1, 32) for q in ("y1", "y2", "r1", "r2", "s")]
             ctxs = [e.context for e in ents]
             if len(idx) >= rlc_min:
-                if seed is None:   # drawn once, as the reference draws its weights (batch.rs:240)
-                    import os
-                    seed = rng.randbytes(32) if (rng is not None and not single) else os.urandom(32)
                 _, _, st = gpu.verify_batch(*rows, seed, first_index=first_index, contexts=ctxs,
                                             params=Parameters(g, h), equations_only=True)
             else:

@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_prepare(RlcPrepArgs a)
 // decode per lane instead of four in sequence (on one lane per proof the prepare took 0.28 -
 // 0.37 ms at n = 1 .. 1000, a latency, with most of the chip idle).  The weights' ChaCha20
 // block is recomputed by each of the four lanes.  A block is 64 proofs: its a s and b s sums
-// go to quarter_sums, and k_rlc_bsum4 adds each 256-proof block's four into block_sums.
+// go to quarter_sums, and k_rlc_bsum4 adds each 128-proof block's two into block_sums.
 __global__ void __launch_bounds__(256, 2) k_rlc_prepare4(RlcPrepArgs a) {
   __shared__ sc red_a[64];
   __shared__ sc red_b[64];

@@ -140,7 +140,7 @@ bool is_no_partial(const uint8_t p[32]) {
 // RLC buffers come in two sets with their own capacities, and an MSM's arguments are derived
 // from the sets it is handed, never from a context-wide size (rlc_msm_args):
 //   RlcPrepared  the batch's prepared MSM input: 4 n + 2 negated Niels points, the digit rows
-//                [16][dstride], per-256-proof block sums.  Capacity: proofs of the batch.
+//                [16][dstride], per-128-proof block sums (kRlcSumBlock).  Capacity: proofs of the batch.
 //   RlcMsmSet    sort / bucket / reduction buffers of ONE MSM, its partial and identity flag.
 //                Capacity: proofs of one MSM (a span of at most CPZ_RLC_SPAN proofs).
 struct RlcPrepared {
@@ -1031,13 +1031,13 @@ int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* stat
 }
 
 // Blocks per launch of the partitioned MSM's sort and walk: 2^24 proofs, ~4.8 GB of lists and
-// offsets (~72 KB per 256-proof block); the window sums, 40 KB per block, are kept for the whole
+// offsets (~41 KB per 128-proof block); the window sums, 40 KB per block, are kept for the whole
 // batch so that one combine launch covers every block.  Per 8192 blocks the launch tails cost C5
 // 5 ms (227.9 / 229.5 ms against 223.7 / 223.6 at 65536, 224.6 / 224.9 at 32768; A/B, one call).
 constexpr int64_t kPartChunkBlocks = (int64_t(1) << 24) / cpz::kPartProofs;
 // Density probe outcomes (invalid entries among the kProbeChunks x 256 sampled) for which the
 // partitioned check pays.  Relative to per-proof verification its prepare costs ~0.19, its
-// block partials ~0.32 (256-proof blocks) or ~0.36 (128), the locate pass ~0.5 per failing
+// block partials ~0.32 (blocks of 256 proofs) or ~0.36 (128), the locate pass ~0.5 per failing
 // fraction, and the per-proof pass over a block holding two or more forgeries ~0.83 (no
 // decodes); a block of B proofs is clean with probability (1 - rho)^B.  At B = 128 it pays up
 // to rho ~ 0.65 % (~27 sampled; ~0.6 % without the locate pass), at 256 up to ~0.35 % (~14);
@@ -1262,9 +1262,10 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
   // density, beside the batch's challenges (the probe's ~0.5 ms of per-proof latency hides under
   // them).  Two or more invalid entries among the kProbeChunks x 256 sampled: the batch
   // cannot pass and bisection cannot prune it (every range of a few thousand proofs fails).
-  //   * up to kPartMaxProbeBad sampled (density up to ~0.3 %, configs[4]'s 0.1 %): the
-  //     partitioned check -- prepare, every 256-proof block's partial in one pass, per-proof
-  //     verification of the failing blocks only; partial_out is the batch's partial.
+  //   * up to kPartMaxProbeBad = 20 sampled (density up to ~0.5 %, configs[4]'s 0.1 %): the
+  //     partitioned check -- prepare, every 128-proof block's partial in one pass, the failing
+  //     blocks' index-weighted partials (part_locate), per-proof verification of the located
+  //     entries and of the blocks holding more; partial_out is the batch's partial.
   //   * denser: nothing is prepared, every entry is verified per proof (k_verify_each on the
   //     challenges just computed), and partial_out is 32 x 0xff ("no partial": not an
   //     encoding) -- the cost of the per-proof path plus the probe.

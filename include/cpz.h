@@ -188,12 +188,19 @@ int cpz_prove_synthetic_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t 
  *                With a fallback, a batch of >= 2^20 entries (with or without contexts) is
  *                first sampled (4096 entries verified per proof, beside the batch's challenges):
  *                if two or more sampled entries are invalid the batch cannot pass and
- *                bisection could not prune it.  Up to 12 sampled invalid entries (density
- *                up to ~0.3 %): the partitioned check -- every 256-proof block's own RLC
- *                partial, per-proof verification of the failing blocks only; partial_out
- *                is the batch's partial as usual.  More: nothing is prepared, every entry
- *                is verified per proof, batch_ok = 0 and partial_out is 32 bytes of 0xff
- *                (not an encoding: "no partial computed").
+ *                bisection could not prune it.  2 to 20 sampled invalid entries (density
+ *                up to ~0.5 %): the partitioned check -- every 128-proof block's own RLC
+ *                partial, then for the failing blocks an index-weighted second partial that
+ *                locates a block's single invalid entry, per-proof verification of the
+ *                located entries and of the blocks holding more; partial_out is the batch's
+ *                partial as usual.  More: nothing is prepared, every entry is verified per
+ *                proof, batch_ok = 0 and partial_out is 32 bytes of 0xff (not an encoding:
+ *                "no partial computed").
+ *   seed         must be secret and unpredictable to whoever produced the proofs (a CSPRNG
+ *                draw per call, as the reference's random_scalar(rng) is, batch.rs:240): the
+ *                weights' 2^-128 bound per forged entry, and the locate pass's ~2^-121 per
+ *                failing block (CPZ_FALLBACK_STATS out[7]), hold only for weights the prover
+ *                could not predict.  A seed an adversary knows lets forgeries cancel.
  * The _device form takes device-resident inputs and always needs d_status_out (decode-level
  * statuses, or exact ones when fallback != 0); it synchronises `stream`. */
 int cpz_verify_batch(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[32], size_t n,
@@ -228,7 +235,9 @@ int cpz_verify_batch_device(cpz_ctx *ctx, const uint8_t g[32], const uint8_t h[3
  *   out[5]  sub-range MSMs the bisection ran
  *   out[6]  failing blocks whose index-weighted partial the locate pass computed
  *   out[7]  of those, blocks whose one invalid entry it located (verified alone; the rest of
- *           such a block is accepted on P'_b = [j] P_b, error <= ~2^-121 per block) */
+ *           such a block is accepted on P'_b = [j] P_b, error <= ~2^-121 per block for a seed
+ *           the proofs' author could not predict -- see `seed` above; with a known seed an
+ *           adversary could place two related forgeries in one block that pass as one) */
 #define CPZ_FALLBACK_STATS 8
 #define CPZ_FALLBACK_NONE 0
 #define CPZ_FALLBACK_BISECTION 1

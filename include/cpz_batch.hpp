@@ -24,8 +24,9 @@
 //
 // BatchVerifier::verify issues exactly the call sequence of the Rust drop-in
 // (rust/reference-patch/gpu.rs): entries grouped by Parameters in order of first appearance;
-// a one-entry batch -> cpz_verify_each_ex (batch.rs:178-180, the rng untouched); otherwise a
-// 32-byte seed drawn once from the caller's rng keys every group's RLC check, groups take
+// a one-entry batch -> cpz_verify_each_ex (batch.rs:178-180, the rng untouched); otherwise
+// 64 bytes per entry are drawn from the caller's rng, as the reference's random_scalar draws
+// them (batch.rs:239-240), the first 32 keying every group's RLC check; groups take
 // consecutive weight indices (first_index), and a group of at least rlc_min_group entries runs
 // cpz_verify_batch_ex (RLC + exact fallback), a smaller one cpz_verify_each_ex.
 #pragma once
@@ -315,12 +316,23 @@ class BatchVerifier {
       if (k == groups.size()) groups.push_back({entries_[i].params, {}});
       groups[k].second.push_back(i);
     }
-    // batch.rs:178-180: a one-entry batch is verify_one and draws nothing from the caller's rng;
-    // its RLC check (0.65 against 1.46 ms per proof, profiles/r04_small_batch.json) is keyed by
-    // a seed from the OS entropy source.
+    // The caller's rng is drawn exactly as the reference draws it, so a caller that keeps using a
+    // seeded rng after verify sees the reference's stream: a one-entry batch is verify_one and
+    // draws nothing (batch.rs:178-180; its RLC check, when the threshold is lowered to 1, is keyed
+    // by a seed from the OS entropy source); a batch of n >= 2 draws one random_scalar, 64 bytes,
+    // per entry (batch.rs:239-240, ristretto.rs:146-150), whatever entry point each group takes.
+    // The first 32 bytes of the first draw key every group's RLC weights.
     const bool single = entries_.size() == 1;
     Bytes32 seed{};
-    bool have_seed = false;
+    if (single) {
+      if (entries_.size() >= rlc_min_group_) os_rng(seed.data(), seed.size());
+    } else {
+      uint8_t draw[64];
+      for (std::size_t i = 0; i < entries_.size(); i++) {
+        rng(draw, sizeof(draw));
+        if (i == 0) std::memcpy(seed.data(), draw, seed.size());
+      }
+    }
     uint64_t first_index = 0;
     for (const auto& grp : groups) {
       const auto& idx = grp.second;
@@ -352,11 +364,6 @@ class BatchVerifier {
       d.first_index = first_index;
       int rc;
       if (n >= rlc_min_group_) {
-        if (!have_seed) {  // drawn once per verify, as the reference draws its weights (batch.rs:240)
-          if (single) os_rng(seed.data(), seed.size());
-          else rng(seed.data(), seed.size());
-          have_seed = true;
-        }
         d.rlc = true;
         d.seed = seed;
         rc = cpz_verify_batch_ex(dev_->get(), CPZ_CALL_EQUATIONS_ONLY, p.g.data(), p.h.data(), n, y1.data(), y2.data(),

@@ -22,9 +22,12 @@ use crate::Result;
 impl BatchVerifier {
     /// Verifies all proofs in the batch (batch.rs:171-183): `Err` for an empty batch,
     /// otherwise one `Result` per entry in entry order.  With the `gpu` feature the
-    /// verification runs on the MI355X (gpu.rs: `verify_one` for n == 1; for n >= 2 a
-    /// random-linear-combination check keyed by 32 bytes drawn from `rng`, with an exact
-    /// per-entry fallback); the per-entry results are those of `verify_one`.
+    /// verification runs on the MI355X (gpu.rs: every `Parameters` group of this API's
+    /// batches, at most 1000 entries, is verified per proof, `verify_one` on eight GPU lanes
+    /// per entry; a group of at least RLC_MIN_GROUP entries would take the
+    /// random-linear-combination check keyed by `rng`, with an exact per-entry fallback);
+    /// the per-entry results are those of `verify_one`, and `rng` is drawn as the reference
+    /// draws it (64 bytes per entry for n >= 2, nothing for n == 1).
     pub fn verify<R: CryptoRngCore>(&self, rng: &mut R) -> Result<Vec<Result<()>>> {
         #[cfg(feature = "gpu")]
         {

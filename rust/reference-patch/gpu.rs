@@ -12,12 +12,16 @@
 //!     most 1000 entries), from the measured latencies -- runs cpz_verify_each: `verify_one`
 //!     per entry (batch.rs:185-231), eight GPU lanes per proof;
 //!   * a larger group takes the random-linear-combination check (cpz_verify_batch: the batch
-//!     equation with the weights on every term, one Pippenger MSM), keyed by a 32-byte seed
-//!     drawn once from `rng` (the reference draws its weights from it, batch.rs:240) -- or,
-//!     for a one-entry batch, which the reference verifies with `verify_one` without touching
-//!     `rng` (batch.rs:178-180), from the OS (`OsRng`); a failing check runs the fallback
-//!     search, which returns exactly `verify_one`'s outcome per entry (verify_individually,
-//!     batch.rs:262-268, 314-318).  Groups take consecutive weight indices (`first_index`).
+//!     equation with the weights on every term, one Pippenger MSM), keyed by the first 32
+//!     bytes `rng` yields -- or, for a one-entry batch, which the reference verifies with
+//!     `verify_one` without touching `rng` (batch.rs:178-180), by 32 bytes from the OS
+//!     (`OsRng`); a failing check runs the fallback search, which returns exactly
+//!     `verify_one`'s outcome per entry (verify_individually, batch.rs:262-268, 314-318).
+//!     Groups take consecutive weight indices (`first_index`).
+//! `rng` is drawn exactly as the reference draws it, whatever entry point each group takes:
+//! nothing for n == 1, one `random_scalar` -- 64 bytes, one `fill_bytes` call -- per entry for
+//! n >= 2 (batch.rs:239-240, ristretto.rs:146-150), so a caller that keeps using a seeded rng
+//! after `verify` sees the same stream as with the reference.
 //! Every call passes EQUATIONS_ONLY: a `Proof` may have been built with `Proof::new` (no
 //! identity / zero-s checks, gadgets.rs:252, 278, 317), and `verify_one` judges it by the
 //! two equations alone -- so the result vector is the reference's for every batch, not only
@@ -85,6 +89,9 @@ impl Pool {
     }
 }
 
+/// Contexts on every visible GPU that opens; a device whose context fails to open is skipped
+/// (its error kept for the message), so one bad GPU does not take `verify` down on the healthy
+/// ones.  Fails only when no context opens at all.
 fn pool() -> Result<&'static Pool> {
     static POOL: OnceLock<std::result::Result<Pool, String>> = OnceLock::new();
     POOL.get_or_init(|| {
@@ -93,10 +100,17 @@ fn pool() -> Result<&'static Pool> {
             return Err("no GPU visible to the HIP runtime".to_string());
         }
         let mut slots = Vec::with_capacity(devices * CONTEXTS_PER_DEVICE);
+        let mut last_err = String::new();
         for _ in 0..CONTEXTS_PER_DEVICE {
             for d in 0..devices {
-                slots.push(Mutex::new(Gpu::new(d).map_err(|e| e.to_string())?));
+                match Gpu::new(d) {
+                    Ok(g) => slots.push(Mutex::new(g)),
+                    Err(e) => last_err = format!("GPU {d}: {e}"),
+                }
             }
+        }
+        if slots.is_empty() {
+            return Err(format!("no verifier context could be opened ({last_err})"));
         }
         Ok(Pool { slots, next: AtomicUsize::new(0) })
     })
@@ -182,7 +196,19 @@ pub(super) fn verify<R: CryptoRngCore + ?Sized>(batch: &BatchVerifier, rng: &mut
         }
     }
     let mut out: Vec<Option<Result<()>>> = (0..entries.len()).map(|_| None).collect();
-    let mut seed: Option<[u8; 32]> = None;
+    // The reference's consumption of `rng` (batch.rs:178-180, 239-240), before any GPU work.
+    let mut seed = [0u8; 32];
+    if entries.len() == 1 {
+        OsRng.fill_bytes(&mut seed); // verify_one draws nothing from the caller's rng
+    } else {
+        let mut draw = [0u8; 64];
+        for i in 0..entries.len() {
+            rng.fill_bytes(&mut draw); // one random_scalar per entry
+            if i == 0 {
+                seed.copy_from_slice(&draw[..32]);
+            }
+        }
+    }
     let mut first_index = 0u64;
     for grp in &groups {
         let rows = group_rows(entries, &grp.idx);
@@ -190,17 +216,8 @@ pub(super) fn verify<R: CryptoRngCore + ?Sized>(batch: &BatchVerifier, rng: &mut
         let status = if rows.len() < RLC_MIN_GROUP {
             gpu.verify_each_with(EQUATIONS_ONLY, g, h, &rows).map_err(|e| Error::InvalidParams(e.to_string()))?
         } else {
-            let seed = seed.get_or_insert_with(|| {
-                let mut s = [0u8; 32];
-                if entries.len() == 1 {
-                    OsRng.fill_bytes(&mut s); // verify_one draws nothing from the caller's rng
-                } else {
-                    rng.fill_bytes(&mut s);
-                }
-                s
-            });
             let (_partial, _ok, st) = gpu
-                .verify_batch_with(EQUATIONS_ONLY, g, h, &rows, seed, first_index)
+                .verify_batch_with(EQUATIONS_ONLY, g, h, &rows, &seed, first_index)
                 .map_err(|e| Error::InvalidParams(e.to_string()))?;
             st
         };

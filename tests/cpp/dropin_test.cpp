@@ -1,6 +1,6 @@
 // The drop-in's call sequence through the C++ mirror: BatchVerifier::verify (include/cpz_batch.hpp)
 // issues what rust/reference-patch/gpu.rs issues -- Parameters groups in order of first
-// appearance, one seed from the caller's rng, consecutive first_index, CPZ_CALL_EQUATIONS_ONLY,
+// appearance, 64 bytes per entry from the caller's rng (the first 32 the seed), consecutive first_index, CPZ_CALL_EQUATIONS_ONLY,
 // cpz_verify_batch_ex for groups of at least rlc_min_group entries and cpz_verify_each_ex
 // otherwise.  Driven by tests/test_gpu_dropin.py:
 //   dropin_test <input> <output>
@@ -79,8 +79,10 @@ int main(int argc, char** argv) {
   }
   std::fclose(f);
   int draws = 0;
-  auto rng = [&](uint8_t* out, std::size_t len) {  // yields the given seed (once per verify)
+  std::size_t drawn = 0;
+  auto rng = [&](uint8_t* out, std::size_t len) {  // yields the given seed, repeated
     draws++;
+    drawn += len;
     for (std::size_t k = 0; k < len; k++) out[k] = seed[k % 32];
   };
   Result overall;
@@ -96,7 +98,7 @@ int main(int argc, char** argv) {
   for (const auto& d : log)
     std::fprintf(o, "dispatch %d %zu %llu %d %s %s\n", d.rlc ? 1 : 0, d.entries, (unsigned long long)d.first_index,
                  d.batch_ok, hex(d.seed).c_str(), hex(d.partial).c_str());
-  std::fprintf(o, "rng_draws %d\n", draws);
+  std::fprintf(o, "rng_draws %d %zu\n", draws, drawn);
   std::fclose(o);
   return 0;
 }

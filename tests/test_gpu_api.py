@@ -288,6 +288,43 @@ def test_commitment_checks_off_equals_verify_one_on_constructed_proofs(gpu):
         cp.Proof.from_bytes(cp.Proof(s0.r1, s0.r2, s0.s).to_bytes(), gpu)
 
 
+def test_batch_verifier_rng_consumption_and_csprng(gpu):
+    """The mirror draws `rng` as the reference does (batch.rs:178-180, 239-240): nothing for
+    one entry, one 64-byte random_scalar per entry otherwise, whatever entry point runs; a
+    predictable random.Random is refused when the RLC check would be keyed by it."""
+    import random
+    import secrets
+
+    class Counting:
+        def __init__(self):
+            self.calls = []
+            self._r = secrets.SystemRandom()
+
+        def randbytes(self, k):
+            self.calls.append(k)
+            return self._r.randbytes(k)
+
+    params = cp.Parameters()
+    recs = [O.prove(O.bench_scalar(b"x", i), 11 + i) for i in range(5)]
+    for n in (1, 2, 5):
+        for rlc_min in (1, cp.RLC_MIN_GROUP):
+            b = cp.BatchVerifier(gpu)
+            for r in recs[:n]:
+                b.add(params, cp.Statement(r.y1, r.y2), cp.Proof(r.r1, r.r2, r.s))
+            rng = Counting()
+            res = b.verify(rng, rlc_min_group=rlc_min)
+            assert all(v.is_ok() for v in res)
+            assert rng.calls == ([64] * n if n > 1 else [])
+    b = cp.BatchVerifier(gpu)
+    for r in recs[:3]:
+        b.add(params, cp.Statement(r.y1, r.y2), cp.Proof(r.r1, r.r2, r.s))
+    with pytest.raises(cp.InvalidParams, match="cryptographic rng"):
+        b.verify(random.Random(5), rlc_min_group=1)
+    # the per-proof path does not key anything by the rng: a seeded rng is accepted there
+    assert all(v.is_ok() for v in b.verify(random.Random(5)))
+    assert all(v.is_ok() for v in b.verify(secrets.SystemRandom(), rlc_min_group=1))
+
+
 def test_add_time_statement_validation_and_capacity(gpu, golden):
     """batch.rs:158 (statement.validate() in add_with_context) and batch.rs:113-118."""
     b = cp.BatchVerifier.with_capacity(5000, gpu)

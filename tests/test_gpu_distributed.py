@@ -148,18 +148,24 @@ def test_two_ranks_dense_shard_marker_combines(gpu):
     assert not ok0 and ok1 and exact0 and exact1
 
 
-def test_bench_rlc_four_rank_rehearsal():
+@pytest.mark.parametrize("launcher", ["torchrun", "none"])
+def test_bench_rlc_four_rank_rehearsal(launcher):
     """bench.py's multi-rank RLC path (configs[3]'s flow: per-rank shard partials keyed by the
     global index, all-gather, combine) as a world-4 gloo rehearsal on the box's one GPU: the
-    combined total of a valid set is the identity, and the line reports no rate."""
+    combined total of a valid set is the identity, and the line reports no rate.  launcher =
+    "none" is the driver's own form, plain `python3 bench.py --gpus 4`: bench.py starts the four
+    ranks itself (torch.distributed.run as a child process) and relays rank 0's line."""
     import json
     import subprocess
-    port = _free_port()
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", "4", "--mode", "rlc", "--n-total", str(1 << 20), "--same-device", "--backend", "gloo",
-           "--steps", "1", "--warmup", "1", "--extras", "0", "--no-cpu-baseline"]
+    env.pop("WORLD_SIZE", None)
+    args = ["--gpus", "4", "--mode", "rlc", "--n-total", str(1 << 20), "--same-device", "--backend", "gloo",
+            "--steps", "1", "--warmup", "1", "--extras", "0", "--no-cpu-baseline"]
+    if launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py")] + args
+    else:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + args
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=360, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]

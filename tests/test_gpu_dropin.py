@@ -6,7 +6,9 @@ the call sequence rust/reference-patch/gpu.rs issues, exercised through its C++ 
     the default generators and the golden custom pair);
   * a one-entry batch (verify_one, batch.rs:178-180) leaves the rng untouched: its RLC check
     is keyed by a seed from the OS entropy source;
-  * otherwise one 32-byte seed drawn from the caller's rng keys every group's RLC check,
+  * otherwise the rng is drawn as the reference draws it, one 64-byte random_scalar per entry
+    (batch.rs:239-240), whatever entry point each group takes; the first draw's first 32
+    bytes key every group's RLC check,
     groups take consecutive weight indices (first_index = entries of the earlier groups),
     groups of >= rlc_min_group entries run cpz_verify_batch_ex, smaller ones
     cpz_verify_each_ex; every call passes CPZ_CALL_EQUATIONS_ONLY (Proof values).
@@ -92,7 +94,7 @@ def _run_mirror(tmp_path, params, groups, rows, ctxs, rlc_min):
     inp.write_bytes(bytes(blob))
     r = subprocess.run([exe, str(inp), str(outp)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    st, disp, draws = {}, [], None
+    st, disp, draws = {}, [], (None, None)
     for line in outp.read_text().splitlines():
         f = line.split()
         if f[0] == "status":
@@ -101,7 +103,7 @@ def _run_mirror(tmp_path, params, groups, rows, ctxs, rlc_min):
             disp.append({"rlc": f[1] == "1", "entries": int(f[2]), "first_index": int(f[3]), "batch_ok": f[4] == "1",
                          "seed": bytes.fromhex(f[5]), "partial": bytes.fromhex(f[6])})
         elif f[0] == "rng_draws":
-            draws = int(f[1])
+            draws = (int(f[1]), int(f[2]))
     return np.array([st[i] for i in range(n)], np.uint8), disp, draws
 
 
@@ -155,4 +157,5 @@ def test_dropin_call_sequence_matches_verify_one(gpu, golden, tmp_path, n, rlc_m
             assert d["partial"] == part, (g, len(idx))
             assert d["batch_ok"] == all(exp[i] == 0 for i in idx)
         fi += len(idx)
-    assert draws == (1 if n > 1 and any(d["rlc"] for d in disp) else 0)
+    # the reference's consumption of rng: n calls of 64 bytes for n >= 2, nothing for n == 1
+    assert draws == ((n, 64 * n) if n > 1 else (0, 0))

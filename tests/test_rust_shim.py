@@ -132,12 +132,15 @@ def test_patch_serves_verify_with_the_reference_signature():
 
 def test_patch_draws_the_seed_from_rng_and_uses_the_batch_check():
     g = _code("rust/reference-patch/gpu.rs")
-    assert "rng.fill_bytes(&mut s)" in g                  # weights keyed by rng (batch.rs:240)
+    # rng drawn as the reference draws it: one 64-byte random_scalar per entry for n >= 2
+    # (batch.rs:239-240), the first 32 bytes keying the weights
+    assert "let mut draw = [0u8; 64];" in g and "for i in 0..entries.len() {" in g
+    assert "rng.fill_bytes(&mut draw);" in g and "seed.copy_from_slice(&draw[..32]);" in g
     assert "gpu.verify_each_with(EQUATIONS_ONLY," in g   # Proof::new entries: equations only, per call
     assert ".verify_batch_with(EQUATIONS_ONLY," in g
     assert "set_commitment_checks" not in g              # never the shared context mode
     assert "if rows.len() < RLC_MIN_GROUP {" in g
-    assert "if entries.len() == 1 {" in g and "OsRng.fill_bytes(&mut s)" in g   # n == 1: rng untouched
+    assert "if entries.len() == 1 {" in g and "OsRng.fill_bytes(&mut seed)" in g   # n == 1: rng untouched
     assert "first_index += rows.len() as u64;" in g      # consecutive weight indices, every group
 
 
