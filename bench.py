@@ -76,6 +76,9 @@ def mad_peak_at_kernel_clock(oc, kernel="k_verify_each"):
     cr_name, cr = _newest_profile("_clock_rates.json")
     if kernel == "k_verify_each":
         pr_name, pr = _newest_profile("_verify_clock_probe.json")
+    elif kernel == "k_part_acc":
+        pr_name, pr = _newest_profile("_c5_clock_probe.json")
+        pr = pr.get(kernel) or {}
     else:
         pr_name, pr = _newest_profile("_rlc_clock_probe.json")
         pr = pr.get(kernel) or {}
@@ -296,6 +299,119 @@ def small_batch_table(gpu=None, sizes=SMALL_SIZES, stages=False, cpu=True):
     return out
 
 
+PAIR_COUNTS = (1, 8, 64)
+
+
+def custom_pairs_table(gpu, n=1000, counts=PAIR_COUNTS, cpu=True):
+    """BatchVerifier batches whose entries carry their own Parameters (batch.rs:52,
+    gadgets.rs:77-103): n entries spread over k distinct (g, h) pairs, verified through the
+    drop-in's call sequence (the Python mirror of gpu.rs: one per-proof call per Parameters
+    group, equations only).  A pair without cached combs is verified from its Niels tables
+    (variable bases, stage 13) instead of building 128 MiB of combs per pair.  cold: a fresh
+    context (every pair's tables built inside the call); warm: the same batch again (tables
+    cached, a service reusing its pairs).  CPU: the C oracle's BatchVerifier::verify per group
+    under that group's generators, one thread."""
+    import hashlib
+
+    import numpy as np
+
+    import chaum_pedersen as cp
+    out = {"n": n, "unit": "ms per BatchVerifier::verify (median of synchronous calls)", "rows": []}
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import coracle  # CPU baseline only (test infrastructure)
+    base = gpu.prove_synthetic(n, SEED_X, SEED_K)   # x, k: reuse the synthetic witnesses per pair below
+    for k in counts:
+        pairs = []
+        for j in range(k):
+            # [a] B, [b] B as encodings: prove with x = a gives y1 = [a] g (default g = B)
+            a = hashlib.sha512(b"bench-pair-g-%d" % j).digest()[:31] + b"\0"
+            b2 = hashlib.sha512(b"bench-pair-h-%d" % j).digest()[:31] + b"\0"
+            o = gpu.prove([a, b2], [a, b2])
+            pairs.append(cp.Parameters(o["y1"][0].tobytes(), o["y1"][1].tobytes()))
+        groups = np.arange(n) % k
+        rows = {q: np.zeros((n, 32), np.uint8) for q in ("y1", "y2", "r1", "r2", "s")}
+        for j in range(k):
+            idx = np.nonzero(groups == j)[0]
+            xs = [hashlib.sha256(b"bx%d" % i).digest() for i in idx]
+            ks = [hashlib.sha256(b"bk%d" % i).digest() for i in idx]
+            o = gpu.prove(xs, ks, params=pairs[j])
+            for q in rows:
+                rows[q][idx] = o[q]
+        fresh = cp.Gpu(gpu.device if hasattr(gpu, "device") else 0)
+        b = cp.BatchVerifier(fresh)
+        for i in range(n):
+            b.add(pairs[int(groups[i])], cp.Statement(rows["y1"][i].tobytes(), rows["y2"][i].tobytes()),
+                  cp.Proof(rows["r1"][i].tobytes(), rows["r2"][i].tobytes(), rows["s"][i].tobytes()))
+        fresh.set_timing(True)
+        fresh.stage_times()
+        t0 = time.perf_counter()
+        res = b.verify()
+        cold = (time.perf_counter() - t0) * 1e3
+        st = fresh.stage_times()
+        fresh.set_timing(False)
+        if any(not r.is_ok() for r in res):
+            raise SystemExit("bench: custom-pair batch rejected a valid proof")
+        warm, calls = _median_call_ms(lambda: b.verify(), budget_s=0.5, min_calls=3)
+        r = {"pairs": k, "cold_ms": cold, "warm_ms": warm, "calls": calls,
+             "varbase_table_builds": st.get("generators_varbase", (0.0, 0))[1],
+             "comb_builds": st.get("generators", (0.0, 0))[1],
+             "varbase_build_ms": st.get("generators_varbase", (0.0, 0))[0]}
+        fresh.close()
+        if cpu:
+            def cpu_run():
+                for j in range(k):
+                    idx = np.nonzero(groups == j)[0]
+                    sub = {q: np.ascontiguousarray(rows[q][idx]) for q in rows}
+                    coracle.reference_batch_verify(sub, 0, len(idx), g=pairs[j].g, h=pairs[j].h)
+            r["cpu_batch_verifier_ms"], _ = _median_call_ms(cpu_run, budget_s=0.5, min_calls=2)
+            r["gpu_over_cpu_speedup_cold"] = r["cpu_batch_verifier_ms"] / cold
+            r["gpu_over_cpu_speedup_warm"] = r["cpu_batch_verifier_ms"] / warm
+        out["rows"].append(r)
+    return out
+
+
+def c5_roofline(ms, n5, oc):
+    """configs[4]'s dominant kernels on the headline's basis: k_part_acc (every 128-proof
+    block's bucket walk, stage 14) by its algorithmic MADs per block -- entries x 7 M + bucket
+    boundaries x 9 M (bench/opcount.json "part": host-counted step costs, entries simulated by
+    tools/part_entries.py) -- and k_rlc_prepare by its MADs per proof, each against the v_mad
+    issue rate x 1024 SIMDs x that kernel's own probed shader clock."""
+    part = oc.get("part", {})
+    out = {"unit": "Tmad/s"}
+
+    def priced(kernel, achieved, **extra):
+        kc = mad_peak_at_kernel_clock(oc, kernel)
+        r = dict(extra, achieved=achieved)
+        if kc:
+            pk = kc["peak"] / 1e12
+            r.update(peak=pk, frac=achieved / pk, peak_clock_ghz=kc["clock_ghz"], peak_sources=kc["sources"],
+                     peak_basis="v_mad_i64_i32 %.2f lanes / SIMD cycle x 1024 SIMDs x %s's own shader clock %.3f GHz"
+                                % (kc["lanes_per_simd_cycle"], kernel, kc["clock_ghz"]))
+        else:
+            r.update(peak=None, frac=None, peak_basis="unpriced: no in-kernel clock probe of %s under profiles/" % kernel)
+        return r
+
+    blocks = (n5 + 127) // 128
+    t = ms.get("part_acc")
+    if t and part:
+        a = part["algorithmic_mads_per_block"] * blocks / (t * 1e-3) / 1e12
+        out["k_part_acc"] = priced(
+            "k_part_acc", a, blocks=blocks, kernel_ms=t, algorithmic_mads_per_block=part["algorithmic_mads_per_block"],
+            executed_mads_per_block=part["executed_mads_per_block"],
+            executed_tmad_s=part["executed_mads_per_block"] * blocks / (t * 1e-3) / 1e12,
+            non_algorithmic_share=part["non_algorithmic_share"],
+            basis="%d entries x 7 M + %d boundaries x 9 M per block (the kernel executes 9 M per step)"
+                  % (part["entries_per_block"], part["boundaries_per_block"]))
+    prep = oc.get("rlc", {}).get("prepare_per_proof", {}).get("mads")
+    t = ms.get("rlc_prepare")
+    if t and prep:
+        out["k_rlc_prepare"] = priced("k_rlc_prepare", prep * n5 / (t * 1e-3) / 1e12, kernel_ms=t, mads_per_proof=prep)
+    if ms.get("part_acc_locate"):
+        out["k_part_acc_locate_ms"] = ms["part_acc_locate"]
+    return out
+
+
 def c5_extra(gpu, torch, dev, stream, n5, ctx_len):
     """configs[4]: n5 proofs, 0.1 % forged, through the batch check + fallback -> the exact
     invalid set, timed against cpz_verify_each of the same batch.  ctx_len = 32: every proof
@@ -350,6 +466,7 @@ def c5_extra(gpu, torch, dev, stream, n5, ctx_len):
     if not np.array_equal(pp, got):
         raise SystemExit("bench: C5 per-proof statuses differ from the fallback's")
     ms = {k: v[0] for k, v in c_st.items()}
+    roof = c5_roofline(ms, n5, oc=_load_json("bench/opcount.json") or {})
     out = {"workload": "configs[4]: %d proofs%s, %d forged (half s+1, half %s), RLC batch check + fallback "
                        "(density probe beside the challenges; at this density the partitioned check: every "
                        "128-proof block's RLC partial, the failing blocks' index-weighted partials locating a "
@@ -358,8 +475,11 @@ def c5_extra(gpu, torch, dev, stream, n5, ctx_len):
                                               "a replayed context" if ctx_len else "wrong y1"),
            "proofs": n5, "forged": nf, "ms": c_el * 1e3, "proofs_per_s": n5 / c_el, "exact_set": True,
            "phase_ms": {"challenge": ms.get("challenge", 0.0), "rlc_prepare": ms.get("rlc_prepare", 0.0),
-                        "rlc_msm": ms.get("rlc_msm", 0.0), "fallback_per_proof": ms.get("fallback", 0.0)},
+                        "rlc_msm": ms.get("rlc_msm", 0.0), "part_acc": ms.get("part_acc", 0.0),
+                        "part_acc_locate": ms.get("part_acc_locate", 0.0),
+                        "fallback_per_proof": ms.get("fallback", 0.0)},
            "fallback": c_fb,
+           "roofline": roof,
            "per_proof_only_ms": p_el * 1e3,
            "ratio_to_per_proof": c_el / p_el,
            "partial": partial.hex(),
@@ -606,9 +726,10 @@ def main():
                     "proofs_per_s": n * steps_h / h_el, "ms_per_call": h_el * 1e3 / steps_h, "calls": steps_h}
         del hrows
 
-    small = None
+    small = pairs_tab = None
     if args.mode == "each" and solo and extra(args.small_batch):
         small = small_batch_table(gpu, cpu=not args.no_cpu_baseline)
+        pairs_tab = custom_pairs_table(gpu, cpu=not args.no_cpu_baseline)
 
     value = total_proofs * args.steps / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
@@ -729,6 +850,8 @@ def main():
             line["host_e2e"] = host_e2e
         if small:
             line["small_batch"] = small
+        if pairs_tab:
+            line["custom_pairs"] = pairs_tab
         if args.same_device:
             # several ranks on one GPU: a correctness rehearsal of the multi-rank path, not a
             # measurement -- no rate is reported

@@ -329,7 +329,8 @@ class Gpu:
 
     # -- per-kernel timing (HIP events on the launch stream) -------------------------------
     STAGES = ("challenge", "verify_each", "rlc_prepare", "rlc_msm", "fallback", "verify_span", "prove", "generators",
-              "rlc_sort", "rlc_bucket", "rlc_bucket_fix", "rlc_reduce", "rlc_final", "s13", "s14", "s15")
+              "rlc_sort", "rlc_bucket", "rlc_bucket_fix", "rlc_reduce", "rlc_final", "generators_varbase", "part_acc",
+              "part_acc_locate")
 
     def set_timing(self, enable: bool) -> None:
         _native.check(self._lib.cpz_ctx_set_timing(self._h, 1 if enable else 0))

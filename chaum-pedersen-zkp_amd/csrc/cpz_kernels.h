@@ -103,6 +103,14 @@ struct ProbeGatherArgs {
 #endif
 constexpr int64_t kQuadVerifyMax = CPZ_QUAD_MAX;
 constexpr int kQuadTableInts = 2 * 9 * 40;  // per quad: two tables of 9 entries of 4 x 10 limbs
+// Per-proof calls of at most this many proofs whose (g, h) has no comb in the context's cache
+// verify against the pair's 128-entry Niels tables (VerifyArgs::vtab) instead of building the
+// 128 MiB combs (~3 ms): [s'] B by radix-256 digits inside the Straus loop, +16 additions per
+// equation against the comb's 16.  The default pair always gets its comb.
+constexpr int64_t kVarBaseMax = kQuadVerifyMax;
+// k_verify_quad phase stamps (CPZ_CLOCK_PROBE): start, split + digits, decode, tables, Straus,
+// comb, verdict; then the 100 MHz clock at start and end.
+constexpr int kQuadPhases = 9;
 constexpr int64_t kQuadProofScratch = 2 * kQuadTableInts * 4;
 
 struct VerifyArgs {
@@ -129,6 +137,12 @@ struct VerifyArgs {
   int64_t nblocks = 0;
   int64_t quad_max = 0;             // launches of at most this many proofs use k_verify_quad (the
                                     // runtime: kQuadVerifyMax, bounded by the slab's size)
+  uint64_t* clock_probe = nullptr;  // CPZ_CLOCK_PROBE builds only: k_verify_quad's phase stamps
+                                    // (kQuadPhases shader-clock words of block 0's first proof)
+  const ge_niels* vtab = nullptr;   // variable-base generators (no comb built for this (g, h)):
+                                    // Niels multiples 1..128 of g, h, 2^128 g, 2^128 h
+                                    // (k_build_niels), [s'] B from them inside the Straus loop;
+                                    // k_verify_quad only (launches of at most quad_max proofs)
 };
 
 struct ProveArgs {

@@ -656,6 +656,20 @@ __device__ __forceinline__ fe quad_lookup(const int32_t* tab, int d, int q) {
   return (neg && q == 2) ? fe_neg(x) : x;
 }
 
+// lane q's operand of the Niels multiple d (|d| <= 128, d = 0: the identity (1, 1, 0)) of a
+// fixed base whose multiples 1..128 are at tab[0..127] (k_build_niels): Y+X, Y-X, 2dXY, and
+// Z = 1 on lane 3; a negative digit swaps lanes 0 / 1's fields and negates lane 2's
+__device__ __forceinline__ fe quad_niels_lookup(const ge_niels* tab, int d, int q) {
+  const bool neg = d < 0;
+  const int mag = neg ? -d : d;
+  const int f = (neg && q < 2) ? 1 - q : q;
+  const int32_t* e = reinterpret_cast<const int32_t*>(tab + (mag == 0 ? 0 : mag - 1));
+  fe x = fe_load_limbs(e + 10 * (f < 3 ? f : 0));
+  x = fe_select(x, fe_one(), mag == 0 || q == 3);
+  x = fe_select(x, fe_zero(), mag == 0 && q == 2);
+  return (neg && q == 2) ? fe_neg(x) : x;
+}
+
 __device__ __forceinline__ ge_p3 p3_bcast(const ge_p3& P, int from) {
   ge_p3 r;
   if (from == 0) {
@@ -666,7 +680,10 @@ __device__ __forceinline__ ge_p3 p3_bcast(const ge_p3& P, int from) {
   return r;
 }
 
-template <bool kPre>
+// kVar: no comb for this (g, h) -- [s'] B comes from the Niels multiples 1..128 of B and
+// 2^128 B (a.vtab) as 2 x 16 signed radix-256 digits of s', one pair of mixed additions every
+// second window of the Straus loop (32 additions per equation against the comb's 16).
+template <bool kPre, bool kVar>
 __global__ void __launch_bounds__(256) k_verify_quad(VerifyArgs a) {
   const int t = threadIdx.x;
   int64_t i = (int64_t)blockIdx.x * 32 + (t >> 3);
@@ -678,7 +695,16 @@ __global__ void __launch_bounds__(256) k_verify_quad(VerifyArgs a) {
   }
   if (i >= a.n) return;                          // a proof's eight lanes together
   if (kPre && a.status[i] != kStOk) return;      // decode-level rejection: already final
-  const CombTable comb{a.comb + (e ? kCombPerBase : 0)};
+#if defined(CPZ_CLOCK_PROBE)
+  // timing builds only: shader-clock stamps at the phase boundaries of block 0's first proof
+  uint64_t stamp[kQuadPhases];
+  stamp[0] = __builtin_amdgcn_s_memtime();
+  stamp[7] = __builtin_amdgcn_s_memrealtime();
+#define CPZ_QUAD_STAMP(k) stamp[k] = __builtin_amdgcn_s_memtime()
+#else
+#define CPZ_QUAD_STAMP(k) (void)0
+#endif
+  const CombTable comb{kVar ? nullptr : a.comb + (e ? kCombPerBase : 0)};
   int32_t* tab = reinterpret_cast<int32_t*>(a.scratch) + ((int64_t)blockIdx.x * 64 + (t >> 2)) * kQuadTableInts;  // by slot
   uint32_t sw[8], cw[8];
   load_words8(sw, a.s, i);
@@ -700,8 +726,12 @@ __global__ void __launch_bounds__(256) k_verify_quad(VerifyArgs a) {
     }
     sc sp = sc_mul(vs, ss);
     if (vneg) sp = sc_neg(sp);
-    sc_recode_radix65536(sd, sp.w);
+    if constexpr (kVar)
+      sc_recode_radix256(sd, sp.w);   // bytes 0..15: digits on B, bytes 16..31: on 2^128 B
+    else
+      sc_recode_radix65536(sd, sp.w);
   }
+  CPZ_QUAD_STAMP(1);
   // lane 0 decodes this equation's Y, lane 1 its R
   ge_p3 P = ge_identity();
   bool ok = true;
@@ -715,20 +745,29 @@ __global__ void __launch_bounds__(256) k_verify_quad(VerifyArgs a) {
     }
   }
   ge_p3 Y = p3_bcast(P, 0), R = p3_bcast(P, 1);
+  CPZ_QUAD_STAMP(2);
   Y = ge_neg(Y);
   if (!vneg) R = ge_neg(R);
   quad_table(tab, Y, q);
   quad_table(tab + kQuadTableInts / 2, R, q);
   __threadfence_block();  // the quad's other lanes' fields (a negative digit reads them)
+  CPZ_QUAD_STAMP(3);
   // Q = [u] Y' + [|v|] R' + [s'] B: identity (mod E[4]) iff the equation holds
+  const ge_niels* gt = kVar ? a.vtab + e * kNielsEntries : nullptr;          // B = g or h
+  const ge_niels* gt2 = kVar ? a.vtab + (2 + e) * kNielsEntries : nullptr;   // 2^128 B
   ge_p3 acc = ge_identity();
 #pragma unroll 1
   for (int j = 0; j < 4; j++) {
     const uint32_t wu = ud[3], wv = vd[3];
+    const uint32_t wg = kVar ? sd[3] : 0u, wg2 = kVar ? sd[7] : 0u;
 #pragma unroll
     for (int k = 3; k > 0; k--) {
       ud[k] = ud[k - 1];
       vd[k] = vd[k - 1];
+      if constexpr (kVar) {
+        sd[k] = sd[k - 1];
+        sd[4 + k] = sd[4 + k - 1];
+      }
     }
 #pragma unroll 1
     for (int m = 7; m >= 0; m--) {
@@ -738,10 +777,19 @@ __global__ void __launch_bounds__(256) k_verify_quad(VerifyArgs a) {
       if (j != 0 || m != 7) acc = p3_dbl_n_quad(acc, 4, q);
       acc = ge_add_quad(acc, cached_of_field(ey), q);
       acc = ge_add_quad(acc, cached_of_field(er), q);
+      if constexpr (kVar) {
+        if ((m & 1) == 0) {  // byte 4 (3 - j) + m / 2 of s' (and of s' >> 128): weight 2^(4 t), t even
+          const int dg = (int32_t)(wg << (24 - 4 * m)) >> 24;
+          const int dg2 = (int32_t)(wg2 << (24 - 4 * m)) >> 24;
+          acc = ge_add_quad(acc, cached_of_field(quad_niels_lookup(gt, dg, q)), q);
+          acc = ge_add_quad(acc, cached_of_field(quad_niels_lookup(gt2, dg2, q)), q);
+        }
+      }
     }
   }
+  CPZ_QUAD_STAMP(4);
 #pragma unroll 1
-  for (int j = 0; j < 8; j++) {
+  for (int j = 0; j < (kVar ? 0 : 8); j++) {
     const uint32_t w = sd[0];
 #pragma unroll
     for (int k = 0; k < 7; k++) sd[k] = sd[k + 1];
@@ -757,6 +805,7 @@ __global__ void __launch_bounds__(256) k_verify_quad(VerifyArgs a) {
       acc = ge_add_quad(acc, c, q);
     }
   }
+  CPZ_QUAD_STAMP(5);
   // the proof's verdict from its two quads (lane 0 of quad e = 0 writes it)
   int eq = ristretto_is_identity(acc) ? 1 : 0;
   eq &= __shfl_xor(eq, 4);
@@ -780,17 +829,29 @@ __global__ void __launch_bounds__(256) k_verify_quad(VerifyArgs a) {
   else if (st_s == kStBadChallenge) st = kStBadScalar;
   else st = eq ? kStOk : kStEqFail;
   a.status[i] = st;
+#if defined(CPZ_CLOCK_PROBE)
+  CPZ_QUAD_STAMP(6);
+  stamp[8] = __builtin_amdgcn_s_memrealtime();
+  if (a.clock_probe && blockIdx.x == 0 && t == 0)
+    for (int k = 0; k < kQuadPhases; k++) a.clock_probe[k] = stamp[k];
+#endif
+#undef CPZ_QUAD_STAMP
 }
 
 hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
   const int64_t slots = a.blocks ? a.nblocks * (int64_t)a.block_proofs : a.n;
+  if (a.vtab && (a.pre || slots > a.quad_max)) return hipErrorInvalidValue;  // no comb: eight-lane kernel only
+  if (a.vtab) {
+    hipLaunchKernelGGL((k_verify_quad<false, true>), dim3((unsigned)((slots + 31) / 32)), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
   if (CPZ_VERIFY_QUAD && slots <= a.quad_max) {  // small batches: eight lanes per proof
     const unsigned g = (unsigned)((slots + 31) / 32);
     if (a.pre)
-      hipLaunchKernelGGL(k_verify_quad<true>, dim3(g), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((k_verify_quad<true, false>), dim3(g), dim3(256), 0, st, a);
     else
-      hipLaunchKernelGGL(k_verify_quad<false>, dim3(g), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((k_verify_quad<false, false>), dim3(g), dim3(256), 0, st, a);
     return hipGetLastError();
   }
   if (a.pre)

@@ -266,6 +266,8 @@ __global__ void __launch_bounds__(256, 2) k_part_acc(PartArgs a) {
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + wv;
   if (b >= a.nblk) return;  // whole waves
+  ClockStamp clk;
+  clk.start();
   const int64_t gb = a.blk0 + b;
   const uint32_t units = a.assign[b * kPartUnits + lane];  // (low unit, high unit), k_part_sort
   int v = (units & 0xff) >> 2, h = units & 3;
@@ -346,7 +348,10 @@ __global__ void __launch_bounds__(256, 2) k_part_acc(PartArgs a) {
       const ge_cached acc = acc_get();
       store_p3(ws + (v * kPartQuarters + h) * 2, *reinterpret_cast<const ge_p3*>(&acc));  // A_h (cached)
       store_p3(ws + (v * kPartQuarters + h) * 2 + 1, run);                                // S_h
-      if (v >= 16) break;
+      if (v >= 16) {
+        clk.stop(a.clock_probe, b);
+        break;
+      }
       v = (units >> 8) >> 2;
       h = (units >> 8) & 3;
       width = part_width(v);
@@ -645,13 +650,22 @@ hipError_t launch_gather_status(const uint8_t* status, const uint32_t* idx, int6
   return hipGetLastError();
 }
 
-hipError_t launch_part_msm(const PartArgs& a, hipStream_t st) {
+hipError_t launch_part_sort(const PartArgs& a, hipStream_t st) {
   if (a.nblk <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_part_sort, dim3((unsigned)a.nblk), dim3(kPartProofs), 0, st, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+hipError_t launch_part_acc(const PartArgs& a, hipStream_t st) {
+  if (a.nblk <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_part_acc, dim3((unsigned)((a.nblk + 3) / 4)), dim3(256), 0, st, a);
   return hipGetLastError();
+}
+
+hipError_t launch_part_msm(const PartArgs& a, hipStream_t st) {
+  hipError_t e = launch_part_sort(a, st);
+  if (e != hipSuccess) return e;
+  return launch_part_acc(a, st);
 }
 
 // One launch for every block of the batch: a block's combine is a chain of ~800 dependent

@@ -142,6 +142,7 @@ struct PartArgs {
                                  // digit exceeded kPartTopBuckets (the block is verified per proof)
   const uint32_t* pmap = nullptr;  // locate pass: listed block b's points are those of prepared
                                    // block pmap[b] (digits, sums and outputs are compact)
+  uint64_t* clock_probe = nullptr;  // CPZ_CLOCK_PROBE builds only: k_part_acc, 5 words per wave
 };
 
 // ---- locating a failing block's forged entry (part.hip) ----------------------------------
@@ -191,6 +192,8 @@ hipError_t launch_part_locate(const PartLocArgs& a, hipStream_t st);
 hipError_t launch_gather_status(const uint8_t* status, const uint32_t* idx, int64_t m, uint8_t* out, hipStream_t st);
 
 hipError_t launch_part_msm(const PartArgs& a, hipStream_t st);      // sort + walk of [blk0, blk0 + nblk)
+hipError_t launch_part_sort(const PartArgs& a, hipStream_t st);     // the sort alone
+hipError_t launch_part_acc(const PartArgs& a, hipStream_t st);      // the walk alone (k_part_acc)
 hipError_t launch_part_combine(const PartArgs& a, hipStream_t st);  // P_b and fail flags of [blk0, blk0 + nblk)
 // out = sum of part[0 .. nblk) (encoded, identity flag), through the scratch `tmp` of
 // ceil(nblk / 16) ge_p3

@@ -12,6 +12,7 @@
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -163,9 +164,12 @@ struct RlcMsmSet {
   }
 };
 
-// Fixed-base tables and transcript prefix of one (g, h) pair (ensure_generators).
+// Fixed-base tables and transcript prefix of one (g, h) pair (ensure_generators).  A full set
+// has the combs; a light set (a small per-proof call on a pair without one) only the Niels
+// tables, which k_verify_quad reads as variable bases (VerifyArgs::vtab).
 struct GenSet {
   bool valid = false;
+  bool full = true;
   uint64_t used = 0;  // LRU stamp
   uint8_t gh[64];
   DevBuf tab;       // 4 x 128 ge_niels (g, h, 2^128 g, 2^128 h)
@@ -189,6 +193,8 @@ struct GenSet {
 #define CPZ_GEN_CACHE 4
 #endif
 constexpr int kGenCache = CPZ_GEN_CACHE;
+// Light sets (64 KB of Niels tables + the transcript prefix each) a context keeps.
+constexpr int kLightCache = 64;
 
 }  // namespace
 
@@ -200,6 +206,8 @@ struct cpz_ctx {
   std::mutex mu;
   // fixed-base tables of the kGenCache most recently used (g, h) pairs; `gs` is the current one
   GenSet gen[kGenCache];
+  int gen_cap = kGenCache;  // full sets kept (env CPZ_GEN_CACHE at creation: 1 .. kGenCache)
+  GenSet light[kLightCache];
   GenSet* gs = nullptr;
   uint64_t gen_clock = 0;
   DevBuf ok_flags;  // 2 ints
@@ -254,10 +262,10 @@ struct cpz_ctx {
   hipEvent_t last_done = nullptr;
   bool have_last = false;
 #if defined(CPZ_CLOCK_PROBE)
-  // timing-only builds: the in-kernel clock stamps of the last k_rlc_prepare [0] and
-  // k_rlc_bucket [1] launch (cpz_ctx_clock_probe), 5 words per wave
-  DevBuf clk[2];
-  size_t clk_waves[2] = {0, 0};
+  // timing-only builds: the in-kernel clock stamps of the last k_rlc_prepare [0],
+  // k_rlc_bucket [1] and k_part_acc [2] launch (cpz_ctx_clock_probe), 5 words per wave
+  DevBuf clk[4];
+  size_t clk_waves[4] = {0, 0, 0, 0};
 #endif
   // optional per-kernel timing
   bool timing = false;
@@ -331,33 +339,23 @@ void words_from_bytes(uint32_t w[16], const uint8_t g[32], const uint8_t h[32]) 
   std::memcpy(w + 8, h, 32);
 }
 
-// Make the tables of (g, h) current: a cached set is reused, otherwise the least recently
-// used set (an unused one first) is rebuilt -- k_build_niels, k_transcript_prefix and the
-// 128 MiB combs (~3 ms), timed as stage 7 when timing is on.
-int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32]) {
-  uint8_t both[64];
-  std::memcpy(both, g, 32);
-  std::memcpy(both + 32, h, 32);
-  GenSet* victim = nullptr;
-  for (GenSet& e : ctx->gen) {
-    if (e.valid && std::memcmp(e.gh, both, 64) == 0) {
-      e.used = ++ctx->gen_clock;
-      ctx->gs = &e;
-      return CPZ_OK;
-    }
-    if (!victim || (!e.valid && victim->valid) || (e.valid == victim->valid && e.used < victim->used)) victim = &e;
+bool is_default_pair(const uint8_t g[32], const uint8_t h[32]) {
+  return std::memcmp(g, kDefaultG, 32) == 0 && std::memcmp(h, kDefaultH, 32) == 0;
+}
+
+// The least recently used of sets[0 .. n) (an unused one first).
+GenSet* lru_victim(GenSet* sets, int n) {
+  GenSet* v = nullptr;
+  for (int k = 0; k < n; k++) {
+    GenSet& e = sets[k];
+    if (!v || (!e.valid && v->valid) || (e.valid == v->valid && e.used < v->used)) v = &e;
   }
-  // Parameters::with_generators (gadgets.rs:77-103): valid, non-identity, distinct.
-  static const uint8_t zero[32] = {0};
-  if (std::memcmp(g, zero, 32) == 0 || std::memcmp(h, zero, 32) == 0)
-    return fail(CPZ_EGENERATOR, "generator cannot be identity");
-  if (std::memcmp(g, h, 32) == 0) return fail(CPZ_EGENERATOR, "generators g and h must be different");
-  // a set is about to be rebuilt: no earlier call's kernels may still be reading it
-  if (ctx->have_last) CPZ_HIP(hipEventSynchronize(ctx->last_done));
-  GenSet& e = *victim;
-  e.valid = false;
-  if (ctx->gs == &e) ctx->gs = nullptr;
-  StageTimer timer(ctx, 7, ctx->stream);
+  return v;
+}
+
+// The Niels tables (g, h, 2^128 g, 2^128 h) and transcript prefix of (g, h) into e, and the
+// fixed-schedule masks; CPZ_EGENERATOR if an encoding does not decode.
+int build_niels_prefix(cpz_ctx* ctx, GenSet& e, const uint8_t both[64]) {
   CPZ_HIP(e.tab.ensure(4 * cpz::kNielsEntries * sizeof(cpz::ge_niels)));  // g, h, 2^128 g, 2^128 h
   CPZ_HIP(e.prefix.ensure(2 * sizeof(cpz::StrobeSnap)));
   CPZ_HIP(e.gh_words.ensure(64));
@@ -374,16 +372,67 @@ int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32]) {
   CPZ_HIP(hipStreamSynchronize(ctx->stream));
   if (!ok[0] || !ok[1]) return fail(CPZ_EGENERATOR, "generator encoding does not decode to a ristretto255 point");
   e.prefix_fixed = cpz::challenge_prefix_is_fixed(snap[1]) && cpz::challenge_masks(e.chal_k1, e.chal_k2);
-  {
-    uint32_t gw[16];
-    words_from_bytes(gw, g, h);
-    e.ctx32_fixed = cpz::challenge_prefix_is_ctx32(snap[0]) && cpz::challenge_masks_ctx32(e.chal_c32, gw, gw + 8);
+  uint32_t gw[16];
+  std::memcpy(gw, both, 64);
+  e.ctx32_fixed = cpz::challenge_prefix_is_ctx32(snap[0]) && cpz::challenge_masks_ctx32(e.chal_c32, gw, gw + 8);
+  return CPZ_OK;
+}
+
+// Make the tables of (g, h) current.  A cached full set (combs) is reused.  need_comb false (a
+// per-proof call of at most kVarBaseMax proofs on a pair other than the default one): a cached
+// light set is reused, or one is built -- k_build_niels and k_transcript_prefix only, ~0.5 ms
+// instead of the combs' ~3 ms, timed as stage 13 -- and the call verifies with variable bases.
+// Otherwise the least recently used full set (an unused one first) is rebuilt: k_build_niels,
+// k_transcript_prefix and the 128 MiB combs (~3 ms), timed as stage 7.  If the combs do not fit,
+// the other full sets are freed and the allocation is tried once more.
+int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], bool need_comb = true) {
+  uint8_t both[64];
+  std::memcpy(both, g, 32);
+  std::memcpy(both + 32, h, 32);
+  for (int k = 0; k < ctx->gen_cap; k++) {
+    GenSet& e = ctx->gen[k];
+    if (e.valid && std::memcmp(e.gh, both, 64) == 0) {
+      e.used = ++ctx->gen_clock;
+      ctx->gs = &e;
+      return CPZ_OK;
+    }
   }
-  CPZ_HIP(e.comb.ensure((size_t)2 * cpz::kCombPerBase * sizeof(cpz::ge_niels)));
-  CPZ_HIP(e.comb_q.ensure((size_t)2 * cpz::kCombWindows * sizeof(cpz::ge_p3)));
-  CPZ_HIP(cpz::launch_build_comb(static_cast<const uint32_t*>(e.gh_words.p), static_cast<cpz::ge_p3*>(e.comb_q.p),
-                                 static_cast<cpz::ge_niels*>(e.comb.p), ctx->stream));
-  CPZ_HIP(hipStreamSynchronize(ctx->stream));  // callers may launch on another stream
+  const bool light = !need_comb && !is_default_pair(g, h);
+  if (light) {
+    for (GenSet& e : ctx->light) {
+      if (e.valid && std::memcmp(e.gh, both, 64) == 0) {
+        e.used = ++ctx->gen_clock;
+        ctx->gs = &e;
+        return CPZ_OK;
+      }
+    }
+  }
+  // Parameters::with_generators (gadgets.rs:77-103): valid, non-identity, distinct.
+  static const uint8_t zero[32] = {0};
+  if (std::memcmp(g, zero, 32) == 0 || std::memcmp(h, zero, 32) == 0)
+    return fail(CPZ_EGENERATOR, "generator cannot be identity");
+  if (std::memcmp(g, h, 32) == 0) return fail(CPZ_EGENERATOR, "generators g and h must be different");
+  // a set is about to be rebuilt: no earlier call's kernels may still be reading it
+  if (ctx->have_last) CPZ_HIP(hipEventSynchronize(ctx->last_done));
+  GenSet& e = light ? *lru_victim(ctx->light, kLightCache) : *lru_victim(ctx->gen, ctx->gen_cap);
+  e.valid = false;
+  e.full = !light;
+  if (ctx->gs == &e) ctx->gs = nullptr;
+  StageTimer timer(ctx, light ? 13 : 7, ctx->stream);
+  if (int rc = build_niels_prefix(ctx, e, both)) return rc;
+  if (!light) {
+    const size_t comb_bytes = (size_t)2 * cpz::kCombPerBase * sizeof(cpz::ge_niels);
+    if (e.comb.ensure(comb_bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      for (int k = 0; k < ctx->gen_cap; k++)  // trim: every other full set
+        if (&ctx->gen[k] != &e) ctx->gen[k].release();
+      CPZ_HIP(e.comb.ensure(comb_bytes));
+    }
+    CPZ_HIP(e.comb_q.ensure((size_t)2 * cpz::kCombWindows * sizeof(cpz::ge_p3)));
+    CPZ_HIP(cpz::launch_build_comb(static_cast<const uint32_t*>(e.gh_words.p), static_cast<cpz::ge_p3*>(e.comb_q.p),
+                                   static_cast<cpz::ge_niels*>(e.comb.p), ctx->stream));
+    CPZ_HIP(hipStreamSynchronize(ctx->stream));  // callers may launch on another stream
+  }
   std::memcpy(e.gh, both, 64);
   e.valid = true;
   e.used = ++ctx->gen_clock;
@@ -482,6 +531,11 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
     if (va.pre) v.pre = va.pre + 4 * a;
     v.status = va.status + a;
     v.quad_max = std::min<int64_t>(cpz::kQuadVerifyMax, (int64_t)(slab / cpz::kQuadProofScratch));
+#if defined(CPZ_CLOCK_PROBE)
+    CPZ_HIP(ctx->clk[3].ensure(cpz::kQuadPhases * sizeof(uint64_t)));
+    ctx->clk_waves[3] = 1;
+    v.clock_probe = static_cast<uint64_t*>(ctx->clk[3].p);
+#endif
     const int k = (int)((rr ? rr->next++ : c) % nst);  // stream k owns scratch slab k
     v.scratch = static_cast<char*>(ctx->scratch.p) + (size_t)k * slab;
     hipStream_t sc = k == 0 ? st : ctx->aux_stream[k - 1];
@@ -544,6 +598,11 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   va.c = ca.c_out;
   va.status = status;
   va.comb = static_cast<const cpz::ge_niels*>(ctx->gs->comb.p);
+  if (!ctx->gs->full) {  // a light set: variable-base generators (ensure_generators, n <= kVarBaseMax)
+    if ((int64_t)n > cpz::kVarBaseMax) return fail(CPZ_EINVAL, "internal: variable-base call above kVarBaseMax");
+    va.comb = nullptr;
+    va.vtab = static_cast<const cpz::ge_niels*>(ctx->gs->tab.p);
+  }
   va.scratch = nullptr;  // set per launch
   va.eq_only = ca.eq_only;
   StageTimer span(ctx, 5, st);  // all chunks, all streams (the launches overlap)
@@ -1139,7 +1198,9 @@ int part_locate(cpz_ctx* ctx, int64_t n, const void* s, const uint8_t* d_status,
     for (int64_t b0 = 0; b0 < nf; b0 += chunk) {
       pa.blk0 = b0;
       pa.nblk = std::min<int64_t>(chunk, nf - b0);
-      CPZ_HIP(cpz::launch_part_msm(pa, st));
+      CPZ_HIP(cpz::launch_part_sort(pa, st));
+      StageTimer ta(ctx, 15, st);  // the locate pass's walk (k_part_acc)
+      CPZ_HIP(cpz::launch_part_acc(pa, st));
     }
     pa.blk0 = 0;
     pa.nblk = nf;
@@ -1217,10 +1278,20 @@ int part_fallback(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* d_status, con
     pa.wsum = static_cast<cpz::ge_p3*>(ctx->pt_wsum.p);
     pa.part = static_cast<cpz::ge_p3*>(ctx->pt_part.p);
     pa.fail = static_cast<uint8_t*>(ctx->pt_fail.p);
+#if defined(CPZ_CLOCK_PROBE)
+    {  // k_part_acc's clock stamps: one record per wave (= per block) of the last chunk's launch
+      ctx->clk_waves[2] = (size_t)chunk;
+      CPZ_HIP(ctx->clk[2].ensure(ctx->clk_waves[2] * 40));
+      CPZ_HIP(hipMemsetAsync(ctx->clk[2].p, 0, ctx->clk_waves[2] * 40, st));
+      pa.clock_probe = static_cast<uint64_t*>(ctx->clk[2].p);
+    }
+#endif
     for (int64_t b0 = 0; b0 < nblk; b0 += chunk) {
       pa.blk0 = b0;
       pa.nblk = std::min<int64_t>(chunk, nblk - b0);
-      CPZ_HIP(cpz::launch_part_msm(pa, st));
+      CPZ_HIP(cpz::launch_part_sort(pa, st));
+      StageTimer ta(ctx, 14, st);  // every block's walk (k_part_acc), the C5 roofline's kernel
+      CPZ_HIP(cpz::launch_part_acc(pa, st));
     }
     pa.blk0 = 0;
     pa.nblk = nblk;
@@ -1434,6 +1505,11 @@ int ctx_create(int device_ordinal, cpz_ctx** out) {
   }
   ctx->cus = prop.multiProcessorCount;
   ctx->verify_blocks_per_cu = cpz::verify_each_blocks_per_cu();  // the grid-stride verify grid fills the chip once
+  // full (g, h) sets (128 MiB of combs each) this context may keep: CPZ_GEN_CACHE=1..4
+  if (const char* v = std::getenv("CPZ_GEN_CACHE")) {
+    const int k = std::atoi(v);
+    if (k >= 1 && k <= kGenCache) ctx->gen_cap = k;
+  }
   *out = ctx;
   return CPZ_OK;
 }
@@ -1460,11 +1536,23 @@ int cpz_ctx_create_timing_only(int device_ordinal, cpz_ctx** out) { return ctx_c
 #endif
 
 #if defined(CPZ_CLOCK_PROBE)
-// The clock stamps of the last k_rlc_prepare (kernel 0) or k_rlc_bucket (kernel 1) launch:
-// up to max_waves records of 5 words (a wave that did no work leaves zeros); *got = the
-// launch's waves.  Exported by CPZ_CLOCK_PROBE builds alone (tools/time_verify.py MODE=rlc).
+// The clock stamps of the last k_rlc_prepare (kernel 0), k_rlc_bucket (kernel 1) or, of the
+// partitioned check's first pass, k_part_acc (kernel 2) launch: up to max_waves records of 5
+// words (a wave that did no work leaves zeros); *got = the launch's waves.  Kernel 3: the last
+// k_verify_quad launch's kQuadPhases phase stamps (one 72-byte record; max_waves counts 40-byte
+// records, so pass at least 2).  Exported by CPZ_CLOCK_PROBE builds alone
+// (tools/time_verify.py MODE=rlc / MODE=c5, tools/quad_phases.py).
 int cpz_ctx_clock_probe(cpz_ctx* ctx, int kernel, uint64_t* out, size_t max_waves, size_t* got) {
-  if (!ctx || !out || !got || kernel < 0 || kernel > 1) return fail(CPZ_EINVAL, "bad arguments");
+  if (!ctx || !out || !got || kernel < 0 || kernel > 3) return fail(CPZ_EINVAL, "bad arguments");
+  if (kernel == 3) {
+    CallLock lock(ctx);
+    CPZ_HIP(hipSetDevice(ctx->device));
+    CPZ_HIP(hipDeviceSynchronize());
+    if (max_waves < 2 || !ctx->clk[3].p) return fail(CPZ_EINVAL, "no k_verify_quad stamps");
+    CPZ_HIP(hipMemcpy(out, ctx->clk[3].p, cpz::kQuadPhases * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    *got = 1;
+    return CPZ_OK;
+  }
   CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
   CPZ_HIP(hipDeviceSynchronize());
@@ -1900,7 +1988,7 @@ int cpz_verify_each_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32
   if (d_ctx_off && !d_ctx_bytes) return fail(CPZ_EINVAL, "ctx_off given without ctx_bytes");
   CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
-  int rc = ensure_generators(ctx, g, h);
+  int rc = ensure_generators(ctx, g, h, (int64_t)n > cpz::kVarBaseMax);
   if (rc) return rc;
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   if ((rc = order_after_last(ctx, st))) return rc;
@@ -1927,7 +2015,7 @@ int cpz_verify_each_ex(cpz_ctx* ctx, uint32_t flags, const uint8_t g[32], const 
   if (ctx_off && !ctx_bytes && ctx_off[n] != ctx_off[0]) return fail(CPZ_EINVAL, "ctx_off given without ctx_bytes");
   CallLock lock(ctx, flags);
   CPZ_HIP(hipSetDevice(ctx->device));
-  int rc = ensure_generators(ctx, g, h);
+  int rc = ensure_generators(ctx, g, h, (int64_t)n > cpz::kVarBaseMax);
   if (rc) return rc;
   if ((rc = order_after_last(ctx, ctx->stream))) return rc;
   const uint8_t* host[5] = {y1, y2, r1, r2, s};
@@ -1959,7 +2047,7 @@ int cpz_challenges(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], size_
   if (!y1 || !y2 || !r1 || !r2 || !c_out) return fail(CPZ_EINVAL, "null input pointer");
   CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
-  int rc = ensure_generators(ctx, g, h);
+  int rc = ensure_generators(ctx, g, h, false);
   if (rc) return rc;
   if ((rc = order_after_last(ctx, ctx->stream))) return rc;
   const uint8_t* host[5] = {y1, y2, r1, r2, nullptr};
@@ -2170,6 +2258,11 @@ int verify_response_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2,
   va.c = static_cast<const uint32_t*>(ctx->c.p);
   va.status = status;
   va.comb = static_cast<const cpz::ge_niels*>(ctx->gs->comb.p);
+  if (!ctx->gs->full) {  // a light set: variable-base generators (ensure_generators, n <= kVarBaseMax)
+    if ((int64_t)n > cpz::kVarBaseMax) return fail(CPZ_EINVAL, "internal: variable-base call above kVarBaseMax");
+    va.comb = nullptr;
+    va.vtab = static_cast<const cpz::ge_niels*>(ctx->gs->tab.p);
+  }
   va.scratch = nullptr;  // set per launch
   va.eq_only = ctx->call_eq ? 1 : 0;
   StageTimer span(ctx, 5, st);
@@ -2256,7 +2349,7 @@ int cpz_verify_response_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t 
   if (!rows_aligned(rows, 6)) return fail(CPZ_EINVAL, "device inputs must be 16-byte aligned");
   CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
-  int rc = ensure_generators(ctx, g, h);
+  int rc = ensure_generators(ctx, g, h, (int64_t)n > cpz::kVarBaseMax);
   if (rc) return rc;
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   if ((rc = order_after_last(ctx, st))) return rc;
@@ -2279,7 +2372,7 @@ int cpz_verify_response_ex(cpz_ctx* ctx, uint32_t flags, const uint8_t g[32], co
   if (!y1 || !y2 || !r1 || !r2 || !s || !c || !status_out) return fail(CPZ_EINVAL, "null input pointer");
   CallLock lock(ctx, flags);
   CPZ_HIP(hipSetDevice(ctx->device));
-  int rc = ensure_generators(ctx, g, h);
+  int rc = ensure_generators(ctx, g, h, (int64_t)n > cpz::kVarBaseMax);
   if (rc) return rc;
   if ((rc = order_after_last(ctx, ctx->stream))) return rc;
   const uint8_t* host[5] = {y1, y2, r1, r2, s};

@@ -8,6 +8,7 @@
 //     Q = [s] B + [c] V        (B = g or h fixed, V = -y1 or -y2 per proof)
 // whose result is compared with r by ristretto equality.
 #pragma once
+#include "timing_only.h"
 #include "ristretto.h"
 
 namespace cpz {
@@ -230,8 +231,15 @@ CPZ_HD ge_p1p1 straus_half_comb(const SlabTable& tab_y, const SlabTable& tab_r, 
       // (the tables live in the HBM-backed scratch slab; measured ~1 % faster)
       const ge_cached ey = cached_lookup(tab_y, du), er = cached_lookup(tab_r, dv);
       if (j != 3 || m != 7) cur = dbl4(cur);
+#if defined(CPZ_EXP_NIELS_TABLES)
+      // timing experiment only (timing_only.h: wrong verdicts): the entries added as affine
+      // Niels points, Z never read -- the best case of normalised per-proof tables
+      cur = ge_add_niels(p1p1_to_p3(cur), ge_niels{ey.YpX, ey.YmX, ey.T2d, {0, 0}});
+      cur = ge_add_niels(p1p1_to_p3(cur), ge_niels{er.YpX, er.YmX, er.T2d, {0, 0}});
+#else
       cur = ge_add_cached(p1p1_to_p3(cur), ey);
       cur = ge_add_cached(p1p1_to_p3(cur), er);
+#endif
     }
   }
   return comb_add(cur, comb, sdig);

@@ -290,7 +290,14 @@ CPZ_EQ_LOOP
     for (int q = 0; q < 8; q++) acc |= r[q];
     r_identity = acc == 0;
   }
+#if defined(CPZ_EXP_EXTRA_INV)
+  // timing experiment only (timing_only.h: wrong verdicts): one field inversion per equation
+  ge_p1p1 q = straus_half_comb(tab_y, tab_r, comb, udig, vdig, sdig);
+  q.X = fe_mul(q.X, fe_invert(q.Z));
+  return ristretto_is_identity(q);
+#else
   return ristretto_is_identity(straus_half_comb(tab_y, tab_r, comb, udig, vdig, sdig));
+#endif
 }
 
 // Full per-proof outcome given the challenge c (canonical) and the response status st_s.

@@ -326,10 +326,17 @@ int cpz_verify_batch_multi(cpz_ctx *const *ctxs, int nctx, const uint8_t g[32], 
  * whose launches overlap on several streams), 6 = prover (commitments / statements, then
  * challenges + responses), 7 = generator tables (a (g, h) pair's combs and transcript prefix
  * built: a cache miss, one launch each; a context keeps the tables of its 4 most recently used
- * pairs); phases of the RLC MSM (inside stage 3): 8 = bucket sort, 9 =
- * bucket accumulation (k_rlc_bucket), 10 = bucket fix-up, 11 = bucket reduction (segment +
- * window), 12 = window combine + encode (k_rlc_final).  cpz_ctx_stage_times synchronises, writes the summed milliseconds and
- * launch counts per stage since the last call, and resets them. */
+ * pairs, or of CPZ_GEN_CACHE = 1..4 set in the environment when it is created, and frees the
+ * others when a new pair's combs do not fit); phases of the RLC MSM (inside stage 3): 8 = bucket
+ * sort, 9 = bucket accumulation (k_rlc_bucket), 10 = bucket fix-up, 11 = bucket reduction
+ * (segment + window), 12 = window combine + encode (k_rlc_final); 13 = variable-base generator
+ * tables (a per-proof call of at most 16384 proofs on a pair other than the default one and
+ * without combs in the cache builds only the pair's Niels tables and transcript prefix, ~0.5 ms
+ * instead of ~3 ms, and verifies [s'] g, [s'] h from them; a context keeps 64 such pairs);
+ * phases of the partitioned check (inside stage 3): 14 = every block's bucket walk
+ * (k_part_acc), 15 = the locate pass's walk over the failing blocks.
+ * cpz_ctx_stage_times synchronises, writes the summed milliseconds and launch counts per stage
+ * since the last call, and resets them. */
 #define CPZ_NUM_STAGES 16
 int cpz_ctx_set_timing(cpz_ctx *ctx, int enable);
 int cpz_ctx_stage_times(cpz_ctx *ctx, double ms_out[CPZ_NUM_STAGES], int launches_out[CPZ_NUM_STAGES]);

@@ -267,7 +267,12 @@ int cpzt_verify_opcount(unsigned long long* mul, unsigned long long* sq, const u
 //   which = 1: k_rlc_bucket per sorted entry -- one p1p1 -> p3 conversion + one mixed
 //              (affine Niels) addition;
 //   which = 2: k_verify_prepared per proof (the fallback's per-proof pass) -- the equations
-//              with the points rebuilt from the prepared Niels forms instead of decoded.
+//              with the points rebuilt from the prepared Niels forms instead of decoded;
+//   which = 3: one k_part_acc walk step as the kernel executes it (part.hip): run + the
+//              cached operand (the staged Niels point with Z = 1, or acc), p1p1 -> p3, and
+//              acc's cached form (2 d T) -- the same products for an entry and a boundary;
+//   which = 4: the algorithmic entry step of that walk: run + an affine Niels point (a mixed
+//              addition) and p1p1 -> p3 (a boundary step, acc += run, is which = 3's work).
 int cpzt_rlc_opcount(int which, unsigned long long* mul, unsigned long long* sq, const uint8_t* g, const uint8_t* h,
                      const uint8_t* y1, const uint8_t* y2, const uint8_t* r1, const uint8_t* r2, const uint8_t* s,
                      const uint8_t* c) {
@@ -299,6 +304,20 @@ int cpzt_rlc_opcount(int which, unsigned long long* mul, unsigned long long* sq,
     r = ge_add_niels(p1p1_to_p3(r), pre[0]);
     cpzt_opcount(&m0, &s0);  // one steady-state step: conversion + addition
     r = ge_add_niels(p1p1_to_p3(r), pre[1]);
+  } else if (which == 3) {
+    ge_p3 run = p1p1_to_p3(ge_add_niels(ge_identity(), pre[0]));
+    cpzt_opcount(&m0, &s0);
+    ge_cached oc;  // the staged point as k_part_acc forms its cached operand (Z = 1 selected)
+    oc.YpX = pre[1].ypx;
+    oc.YmX = pre[1].ymx;
+    oc.T2d = pre[1].xy2d;
+    oc.Z = fe_one();
+    const ge_p3 r = p1p1_to_p3(ge_add_cached(run, oc));
+    (void)p3_to_cached(r);  // acc's cached form (written under the boundary lanes' mask)
+  } else if (which == 4) {
+    ge_p3 run = p1p1_to_p3(ge_add_niels(ge_identity(), pre[0]));
+    cpzt_opcount(&m0, &s0);
+    (void)p1p1_to_p3(ge_add_niels(run, pre[1]));
   } else {
     GenTables gt;
     if (!gt.build(g, h)) return -1;

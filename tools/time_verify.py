@@ -61,6 +61,54 @@ def rlc_probe(cp, gpu, t, status, steps):
     print(json.dumps(out))
 
 
+def c5_probe(cp, gpu, steps):
+    """MODE=c5: a configs[4]-shaped batch (N proofs, default 2^22, 0.1 % s + 1 forgeries) through
+    the batch check's partitioned fallback; the first pass's k_part_acc clock stamps (kernel 2 of
+    cpz_ctx_clock_probe: one record per wave = per 128-proof block, of the last walk launch)
+    and its HIP-event time (stage 14) per call.  Verdicts are not checked (timing-only build)."""
+    import ctypes
+    import json
+
+    import numpy as np
+    import torch
+    n = int(os.environ.get("N", 1 << 22))
+    dev = torch.device("cuda", 0)
+    t = {k: torch.empty((n, 32), dtype=torch.uint8, device=dev) for k in ("y1", "y2", "r1", "r2", "s")}
+    gpu.prove_synthetic_device(n, bytes(32), bytes(range(32)), t["y1"], t["y2"], t["r1"], t["r2"], t["s"])
+    idx = np.sort(np.random.default_rng(2024).choice(n, size=max(1, n // 1000), replace=False))
+    sys.path.insert(0, ROOT)
+    import bench
+    bench._bump_s(torch, t, idx)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    rows = [t[k] for k in ("y1", "y2", "r1", "r2", "s")]
+    seed = bytes(range(32))
+    gpu.verify_batch_device(*rows, status, seed, fallback=True)
+    torch.cuda.synchronize()
+    gpu.set_timing(True)
+    gpu.stage_times()
+    for _ in range(steps):
+        gpu.verify_batch_device(*rows, status, seed, fallback=True)
+    torch.cuda.synchronize()
+    st = gpu.stage_times()
+    lib = cp._native.load()
+    fn = lib.cpz_ctx_clock_probe
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+    got = ctypes.c_size_t(0)
+    buf = np.zeros((1 << 20) * 5, np.uint64)
+    cp._native.check(fn(gpu._h, 2, buf.ctypes.data, 1 << 20, ctypes.byref(got)))
+    w = buf[:5 * min(got.value, 1 << 20)].reshape(-1, 5).astype(np.int64)
+    rec = _clock_summary(w)
+    ms, cnt = st.get("part_acc", (0.0, 1))
+    rec["kernel_ms_per_call"] = ms / max(steps, 1)
+    rec["launches_per_call"] = cnt / max(steps, 1)
+    print(json.dumps({"what": "k_part_acc built with -DCPZ_CLOCK_PROBE -DCPZ_TIMING_ONLY (rlc_dev.h ClockStamp): per "
+                              "wave (one 128-proof block), s_memtime / s_memrealtime around its walk; the partitioned "
+                              "check's first pass over %d proofs with 0.1 %% forged, last of %d calls "
+                              "(tools/time_verify.py MODE=c5)" % (n, steps),
+                      "fallback": gpu.fallback_stats(), "k_part_acc": rec}))
+
+
 def main():
     import torch
     import chaum_pedersen as cp
@@ -68,6 +116,8 @@ def main():
     dev = torch.device("cuda", 0)
     # a timing-only build (csrc/timing_only.h) opens its context through the timing entry
     gpu = cp.Gpu(0, timing_only=hasattr(cp._native.load(), "cpz_ctx_create_timing_only"))
+    if os.environ.get("MODE") == "c5":
+        return c5_probe(cp, gpu, steps)
     t = {k: torch.empty((n, 32), dtype=torch.uint8, device=dev) for k in ("y1", "y2", "r1", "r2", "s")}
     status = torch.empty(n, dtype=torch.uint8, device=dev)
     gpu.prove_synthetic_device(n, bytes(32), bytes(range(32)), t["y1"], t["y2"], t["r1"], t["r2"], t["s"])
