@@ -97,7 +97,7 @@ struct RlcMsmArgs {
 // Pippenger MSM per block with signed 8-bit windows (the 16-bit digits of the prepare split in
 // two), giving every block's partial P_b = sum over its proofs of the RLC terms.  A block with
 // P_b the identity holds no forgery (w.o.p.); the others go to per-proof verification.
-// 128: C5 210.8 / 210.0 ms against 221.3 / 221.8 ms with 256-proof blocks (A/B, one call): the
+// 128: C5 210.8 / 210.0 ms against 221.3 / 221.8 ms with blocks of 256 proofs (A/B, one call): the
 // failing blocks' per-proof pass halves (12 % of the proofs at 0.1 % forged instead of 23 %),
 // the block partials cost 16 % more per proof (98 -> 114 ms: the 32 x 128 bucket boundaries per
 // block are spread over half the entries).
