@@ -166,11 +166,16 @@ hipError_t launch_challenge(const ChallengeArgs& a, hipStream_t st);
 hipError_t launch_probe_gather(const ProbeGatherArgs& a, hipStream_t st);
 bool challenge_prefix_is_fixed(const StrobeSnap& snap);  // the no-context fast path applies
 bool challenge_prefix_is_ctx32(const StrobeSnap& snap);  // prefix[0]: the 32-byte-context fast path applies
-hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, hipStream_t st);
+// Niels tables of 2 * nbases bases (nbases <= 8); `bases` is scratch for 2 * nbases ge_p3.
+hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, ge_p3* bases,
+                              hipStream_t st);
 hipError_t launch_parse_proofs(const ParseArgs& a, hipStream_t st);
 // Fixed-base combs of 2 bases (g, h): bases_scratch holds 2 * kCombWindows ge_p3.
 hipError_t launch_build_comb(const uint32_t* gh_words, ge_p3* bases_scratch, ge_niels* comb, hipStream_t st);
 hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st);
+// k_verify_small (kernels.hip): three waves per 8 proofs, the drop-in's latency path.  a.c null:
+// the challenges and response statuses are computed in the kernel from ca (k_challenge's inputs).
+hipError_t launch_verify_small(const VerifyArgs& a, const ChallengeArgs& ca, hipStream_t st);
 int verify_each_blocks_per_cu();  // resident k_verify_each blocks per CU (occupancy API)
 hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st);
 hipError_t launch_prove_response(const ProveArgs& a, hipStream_t st);

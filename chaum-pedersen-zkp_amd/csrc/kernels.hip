@@ -8,8 +8,8 @@
 //                        registers, any other context length on an LDS sponge image
 //                        batch.rs:188-206, gadgets.rs:466-482
 //   k_challenge_noctx    the same for batches without contexts (registers only)
-//   k_build_niels        (k * B) for k = 1..128, B in {g, h, 2^128 g, 2^128 h}: affine
-//                        Niels tables
+//   k_niels_bases /      (k * B) for k = 1..128, B in {g, h, 2^128 g, 2^128 h}: affine
+//   k_build_niels        Niels tables
 //   k_verify_each        1 thread / proof: challenge split v c = u (mod l) with
 //                        u, |v| < 2^127 (verify.h), 4 ristretto decodes, then per equation
 //                        [v s] B - [u] y - [v] r in E[4]  <=>  [s] B - [c] y == r
@@ -181,21 +181,29 @@ __global__ void __launch_bounds__(256) k_challenge_noctx(ChallengeArgs a) {
 // Fixed-base tables: tab[b * 128 + (k - 1)] = k * base_b in affine Niels form.
 // ---------------------------------------------------------------------------------------
 // Tables for 2 * nbases bases: [b0 .. b_{n-1}, 2^128 b0 .. 2^128 b_{n-1}], 128 entries each.
-__global__ void __launch_bounds__(64) k_build_niels(const uint32_t* __restrict__ base_words, int nbases, ge_niels* __restrict__ tab,
-                              int* __restrict__ ok) {
+// k_niels_bases: quad b decodes base b % nbases (every lane; ok flags from the first nbases
+// quads) and, for b >= nbases, doubles it 128 times as quad-cooperative doublings (~0.15 ms
+// for the chain, against ~0.35 ms on one lane per thread); k_build_niels: one thread per entry,
+// [k] B_b by double-and-add and one inversion to affine Niels.  A variable-base call's cold
+// (g, h) waits for both (ensure_generators).
+__global__ void __launch_bounds__(64) k_niels_bases(const uint32_t* __restrict__ base_words, int nbases,
+                                                     ge_p3* __restrict__ bases, int* __restrict__ ok) {
+  const int b = threadIdx.x >> 2, q = threadIdx.x & 3;
+  if (b >= 2 * nbases) return;  // whole quads
+  ge_p3 B;
+  const bool dec = ristretto_decode(B, base_words + 8 * (b % nbases));
+  if (b < nbases && q == 0) ok[b] = dec ? 1 : 0;
+  if (b >= nbases) B = p3_dbl_n_quad(B, 128, q);
+  if (q == 0) bases[b] = B;
+}
+
+__global__ void __launch_bounds__(64) k_build_niels(const ge_p3* __restrict__ bases, int nbases,
+                                                    ge_niels* __restrict__ tab) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 2 * nbases * kNielsEntries) return;
   const int b = t / kNielsEntries;
   const int k = t % kNielsEntries + 1;
-  const int src = b % nbases;
-  ge_p3 B;
-  const bool dec = ristretto_decode(B, base_words + 8 * src);
-  if (k == 1 && b < nbases) ok[b] = dec ? 1 : 0;
-  if (b >= nbases) {
-#pragma unroll 1
-    for (int d = 0; d < 128; d++) B = p1p1_to_p3(p3_dbl(B));
-  }
-  tab[t] = p3_to_niels(small_mul(B, k));
+  tab[t] = p3_to_niels(small_mul(bases[b], k));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -570,9 +578,14 @@ hipError_t launch_probe_gather(const ProbeGatherArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, hipStream_t st) {
+hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, ge_p3* bases,
+                              hipStream_t st) {
+  if (nbases < 1 || 2 * nbases > 16) return hipErrorInvalidValue;  // one wave of quads
+  hipLaunchKernelGGL(k_niels_bases, dim3(1), dim3(64), 0, st, base_words, nbases, bases, ok);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   const int total = 2 * nbases * kNielsEntries;
-  hipLaunchKernelGGL(k_build_niels, dim3((total + 63) / 64), dim3(64), 0, st, base_words, nbases, tab, ok);
+  hipLaunchKernelGGL(k_build_niels, dim3((total + 63) / 64), dim3(64), 0, st, (const ge_p3*)bases, nbases, tab);
   return hipGetLastError();
 }
 
@@ -836,6 +849,221 @@ __global__ void __launch_bounds__(256) k_verify_quad(VerifyArgs a) {
     for (int k = 0; k < kQuadPhases; k++) a.clock_probe[k] = stamp[k];
 #endif
 #undef CPZ_QUAD_STAMP
+}
+
+// ---------------------------------------------------------------------------------------
+// The drop-in's own regime (a BatchVerifier batch, at most 1000 entries): a call is one
+// dependent chain -- challenge, decodes, tables, 124 doublings, additions -- so its latency is
+// the longest chain, not the work.  k_verify_small splits each proof's chain over three waves of
+// one workgroup (8 proofs per workgroup, a quad per (proof, equation) in each wave):
+//   wave 0  decodes Y of each equation (lane 0 of the quad), builds the table of -Y in LDS,
+//           then [u] (-Y): 124 doublings + 32 additions;
+//   wave 1  the same for R: the table of +R, then [|v|] (-+R) (digits negated unless v < 0);
+//   wave 2  the transcript challenge (fixed schedules without a context or with a 32-byte one;
+//           the byte-wise sponge on one lane per proof otherwise), the response checks, the
+//           challenge split and recodings -- while waves 0 and 1 decode -- then [s'] B: 16 comb
+//           additions, or with variable-base generators (VerifyArgs::vtab) 120 doublings and
+//           32 Niels additions, beside waves 0 and 1's loops.
+// k_verify_quad ran all of it on one quad per equation: the challenge in a separate launch,
+// then decode, both tables, 124 doublings + 64 additions, the 16 comb additions in sequence.
+// The waves meet at two barriers (digits ready; partial sums ready), and wave 0 adds the three
+// partial sums and writes the statuses (verify_proof's precedence).  a.c != nullptr: the
+// challenges and response statuses were computed before (cpz_verify_response, or the
+// challenge kernel), wave 2 only splits.
+// ---------------------------------------------------------------------------------------
+constexpr int kSmallProofs = 8;  // proofs per workgroup (3 waves of 64 lanes)
+
+struct SmallShared {
+  uint32_t dig[kSmallProofs][16];      // u (0..3), |v| (4..7), s' (8..15) digit words
+  uint32_t meta[kSmallProofs];         // bit 0: v < 0; bits 8..15: response status
+  int32_t tab[2][16][9 * 40];          // waves 0 / 1: per quad, entries 0..8 (4 fields x 10 limbs)
+  ge_p3 part[3][16];                   // per quad: [u] (-Y), [|v|] (-+R), [s'] B
+  uint8_t bad[2][16];                  // decode failures (waves 0 / 1)
+  uint8_t rid[16];                     // R encodes the identity (wave 1)
+  uint32_t sponge[50][kSmallProofs];   // wave 2's byte-wise transcript, one column per proof
+};
+
+__global__ void __launch_bounds__(64 * 3) k_verify_small(VerifyArgs a, ChallengeArgs ca) {
+  __shared__ SmallShared sh;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int j = l >> 3, quad = l >> 2, e = (l >> 2) & 1, q = l & 3;
+  const int64_t i = (int64_t)blockIdx.x * kSmallProofs + j;
+  const bool live = i < a.n;
+  const int64_t ii = live ? i : 0;  // dead proofs run the same code on proof 0's rows, unwritten
+  ge_p3 acc = ge_identity();
+  if (w < 2) {
+    // ---- waves 0 / 1: decode Y (R) of equation e, its table --------------------------
+    ge_p3 P = ge_identity();
+    bool ok = true;
+    uint32_t enc[8];
+    load_words8(enc, w == 0 ? (e ? a.y2 : a.y1) : (e ? a.r2 : a.r1), ii);
+    if (q == 0) ok = ristretto_decode(P, enc);
+    P = p3_bcast(P, 0);
+    if (q == 0) {
+      sh.bad[w][quad] = ok ? 0 : 1;
+      if (w == 1) sh.rid[quad] = words8_zero(enc) ? 1 : 0;
+    }
+    if (w == 0) P = ge_neg(P);
+    int32_t* tab = &sh.tab[w][quad][0];
+    quad_table(tab, P, q);
+    __syncthreads();  // A: wave 2's digits; the quad's table fields
+    // ---- the half-length Straus loop over one point ---------------------------------
+    uint32_t d[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) d[k] = sh.dig[j][4 * w + k];
+    // wave 1: [|v|] (v < 0 ? R : -R) = [+-|v|] R from the table of +R
+    const bool flip = w == 1 && !(sh.meta[j] & 1u);
+#pragma unroll 1
+    for (int jj = 0; jj < 4; jj++) {
+      const uint32_t wd = d[3 - jj];
+#pragma unroll 1
+      for (int m = 7; m >= 0; m--) {
+        int dd = ((int32_t)(wd << (28 - 4 * m))) >> 28;
+        dd = flip ? -dd : dd;
+        const fe ex = quad_lookup(tab, dd, q);
+        if (jj != 0 || m != 7) acc = p3_dbl_n_quad(acc, 4, q);
+        acc = ge_add_quad(acc, cached_of_field(ex), q);
+      }
+    }
+    if (q == 0) sh.part[w][quad] = acc;
+  } else {
+    // ---- wave 2: challenge, response checks, split, digits ------------------------------
+    uint32_t sw[8], cw[8];
+    load_words8(sw, a.s, ii);
+    uint8_t st_s;
+    if (a.c) {
+      load_words8(cw, a.c, ii);
+      st_s = a.status[ii];
+    } else {
+      uint32_t y1[8], y2[8], r1[8], r2[8];
+      load_words8(y1, a.y1, ii);
+      load_words8(y2, a.y2, ii);
+      load_words8(r1, a.r1, ii);
+      load_words8(r2, a.r2, ii);
+      const bool has_ctx = ca.ctx_off != nullptr && (ca.ctx_present == nullptr || ca.ctx_present[ii] != 0);
+      const uint64_t b0 = has_ctx ? ca.ctx_off[ii] : 0, b1 = has_ctx ? ca.ctx_off[ii + 1] : 0;
+      const bool fixed_noctx = !has_ctx && ca.fast_noctx;
+      const bool fixed_ctx32 = has_ctx && ca.fast_ctx32 && b1 - b0 == 32 &&
+                               ((reinterpret_cast<uintptr_t>(ca.ctx_bytes) + b0) & 3) == 0;
+      sc c;
+      if (fixed_noctx) {
+        c = challenge_fixed(reinterpret_cast<const uint32_t*>(ca.prefix[1].state), ca.k1, ca.k2, y1, y2, r1, r2);
+      } else if (fixed_ctx32) {
+        uint32_t cx[8];
+        const uint32_t* cp = reinterpret_cast<const uint32_t*>(ca.ctx_bytes + b0);
+#pragma unroll
+        for (int k = 0; k < 8; k++) cx[k] = cp[k];
+        c = challenge_fixed_ctx32(reinterpret_cast<const uint32_t*>(ca.prefix[0].state), ca.c32, cx, y1, y2, r1, r2);
+      } else {
+        // any other context: the byte-wise sponge, on the proof's first lane (LDS column j)
+        for (int k = 0; k < 8; k++) c.w[k] = 0;
+        if ((l & 7) == 0) {
+          LdsState lst{&sh.sponge[0][0], j, kSmallProofs};
+          const StrobeSnap& snap = ca.prefix[has_ctx ? 0 : 1];
+          const uint32_t* src = reinterpret_cast<const uint32_t*>(snap.state);
+          for (int k = 0; k < 50; k++) sh.sponge[k][j] = src[k];
+          Strobe<LdsState> st(lst, snap.pos, snap.pos_begin, (uint8_t)snap.flags);
+          if (has_ctx) {
+            transcript_context(st, ca.ctx_bytes + b0, (uint32_t)(b1 - b0));
+            transcript_parameters(st, ca.gh_words, ca.gh_words + 8);
+          }
+          c = transcript_challenge(st, y1, y2, r1, r2);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) cw[k] = c.w[k];
+      st_s = response_status(sw, ca.eq_only != 0);
+    }
+    uint32_t ud[4], vd[4], sd[8];
+    bool vneg;
+    {
+      uint32_t u[4], va[4];
+      sc_half_split(cw, u, va, vneg);
+      sc_recode_radix16_half(ud, u);
+      sc_recode_radix16_half(vd, va);
+      sc vs, ss;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        vs.w[k] = k < 4 ? va[k] : 0u;
+        ss.w[k] = sw[k];
+      }
+      sc sp = sc_mul(vs, ss);
+      if (vneg) sp = sc_neg(sp);
+      if (a.vtab)
+        sc_recode_radix256(sd, sp.w);
+      else
+        sc_recode_radix65536(sd, sp.w);
+    }
+    if ((l & 7) == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        sh.dig[j][k] = ud[k];
+        sh.dig[j][4 + k] = vd[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) sh.dig[j][8 + k] = sd[k];
+      sh.meta[j] = (vneg ? 1u : 0u) | ((uint32_t)st_s << 8);
+    }
+    __syncthreads();  // A
+    // the digits as the proof's first lane wrote them (its lanes differ on the byte-wise path)
+#pragma unroll
+    for (int k = 0; k < 8; k++) sd[k] = sh.dig[j][8 + k];
+    // ---- [s'] B of equation e -------------------------------------------------------------
+    if (a.vtab) {  // variable bases: 16 radix-256 windows of s' on B and of s' >> 128 on 2^128 B
+      const ge_niels* gt = a.vtab + e * kNielsEntries;
+      const ge_niels* gt2 = a.vtab + (2 + e) * kNielsEntries;
+#pragma unroll 1
+      for (int b = 15; b >= 0; b--) {
+        const int dg = (int32_t)(sd[b >> 2] << (24 - 8 * (b & 3))) >> 24;
+        const int dg2 = (int32_t)(sd[4 + (b >> 2)] << (24 - 8 * (b & 3))) >> 24;
+        if (b != 15) acc = p3_dbl_n_quad(acc, 8, q);
+        acc = ge_add_quad(acc, cached_of_field(quad_niels_lookup(gt, dg, q)), q);
+        acc = ge_add_quad(acc, cached_of_field(quad_niels_lookup(gt2, dg2, q)), q);
+      }
+    } else {
+      const CombTable comb{a.comb + (e ? kCombPerBase : 0)};
+#pragma unroll 1
+      for (int k = 0; k < 16; k++) {
+        const int dgt = (int32_t)(sd[k >> 1] << (16 - 16 * (k & 1))) >> 16;
+        const ge_niels nl = comb.lookup(k, dgt);
+        ge_cached cc;
+        cc.YpX = nl.ypx;
+        cc.YmX = nl.ymx;
+        cc.T2d = nl.xy2d;
+        cc.Z = fe_one();
+        acc = ge_add_quad(acc, cc, q);
+      }
+    }
+    if (q == 0) sh.part[2][quad] = acc;
+  }
+  __syncthreads();  // B: the three partial sums
+  if (w != 0) return;
+  // ---- wave 0: Q = [u] (-Y) + [|v|] (-+R) + [s'] B, identity (mod E[4]) per equation ------
+  acc = ge_add_quad(acc, sh.part[1][quad], q);
+  acc = ge_add_quad(acc, sh.part[2][quad], q);
+  int eq = ristretto_is_identity(acc) ? 1 : 0;
+  eq &= __shfl_xor(eq, 4);
+  if ((l & 7) != 0 || !live) return;
+  const int q0 = 2 * j;
+  const bool bad = sh.bad[0][q0] | sh.bad[0][q0 + 1] | sh.bad[1][q0] | sh.bad[1][q0 + 1];
+  const bool rid = sh.rid[q0] | sh.rid[q0 + 1];
+  const uint8_t st_s = (uint8_t)(sh.meta[j] >> 8);
+  uint8_t st;
+  if (bad) st = kStBadPoint;
+  else if (st_s == kStBadScalar) st = kStBadScalar;
+  else if (rid && !a.eq_only) st = kStIdentity;
+  else if (st_s == kStZeroS) st = kStZeroS;
+  else if (st_s == kStBadChallenge) st = kStBadScalar;
+  else st = eq ? kStOk : kStEqFail;
+  a.status[i] = st;
+}
+
+hipError_t launch_verify_small(const VerifyArgs& a, const ChallengeArgs& ca, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  if (a.pre || a.blocks) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_verify_small, dim3((unsigned)((a.n + kSmallProofs - 1) / kSmallProofs)), dim3(64 * 3), 0, st,
+                     a, ca);
+  return hipGetLastError();
 }
 
 hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st) {

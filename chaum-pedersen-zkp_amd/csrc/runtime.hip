@@ -211,6 +211,7 @@ struct cpz_ctx {
   GenSet* gs = nullptr;
   uint64_t gen_clock = 0;
   DevBuf ok_flags;  // 2 ints
+  DevBuf gen_bases; // 4 ge_p3: g, h, 2^128 g, 2^128 h (k_niels_bases)
   // work buffers
   DevBuf c;         // n x 32
   DevBuf st;        // n
@@ -360,9 +361,11 @@ int build_niels_prefix(cpz_ctx* ctx, GenSet& e, const uint8_t both[64]) {
   CPZ_HIP(e.prefix.ensure(2 * sizeof(cpz::StrobeSnap)));
   CPZ_HIP(e.gh_words.ensure(64));
   CPZ_HIP(ctx->ok_flags.ensure(2 * sizeof(int)));
+  CPZ_HIP(ctx->gen_bases.ensure(4 * sizeof(cpz::ge_p3)));
   CPZ_HIP(hipMemcpyAsync(e.gh_words.p, both, 64, hipMemcpyHostToDevice, ctx->stream));
   CPZ_HIP(cpz::launch_build_niels(static_cast<const uint32_t*>(e.gh_words.p), 2, static_cast<cpz::ge_niels*>(e.tab.p),
-                                  static_cast<int*>(ctx->ok_flags.p), ctx->stream));
+                                  static_cast<int*>(ctx->ok_flags.p), static_cast<cpz::ge_p3*>(ctx->gen_bases.p),
+                                  ctx->stream));
   CPZ_HIP(cpz::launch_transcript_prefix(static_cast<const uint32_t*>(e.gh_words.p),
                                         static_cast<cpz::StrobeSnap*>(e.prefix.p), ctx->stream));
   int ok[2] = {0, 0};
@@ -477,6 +480,15 @@ int verify_grid(cpz_ctx* ctx, size_t n) {
 #ifndef CPZ_VERIFY_STREAMS
 #define CPZ_VERIFY_STREAMS 2
 #endif
+// Launches of at most kSmallMax proofs (without prepared points or block lists) take
+// k_verify_small: three waves per 8 proofs, the transcript challenge computed inside.
+#ifndef CPZ_VERIFY_SMALL
+#define CPZ_VERIFY_SMALL 1
+#endif
+#ifndef CPZ_SMALL_MAX
+#define CPZ_SMALL_MAX 2048
+#endif
+constexpr int64_t kSmallMax = CPZ_SMALL_MAX;
 #ifndef CPZ_VERIFY_CHUNK_DIV
 #define CPZ_VERIFY_CHUNK_DIV 2
 #endif
@@ -539,6 +551,20 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
     const int k = (int)((rr ? rr->next++ : c) % nst);  // stream k owns scratch slab k
     v.scratch = static_cast<char*>(ctx->scratch.p) + (size_t)k * slab;
     hipStream_t sc = k == 0 ? st : ctx->aux_stream[k - 1];
+    if (CPZ_VERIFY_SMALL && v.n <= kSmallMax && !v.pre && !v.blocks && (!ca || !ca->ctx_end)) {
+      // the drop-in's regime: three waves per 8 proofs, the challenge inside (k_verify_small)
+      cpz::ChallengeArgs cc{};
+      if (ca) {
+        cc = *ca;
+        cc.n = v.n;
+        if (ca->ctx_off) cc.ctx_off = ca->ctx_off + a;
+        if (ca->ctx_present) cc.ctx_present = ca->ctx_present + a;
+        v.c = nullptr;  // computed in the kernel
+      }
+      StageTimer t(ctx, stage, sc);
+      CPZ_HIP(cpz::launch_verify_small(v, cc, sc));
+      continue;
+    }
     if (ca) {
       cpz::ChallengeArgs cc = *ca;
       cc.n = v.n;

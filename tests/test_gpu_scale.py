@@ -57,9 +57,23 @@ def test_small_batch_eight_lanes_every_forgery_kind(gpu, golden, n):
     _every_forgery_kind(gpu, golden, n, n, 7 + n)
 
 
-def _every_forgery_kind(gpu, golden, n, nsample, seed):
+@pytest.mark.parametrize("n", [1, 2, 7, 8, 9, 100, 2047, 2048, 2049])
+def test_small_kernel_every_forgery_kind_and_context_shape(gpu, golden, n):
+    """Launches of at most 2048 proofs take k_verify_small (three waves per 8 proofs, the
+    transcript challenge computed inside: fixed schedules for no context and 32-byte contexts,
+    the byte-wise sponge for Some(b"") and other lengths): on both sides of the limit and at
+    the workgroup's 8-proof edges, every status and challenge equals the C oracle's."""
+    _every_forgery_kind(gpu, golden, n, n, 31 + n, ctx_shapes=True)
+
+
+def _every_forgery_kind(gpu, golden, n, nsample, seed, ctx_shapes=False):
     rng = np.random.default_rng(seed)
-    ctxs = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() if i % 4 == 0 else None for i in range(n)]
+    if ctx_shapes:   # none, 32 bytes (fixed schedules), Some(b"") and 1..80 bytes (the sponge)
+        ctxs = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() if i % 4 == 0 else
+                (b"" if i % 4 == 1 else (rng.integers(0, 256, int(rng.integers(1, 81)), dtype=np.uint8).tobytes()
+                                         if i % 4 == 2 else None)) for i in range(n)]
+    else:
+        ctxs = [rng.integers(0, 256, 32, dtype=np.uint8).tobytes() if i % 4 == 0 else None for i in range(n)]
     rows = gpu.prove_synthetic(n, SX, SK, contexts=ctxs)
     rows = {k: np.ascontiguousarray(rows[k]) for k in KEYS}
     sample = np.sort(rng.choice(n, size=nsample, replace=False))
@@ -104,7 +118,10 @@ def _every_forgery_kind(gpu, golden, n, nsample, seed):
     seen = {}
     for i, kind in expect_kind.items():
         seen.setdefault(kind, set()).add(int(st[i]))
-    assert seen == want, seen
+    if len(forged) >= 2 * len(kinds):
+        assert seen == want, seen
+    else:
+        assert all(seen[k] == want[k] for k in seen), seen
     assert np.array_equal(np.nonzero(st)[0], np.sort(forged))
 
 
