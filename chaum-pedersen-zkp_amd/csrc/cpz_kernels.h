@@ -111,6 +111,9 @@ constexpr int64_t kVarBaseMax = kQuadVerifyMax;
 // k_verify_quad phase stamps (CPZ_CLOCK_PROBE): start, split + digits, decode, tables, Straus,
 // comb, verdict; then the 100 MHz clock at start and end.
 constexpr int kQuadPhases = 9;
+// k_verify_small's stamps (CPZ_CLOCK_PROBE): wave 0 start, decoded, table, barrier A, Straus,
+// barrier B, verdict; wave 2 digits, [s'] B; 100 MHz at wave 0's start / end; wave 2's start.
+constexpr int kSmallStamps = 12;
 constexpr int64_t kQuadProofScratch = 2 * kQuadTableInts * 4;
 
 struct VerifyArgs {

@@ -891,6 +891,17 @@ __global__ void __launch_bounds__(64 * 3) k_verify_small(VerifyArgs a, Challenge
   const bool live = i < a.n;
   const int64_t ii = live ? i : 0;  // dead proofs run the same code on proof 0's rows, unwritten
   ge_p3 acc = ge_identity();
+#if defined(CPZ_CLOCK_PROBE)
+  // timing builds only: shader-clock stamps of block 0 (wave 0 lane 0: start, decoded, table,
+  // barrier A, Straus, barrier B, verdict; wave 2 lane 0: digits written, [s'] B done) and the
+  // 100 MHz clock at wave 0's start and end -> a.clock_probe[0 .. kSmallStamps)
+  uint64_t* const stamps = (a.clock_probe && blockIdx.x == 0 && l == 0 && w != 1) ? a.clock_probe : nullptr;
+#define CPZ_SMALL_STAMP(k) do { if (stamps) stamps[k] = __builtin_amdgcn_s_memtime(); } while (0)
+  if (stamps && w == 0) stamps[9] = __builtin_amdgcn_s_memrealtime();
+  CPZ_SMALL_STAMP(w == 0 ? 0 : 11);
+#else
+#define CPZ_SMALL_STAMP(k) (void)0
+#endif
   if (w < 2) {
     // ---- waves 0 / 1: decode Y (R) of equation e, its table --------------------------
     ge_p3 P = ge_identity();
@@ -899,6 +910,7 @@ __global__ void __launch_bounds__(64 * 3) k_verify_small(VerifyArgs a, Challenge
     load_words8(enc, w == 0 ? (e ? a.y2 : a.y1) : (e ? a.r2 : a.r1), ii);
     if (q == 0) ok = ristretto_decode(P, enc);
     P = p3_bcast(P, 0);
+    if (w == 0) CPZ_SMALL_STAMP(1);
     if (q == 0) {
       sh.bad[w][quad] = ok ? 0 : 1;
       if (w == 1) sh.rid[quad] = words8_zero(enc) ? 1 : 0;
@@ -906,7 +918,9 @@ __global__ void __launch_bounds__(64 * 3) k_verify_small(VerifyArgs a, Challenge
     if (w == 0) P = ge_neg(P);
     int32_t* tab = &sh.tab[w][quad][0];
     quad_table(tab, P, q);
+    if (w == 0) CPZ_SMALL_STAMP(2);
     __syncthreads();  // A: wave 2's digits; the quad's table fields
+    if (w == 0) CPZ_SMALL_STAMP(3);
     // ---- the half-length Straus loop over one point ---------------------------------
     uint32_t d[4];
 #pragma unroll
@@ -926,6 +940,7 @@ __global__ void __launch_bounds__(64 * 3) k_verify_small(VerifyArgs a, Challenge
       }
     }
     if (q == 0) sh.part[w][quad] = acc;
+    if (w == 0) CPZ_SMALL_STAMP(4);
   } else {
     // ---- wave 2: challenge, response checks, split, digits ------------------------------
     uint32_t sw[8], cw[8];
@@ -1004,6 +1019,7 @@ __global__ void __launch_bounds__(64 * 3) k_verify_small(VerifyArgs a, Challenge
       for (int k = 0; k < 8; k++) sh.dig[j][8 + k] = sd[k];
       sh.meta[j] = (vneg ? 1u : 0u) | ((uint32_t)st_s << 8);
     }
+    CPZ_SMALL_STAMP(7);
     __syncthreads();  // A
     // the digits as the proof's first lane wrote them (its lanes differ on the byte-wise path)
 #pragma unroll
@@ -1035,9 +1051,11 @@ __global__ void __launch_bounds__(64 * 3) k_verify_small(VerifyArgs a, Challenge
       }
     }
     if (q == 0) sh.part[2][quad] = acc;
+    CPZ_SMALL_STAMP(8);
   }
   __syncthreads();  // B: the three partial sums
   if (w != 0) return;
+  CPZ_SMALL_STAMP(5);
   // ---- wave 0: Q = [u] (-Y) + [|v|] (-+R) + [s'] B, identity (mod E[4]) per equation ------
   acc = ge_add_quad(acc, sh.part[1][quad], q);
   acc = ge_add_quad(acc, sh.part[2][quad], q);
@@ -1056,6 +1074,11 @@ __global__ void __launch_bounds__(64 * 3) k_verify_small(VerifyArgs a, Challenge
   else if (st_s == kStBadChallenge) st = kStBadScalar;
   else st = eq ? kStOk : kStEqFail;
   a.status[i] = st;
+#if defined(CPZ_CLOCK_PROBE)
+  CPZ_SMALL_STAMP(6);
+  if (stamps) stamps[10] = __builtin_amdgcn_s_memrealtime();
+#endif
+#undef CPZ_SMALL_STAMP
 }
 
 hipError_t launch_verify_small(const VerifyArgs& a, const ChallengeArgs& ca, hipStream_t st) {

@@ -544,7 +544,7 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
     v.status = va.status + a;
     v.quad_max = std::min<int64_t>(cpz::kQuadVerifyMax, (int64_t)(slab / cpz::kQuadProofScratch));
 #if defined(CPZ_CLOCK_PROBE)
-    CPZ_HIP(ctx->clk[3].ensure(cpz::kQuadPhases * sizeof(uint64_t)));
+    CPZ_HIP(ctx->clk[3].ensure(cpz::kSmallStamps * sizeof(uint64_t)));
     ctx->clk_waves[3] = 1;
     v.clock_probe = static_cast<uint64_t*>(ctx->clk[3].p);
 #endif
@@ -1566,7 +1566,7 @@ int cpz_ctx_create_timing_only(int device_ordinal, cpz_ctx** out) { return ctx_c
 // partitioned check's first pass, k_part_acc (kernel 2) launch: up to max_waves records of 5
 // words (a wave that did no work leaves zeros); *got = the launch's waves.  Kernel 3: the last
 // k_verify_quad launch's kQuadPhases phase stamps (one 72-byte record; max_waves counts 40-byte
-// records, so pass at least 2).  Exported by CPZ_CLOCK_PROBE builds alone
+// records, so pass at least 2; k_verify_small's kSmallStamps words when it ran instead).  Exported by CPZ_CLOCK_PROBE builds alone
 // (tools/time_verify.py MODE=rlc / MODE=c5, tools/quad_phases.py).
 int cpz_ctx_clock_probe(cpz_ctx* ctx, int kernel, uint64_t* out, size_t max_waves, size_t* got) {
   if (!ctx || !out || !got || kernel < 0 || kernel > 3) return fail(CPZ_EINVAL, "bad arguments");
@@ -1575,7 +1575,7 @@ int cpz_ctx_clock_probe(cpz_ctx* ctx, int kernel, uint64_t* out, size_t max_wave
     CPZ_HIP(hipSetDevice(ctx->device));
     CPZ_HIP(hipDeviceSynchronize());
     if (max_waves < 2 || !ctx->clk[3].p) return fail(CPZ_EINVAL, "no k_verify_quad stamps");
-    CPZ_HIP(hipMemcpy(out, ctx->clk[3].p, cpz::kQuadPhases * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    CPZ_HIP(hipMemcpy(out, ctx->clk[3].p, cpz::kSmallStamps * sizeof(uint64_t), hipMemcpyDeviceToHost));
     *got = 1;
     return CPZ_OK;
   }

@@ -460,6 +460,66 @@ def test_partitioned_locate_edges(gpu):
     assert p == _oracle_partial(host, idx)
 
 
+def test_partitioned_related_forgeries_in_one_block(gpu):
+    """Blocks whose forgeries are related: a forged proof copied byte for byte into
+    another slot of its block (the same error point, differently weighted), s + 1 and s + 2 on
+    two slots (scaled errors), s + 1 and s - 1 on two copies of one proof (opposite errors), and
+    three copies of one forged proof.  For a secret seed no index-weighted candidate matches, so
+    each such block is verified whole: the exact set, the oracle's partial, and the located /
+    whole split of the stats as for independent forgeries."""
+    torch = pytest.importorskip("torch")
+    n = (1 << 20) + 77
+    t = _synthetic_device(gpu, torch, n)
+    rng = np.random.default_rng(7171)
+    idx = rng.choice(n, size=n // 1000, replace=False)
+    B = 256   # placed inside one 128-proof block, whatever the block size
+    free = [b for b in range(64, n // B - 64, 41) if not np.any(idx // B == b)]
+    b1, b2, b3, b4 = free[:4]
+    host = _forge(t, torch, np.sort(idx))
+
+    def copy_row(dst, src):
+        for k in KEYS:
+            t[k][dst] = t[k][src].clone()
+
+    def add_s(e, delta):
+        v = (_le(t["s"][e].cpu().numpy()) + delta) % O.L
+        t["s"][e] = torch.from_numpy(np.frombuffer(v.to_bytes(32, "little"), np.uint8).copy()).to("cuda:0")
+
+    related = []
+    e = B * b1 + 10                      # the same forged proof in two slots
+    add_s(e, 1)
+    copy_row(e + 3, e)
+    related += [e, e + 3]
+    e = B * b2 + 20                      # scaled: s + 1 and s + 2
+    add_s(e, 1)
+    add_s(e + 7, 2)
+    related += [e, e + 7]
+    e = B * b3 + 30                      # opposite: s + 1 and s - 1 on two copies of one proof
+    copy_row(e + 1, e)
+    add_s(e, 1)
+    add_s(e + 1, -1)
+    related += [e, e + 1]
+    e = B * b4 + 40                      # three copies of one forged proof
+    add_s(e, 1)
+    copy_row(e + 2, e)
+    copy_row(e + 5, e)
+    related += [e, e + 2, e + 5]
+    allf = np.union1d(idx, related)
+    sel = torch.from_numpy(allf.astype(np.int64)).to("cuda:0")
+    host = {k: t[k].index_select(0, sel).cpu().numpy() for k in KEYS}
+    st = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    p, ok = gpu.verify_batch_device(*(t[k] for k in KEYS), st, WSEED, fallback=True)
+    stats = gpu.fallback_stats()
+    got = st.cpu().numpy()
+    assert not ok and stats["path"] == "partitioned", stats
+    assert np.array_equal(np.nonzero(got)[0], allf) and set(got[allf].tolist()) == {1}
+    blk = _part_block(n, stats)
+    nfail, one, want_pp = _locate_expect(allf, blk, n)
+    assert stats["blocks_failing"] == stats["blocks_indexed"] == nfail, stats
+    assert stats["blocks_located"] == one and stats["per_proof"] == want_pp, stats
+    assert p == _oracle_partial(host, allf)
+
+
 def test_partitioned_fallback_decode_failures_and_equations_only(gpu, golden):
     """The partitioned check with entries whose decode-level status is non-zero:
     an undecodable r1, s + l (non-canonical), zero s and an identity r1, placed in blocks that

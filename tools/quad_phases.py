@@ -1,9 +1,11 @@
 """Where a small synchronous per-proof call spends its time: with the CPZ_CLOCK_PROBE timing
-build (CPZ_LIB=lib/timing/clock_probe.so), k_verify_quad stamps the shader clock at its phase
-boundaries for block 0's first proof (kernels.hip) -- challenge split and digits, the decode,
-the two tables, the Straus loop, the comb, the verdict -- and the 100 MHz clock around it, so
-the phases come out in microseconds at the kernel's own clock.  N proofs per call (default 1),
-CALLS calls, median per phase; the wall time of the synchronous call beside it."""
+build (CPZ_LIB=lib/timing/clock_probe.so) the per-proof kernel stamps the shader clock at its
+phase boundaries for block 0 (kernels.hip) and the 100 MHz clock around it, so the phases come
+out in microseconds at the kernel's own clock.  k_verify_small (launches of <= 2048 proofs):
+wave 0's decode, table, wait for wave 2's digits, Straus, wait for the partial sums, verdict,
+and wave 2's challenge + split and [s'] B; k_verify_quad (larger launches, or a library built
+with CPZ_VERIFY_SMALL=0; KERNEL=quad): split, decode, tables, Straus, comb, verdict.  N proofs
+per call (default 1), CALLS calls, median per phase; the synchronous call's wall time beside."""
 import ctypes
 import json
 import os
@@ -16,6 +18,8 @@ sys.path.insert(0, os.path.join(ROOT, "chaum-pedersen-zkp_amd"))
 sys.path.insert(0, ROOT)
 
 NAMES = ("split_digits", "decode", "tables", "straus", "comb", "verdict")
+SMALL = (("decode", 0, 1), ("table", 1, 2), ("wait_digits", 2, 3), ("straus", 3, 4), ("wait_partials", 4, 5),
+         ("verdict", 5, 6), ("w2_challenge_split", 11, 7), ("w2_s_B", 7, 8))
 
 
 def main():
@@ -27,35 +31,46 @@ def main():
     lib = cp._native.load()
     gpu = cp.Gpu(0, timing_only=hasattr(lib, "cpz_ctx_create_timing_only"))
     params = None
-    if os.environ.get("CUSTOM"):   # a custom pair: the variable-base form
-        o = gpu.prove([5, 7], [5, 7])
+    pg = gpu
+    if os.environ.get("CUSTOM"):   # a custom pair proved on another context: variable bases here
+        pg = cp.Gpu(0, timing_only=hasattr(lib, "cpz_ctx_create_timing_only"))
+        o = pg.prove([5, 7], [5, 7])
         params = cp.Parameters(o["y1"][0].tobytes(), o["y1"][1].tobytes())
-    rows = gpu.prove_synthetic(n, bench.SEED_X, bench.SEED_K, params=params)
+    rows = pg.prove_synthetic(n, bench.SEED_X, bench.SEED_K, params=params)
     cols = [np.ascontiguousarray(rows[k]) for k in ("y1", "y2", "r1", "r2", "s")]
     fn = lib.cpz_ctx_clock_probe
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
-    per, wall, clk = {k: [] for k in NAMES}, [], []
+    small = os.environ.get("KERNEL", "small" if n <= 2048 else "quad") == "small"
+    names = [x[0] for x in SMALL] if small else list(NAMES)
+    per, wall, clk = {k: [] for k in names}, [], []
     for it in range(calls + 3):
         t0 = time.perf_counter()
         gpu.verify_each(*cols, params=params, equations_only=True)
         el = (time.perf_counter() - t0) * 1e6
-        buf = np.zeros(10, np.uint64)
+        buf = np.zeros(15, np.uint64)
         got = ctypes.c_size_t(0)
-        cp._native.check(fn(gpu._h, 3, buf.ctypes.data, 2, ctypes.byref(got)))
+        cp._native.check(fn(gpu._h, 3, buf.ctypes.data, 3, ctypes.byref(got)))
         if it < 3:
             continue
-        st = buf[:9].astype(np.int64)
-        real_us = (st[8] - st[7]) / 100.0
-        ticks = st[6] - st[0]
+        st = buf[:12].astype(np.int64)
+        if small:
+            real_us, ticks = (st[10] - st[9]) / 100.0, st[6] - st[0]
+        else:
+            real_us, ticks = (st[8] - st[7]) / 100.0, st[6] - st[0]
         ghz = ticks / (real_us * 1e3) if real_us > 0 else float("nan")
         clk.append(ghz)
-        for k, name in enumerate(NAMES):
-            per[name].append((st[k + 1] - st[k]) / (ghz * 1e3))
+        if small:
+            for name, a, b in SMALL:
+                per[name].append((st[b] - st[a]) / (ghz * 1e3))
+        else:
+            for k, name in enumerate(NAMES):
+                per[name].append((st[k + 1] - st[k]) / (ghz * 1e3))
         wall.append(el)
-    out = {"n": n, "calls": calls, "custom_pair": bool(params), "kernel_clock_ghz": statistics.median(clk),
-           "phase_us": {k: round(statistics.median(v), 1) for k, v in per.items()},
-           "kernel_us": round(sum(statistics.median(v) for v in per.values()), 1),
+    med = {k: round(statistics.median(v), 1) for k, v in per.items()}
+    out = {"n": n, "calls": calls, "kernel": "k_verify_small" if small else "k_verify_quad",
+           "custom_pair": bool(params), "kernel_clock_ghz": statistics.median(clk), "phase_us": med,
+           "kernel_us": round(sum(med[k] for k in names if not k.startswith("w2_")), 1),
            "call_wall_us": round(statistics.median(wall), 1)}
     print(json.dumps(out))
 
