@@ -3,8 +3,9 @@ the only device of the test box) each reduce their shard of a forged batch to a 
 partial on the GPU (weights keyed by the global index), all-gather them with
 chaum_pedersen.shard.all_gather_partials (bench.py's code path) and combine them on the
 device; the result equals the single-process whole-batch partial, and the per-proof
-shards' statuses concatenate to the whole batch's.  (RCCL's "nccl" backend cannot put two
-ranks on one GPU; the driver's 8-GPU run exercises it.)"""
+shards' statuses concatenate to the whole batch's.  RCCL's "nccl" backend cannot put two
+ranks on one GPU: a world of one runs all_gather_partials' RCCL branch here, and the driver's
+8-GPU run exercises the exchange itself."""
 import os
 import socket
 import sys
@@ -146,6 +147,48 @@ def test_two_ranks_dense_shard_marker_combines(gpu):
     assert parts0 == parts1 and parts0[0] == marker and parts0[1] == bytes(32)
     assert total0 == total1 == marker and not id0 and not id1
     assert not ok0 and ok1 and exact0 and exact1
+
+
+def _rccl_worker(port, q):
+    """World 1 over the "nccl" backend (RCCL): the collective bench.py's N > 1 RLC path runs,
+    on the one GPU of the box (RCCL cannot put two ranks on one device)."""
+    sys.path.insert(0, os.path.join(ROOT, "chaum-pedersen-zkp_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    import chaum_pedersen as cp
+    from chaum_pedersen.shard import all_gather_partials
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        gpu = cp.Gpu(0)
+        rows = _rows(gpu)
+        d = {k: torch.from_numpy(v.copy()).cuda() for k, v in rows.items()}
+        st = torch.empty(N, dtype=torch.uint8, device="cuda:0")
+        partial, ok = gpu.verify_batch_device(d["y1"], d["y2"], d["r1"], d["r2"], d["s"], st, bytes(range(32)),
+                                              fallback=True)
+        parts = all_gather_partials(partial)
+        total, ident = gpu.combine_partials(parts)
+        q.put((dist.get_backend(), parts, partial, total, ident, ok))
+        gpu.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_all_gather_of_partials_world_one(gpu):
+    """all_gather_partials' RCCL branch (device tensors, "nccl" backend) -- the exchange of
+    configs[3]'s per-GPU partials -- in a world of one rank: the gathered list is the rank's own
+    HIP partial, and combining it gives it back."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    backend, parts, partial, total, ident, ok = q.get(timeout=240)
+    p.join(timeout=60)
+    assert backend == "nccl"
+    assert parts == [partial] and total == partial and not ident and not ok
 
 
 @pytest.mark.parametrize("launcher", ["torchrun", "none"])
