@@ -113,7 +113,7 @@ constexpr int64_t kVarBaseMax = kQuadVerifyMax;
 constexpr int kQuadPhases = 9;
 // k_verify_small's stamps (CPZ_CLOCK_PROBE): wave 0 start, decoded, table, barrier A, Straus,
 // barrier B, verdict; wave 2 digits, [s'] B; 100 MHz at wave 0's start / end; wave 2's start.
-constexpr int kSmallStamps = 12;
+constexpr int kSmallStamps = 13;
 constexpr int64_t kQuadProofScratch = 2 * kQuadTableInts * 4;
 
 struct VerifyArgs {
@@ -179,6 +179,8 @@ hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st);
 // k_verify_small (kernels.hip): three waves per 8 proofs, the drop-in's latency path.  a.c null:
 // the challenges and response statuses are computed in the kernel from ca (k_challenge's inputs).
 hipError_t launch_verify_small(const VerifyArgs& a, const ChallengeArgs& ca, hipStream_t st);
+// one proof per workgroup of five waves, field products on 16-lane rows (fe16.h); no vtab
+hipError_t launch_verify_wide(const VerifyArgs& a, const ChallengeArgs& ca, hipStream_t st);
 int verify_each_blocks_per_cu();  // resident k_verify_each blocks per CU (occupancy API)
 hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st);
 hipError_t launch_prove_response(const ProveArgs& a, hipStream_t st);

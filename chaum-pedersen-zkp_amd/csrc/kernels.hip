@@ -33,6 +33,7 @@
 #include "scalarmul.h"
 #include "verify.h"
 #include "rlc_dev.h"
+#include "fe16.h"
 
 namespace cpz {
 
@@ -871,6 +872,85 @@ __global__ void __launch_bounds__(256) k_verify_quad(VerifyArgs a) {
 // challenges and response statuses were computed before (cpz_verify_response, or the
 // challenge kernel), wave 2 only splits.
 // ---------------------------------------------------------------------------------------
+// The transcript challenge, response checks, challenge split and digit words of proof ii
+// (k_verify_small's wave 2, k_verify_wide's wave 4): dig = u (0..3) and |v| (4..7) as radix-16
+// signed digits, s' = v s mod l (8..15) as radix-2^16 digits (radix-256 with variable-base
+// tables); meta bit 0 = v < 0, bits 8..15 = the response status.  With a.c the challenge and
+// status were computed before.  The fixed transcript schedules (no context, 32-byte context)
+// run on every lane; any other context runs the byte-wise sponge on the lanes with
+// `sponge_lane` set, on column `col` of the LDS image `sponge` (50 x ncols words) -- the other
+// lanes' results are then meaningless and the caller takes the sponge lane's from LDS.
+template <bool kWave = false>
+__device__ __forceinline__ void proof_digits(uint32_t dig[16], uint32_t& meta, const VerifyArgs& a,
+                                             const ChallengeArgs& ca, int64_t ii, bool sponge_lane,
+                                             uint32_t* sponge, int col, int ncols,
+                                             uint64_t* stamp_challenge = nullptr) {
+  uint32_t sw[8], cw[8];
+  load_words8(sw, a.s, ii);
+  uint8_t st_s;
+  if (a.c) {
+    load_words8(cw, a.c, ii);
+    st_s = a.status[ii];
+  } else {
+    uint32_t y1[8], y2[8], r1[8], r2[8];
+    load_words8(y1, a.y1, ii);
+    load_words8(y2, a.y2, ii);
+    load_words8(r1, a.r1, ii);
+    load_words8(r2, a.r2, ii);
+    const bool has_ctx = ca.ctx_off != nullptr && (ca.ctx_present == nullptr || ca.ctx_present[ii] != 0);
+    const uint64_t b0 = has_ctx ? ca.ctx_off[ii] : 0, b1 = has_ctx ? ca.ctx_off[ii + 1] : 0;
+    const bool fixed_noctx = !has_ctx && ca.fast_noctx;
+    const bool fixed_ctx32 = has_ctx && ca.fast_ctx32 && b1 - b0 == 32 &&
+                             ((reinterpret_cast<uintptr_t>(ca.ctx_bytes) + b0) & 3) == 0;
+    sc c;
+    if (fixed_noctx) {
+      c = challenge_fixed(reinterpret_cast<const uint32_t*>(ca.prefix[1].state), ca.k1, ca.k2, y1, y2, r1, r2);
+    } else if (fixed_ctx32) {
+      uint32_t cx[8];
+      const uint32_t* cp = reinterpret_cast<const uint32_t*>(ca.ctx_bytes + b0);
+#pragma unroll
+      for (int k = 0; k < 8; k++) cx[k] = cp[k];
+      c = challenge_fixed_ctx32(reinterpret_cast<const uint32_t*>(ca.prefix[0].state), ca.c32, cx, y1, y2, r1, r2);
+    } else {
+      for (int k = 0; k < 8; k++) c.w[k] = 0;
+      if (sponge_lane) {
+        LdsState lst{sponge, col, ncols};
+        const StrobeSnap& snap = ca.prefix[has_ctx ? 0 : 1];
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(snap.state);
+        for (int k = 0; k < 50; k++) sponge[k * ncols + col] = src[k];
+        Strobe<LdsState> st(lst, snap.pos, snap.pos_begin, (uint8_t)snap.flags);
+        if (has_ctx) {
+          transcript_context(st, ca.ctx_bytes + b0, (uint32_t)(b1 - b0));
+          transcript_parameters(st, ca.gh_words, ca.gh_words + 8);
+        }
+        c = transcript_challenge(st, y1, y2, r1, r2);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) cw[k] = c.w[k];
+    st_s = response_status(sw, ca.eq_only != 0);
+  }
+  if (stamp_challenge) *stamp_challenge = __builtin_amdgcn_s_memtime();  // timing builds only
+  bool vneg;
+  uint32_t u[4], va[4];
+  sc_half_split<kWave>(cw, u, va, vneg);
+  sc_recode_radix16_half(dig, u);
+  sc_recode_radix16_half(dig + 4, va);
+  sc vs, ss;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    vs.w[k] = k < 4 ? va[k] : 0u;
+    ss.w[k] = sw[k];
+  }
+  sc sp = sc_mul(vs, ss);
+  if (vneg) sp = sc_neg(sp);
+  if (a.vtab)
+    sc_recode_radix256(dig + 8, sp.w);
+  else
+    sc_recode_radix65536(dig + 8, sp.w);
+  meta = (vneg ? 1u : 0u) | ((uint32_t)st_s << 8);
+}
+
 constexpr int kSmallProofs = 8;  // proofs per workgroup (3 waves of 64 lanes)
 
 struct SmallShared {
@@ -943,82 +1023,14 @@ __global__ void __launch_bounds__(64 * 3) k_verify_small(VerifyArgs a, Challenge
     if (w == 0) CPZ_SMALL_STAMP(4);
   } else {
     // ---- wave 2: challenge, response checks, split, digits ------------------------------
-    uint32_t sw[8], cw[8];
-    load_words8(sw, a.s, ii);
-    uint8_t st_s;
-    if (a.c) {
-      load_words8(cw, a.c, ii);
-      st_s = a.status[ii];
-    } else {
-      uint32_t y1[8], y2[8], r1[8], r2[8];
-      load_words8(y1, a.y1, ii);
-      load_words8(y2, a.y2, ii);
-      load_words8(r1, a.r1, ii);
-      load_words8(r2, a.r2, ii);
-      const bool has_ctx = ca.ctx_off != nullptr && (ca.ctx_present == nullptr || ca.ctx_present[ii] != 0);
-      const uint64_t b0 = has_ctx ? ca.ctx_off[ii] : 0, b1 = has_ctx ? ca.ctx_off[ii + 1] : 0;
-      const bool fixed_noctx = !has_ctx && ca.fast_noctx;
-      const bool fixed_ctx32 = has_ctx && ca.fast_ctx32 && b1 - b0 == 32 &&
-                               ((reinterpret_cast<uintptr_t>(ca.ctx_bytes) + b0) & 3) == 0;
-      sc c;
-      if (fixed_noctx) {
-        c = challenge_fixed(reinterpret_cast<const uint32_t*>(ca.prefix[1].state), ca.k1, ca.k2, y1, y2, r1, r2);
-      } else if (fixed_ctx32) {
-        uint32_t cx[8];
-        const uint32_t* cp = reinterpret_cast<const uint32_t*>(ca.ctx_bytes + b0);
-#pragma unroll
-        for (int k = 0; k < 8; k++) cx[k] = cp[k];
-        c = challenge_fixed_ctx32(reinterpret_cast<const uint32_t*>(ca.prefix[0].state), ca.c32, cx, y1, y2, r1, r2);
-      } else {
-        // any other context: the byte-wise sponge, on the proof's first lane (LDS column j)
-        for (int k = 0; k < 8; k++) c.w[k] = 0;
-        if ((l & 7) == 0) {
-          LdsState lst{&sh.sponge[0][0], j, kSmallProofs};
-          const StrobeSnap& snap = ca.prefix[has_ctx ? 0 : 1];
-          const uint32_t* src = reinterpret_cast<const uint32_t*>(snap.state);
-          for (int k = 0; k < 50; k++) sh.sponge[k][j] = src[k];
-          Strobe<LdsState> st(lst, snap.pos, snap.pos_begin, (uint8_t)snap.flags);
-          if (has_ctx) {
-            transcript_context(st, ca.ctx_bytes + b0, (uint32_t)(b1 - b0));
-            transcript_parameters(st, ca.gh_words, ca.gh_words + 8);
-          }
-          c = transcript_challenge(st, y1, y2, r1, r2);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 8; k++) cw[k] = c.w[k];
-      st_s = response_status(sw, ca.eq_only != 0);
-    }
-    uint32_t ud[4], vd[4], sd[8];
-    bool vneg;
-    {
-      uint32_t u[4], va[4];
-      sc_half_split(cw, u, va, vneg);
-      sc_recode_radix16_half(ud, u);
-      sc_recode_radix16_half(vd, va);
-      sc vs, ss;
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        vs.w[k] = k < 4 ? va[k] : 0u;
-        ss.w[k] = sw[k];
-      }
-      sc sp = sc_mul(vs, ss);
-      if (vneg) sp = sc_neg(sp);
-      if (a.vtab)
-        sc_recode_radix256(sd, sp.w);
-      else
-        sc_recode_radix65536(sd, sp.w);
-    }
+    uint32_t dg[16], meta;
+    proof_digits(dg, meta, a, ca, ii, (l & 7) == 0, &sh.sponge[0][0], j, kSmallProofs);
     if ((l & 7) == 0) {
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        sh.dig[j][k] = ud[k];
-        sh.dig[j][4 + k] = vd[k];
-      }
-#pragma unroll
-      for (int k = 0; k < 8; k++) sh.dig[j][8 + k] = sd[k];
-      sh.meta[j] = (vneg ? 1u : 0u) | ((uint32_t)st_s << 8);
+      for (int k = 0; k < 16; k++) sh.dig[j][k] = dg[k];
+      sh.meta[j] = meta;
     }
+    uint32_t sd[8];
     CPZ_SMALL_STAMP(7);
     __syncthreads();  // A
     // the digits as the proof's first lane wrote them (its lanes differ on the byte-wise path)
@@ -1086,6 +1098,199 @@ hipError_t launch_verify_small(const VerifyArgs& a, const ChallengeArgs& ca, hip
   if (a.pre || a.blocks) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_verify_small, dim3((unsigned)((a.n + kSmallProofs - 1) / kSmallProofs)), dim3(64 * 3), 0, st,
                      a, ca);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// k_verify_wide: the drop-in's calls of a few proofs, one proof per workgroup of five waves
+// and every field product spread over a 16-lane row (fe16.h): a lone wave's product takes
+// ~145 ns there against ~220 ns on one lane, and a point operation is two such stages
+// (the four products of each on the four rows) instead of eight products on a quad.
+//   waves 0..3  chain c = 2 e + R of equation e: decode Y_e (R_e) -- every row the same --,
+//               its table of 9 cached multiples in LDS (of -Y, or of +R), then the
+//               half-length Straus loop [u] (-Y) or [|v|] (-+R) (k_verify_small's waves 0/1)
+//   wave 4      the challenge, response checks, split and digits (proof_digits), then
+//               [s'] B of both equations from the comb on two quads, as canonical words
+// Barrier A: the digits.  Barrier B: the R chains' sums and [s'] B; waves 0 and 2 add their
+// equation's three sums and test the identity.  Barrier C: wave 0 writes the status with
+// verify_proof's precedence.  Custom generators (VerifyArgs::vtab) take k_verify_small.
+// ---------------------------------------------------------------------------------------
+struct WideShared {
+  uint32_t dig[16];            // u (0..3), |v| (4..7), s' (8..15) digit words
+  uint32_t meta;               // bit 0: v < 0; bits 8..15: response status
+  int32_t tab[4][9][4][16];    // chain, multiple 0..8, field (Y+X, Y-X, Z, 2dT), limb
+  int32_t part[4][4][16];      // the R chains' sums: X, Y, Z, T limbs
+  uint32_t sB[2][4][8];        // [s'] B of each equation: canonical words of X, Y, Z, T
+  uint32_t bad[4];             // decode failure per chain
+  uint32_t rid[2];             // R_e encodes the identity
+  uint32_t eq[2];              // equation e holds
+  uint32_t sponge[50];         // byte-wise transcript image (contexts off the fixed schedules)
+};
+
+__global__ void __launch_bounds__(64 * 5) k_verify_wide(VerifyArgs a, ChallengeArgs ca) {
+  __shared__ WideShared sh;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t i = blockIdx.x;
+  const r16::Lane L = r16::lane_of(l);
+  r16::P4 acc = r16::identity(L);
+#if defined(CPZ_CLOCK_PROBE)
+  // timing builds only: shader-clock stamps of block 0 (wave 0 lane 0: start, decoded, table,
+  // barrier A, Straus, barrier B, identity test, end; wave 4 lane 0: digits, [s'] B,
+  // challenge (12)) and the 100 MHz clock at wave 0's start and end (10, 11) -> a.clock_probe
+  uint64_t* const stamps = (a.clock_probe && blockIdx.x == 0 && l == 0 && (w == 0 || w == 4)) ? a.clock_probe : nullptr;
+#define CPZ_WIDE_STAMP(k) do { if (stamps) stamps[k] = __builtin_amdgcn_s_memtime(); } while (0)
+  if (stamps && w == 0) stamps[10] = __builtin_amdgcn_s_memrealtime();
+  if (w == 0) CPZ_WIDE_STAMP(0);
+#else
+#define CPZ_WIDE_STAMP(k) (void)0
+#endif
+  if (w < 4) {
+    const int e = w >> 1;
+    const bool isR = (w & 1) != 0;
+    const uint32_t* src = isR ? (e ? a.r2 : a.r1) : (e ? a.y2 : a.y1);
+    uint32_t wu[8];
+    load_words8(wu, src, i);
+    r16::P4 P;
+    const bool ok = r16::decode(P, src + 8 * i, wu, L);
+    if (w == 0) CPZ_WIDE_STAMP(1);
+    if (l == 0) {
+      sh.bad[w] = ok ? 0u : 1u;
+      if (isR) sh.rid[e] = words8_zero(wu) ? 1u : 0u;
+    }
+    if (!isR) P = r16::neg(P);
+    // table: entry j = cached(j P), j = 0..8; row r stores field r
+    int32_t* tab = &sh.tab[w][0][0][0];
+    const int slot = L.row * 16 + L.k;
+    tab[slot] = L.row == 3 ? 0 : r16::one(L);  // identity: Y+X = Y-X = Z = 1, 2dT = 0
+    const r16::C4 c1 = r16::to_cached(P, L);
+    tab[64 + slot] = r16::sel4(c1.ypx, c1.ymx, c1.z, c1.t2d, L);
+    r16::P4 M = r16::dbl(P, L);
+#pragma unroll 1
+    for (int j = 2; j <= 8; j++) {
+      if (j > 2) M = r16::add_b(M, r16::cached_b(c1, false, L), L);
+      const r16::C4 cj = r16::to_cached(M, L);
+      tab[64 * j + slot] = r16::sel4(cj.ypx, cj.ymx, cj.z, cj.t2d, L);
+    }
+    if (w == 0) CPZ_WIDE_STAMP(2);
+    __syncthreads();  // A: digits
+    if (w == 0) CPZ_WIDE_STAMP(3);
+    uint32_t d[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) d[k] = sh.dig[(isR ? 4 : 0) + k];
+    // R chains: [|v|] (v < 0 ? R : -R) = -[v] R from the table of +R
+    const bool flip = isR && !(sh.meta & 1u);
+    // the field row r reads for +C: Y-X, Y+X, 2dT, Z; for -C: Y+X, Y-X, -2dT, Z
+    const int fpos = L.row == 0 ? 1 : (L.row == 1 ? 0 : (L.row == 2 ? 3 : 2));
+    const int fneg = L.row == 0 ? 0 : (L.row == 1 ? 1 : fpos);
+#pragma unroll 1
+    for (int jj = 0; jj < 4; jj++) {
+      const uint32_t wd = d[3 - jj];
+#pragma unroll 1
+      for (int m = 7; m >= 0; m--) {
+        int dd = ((int32_t)(wd << (28 - 4 * m))) >> 28;
+        dd = flip ? -dd : dd;
+        const bool ng = dd < 0;
+        const int ad = ng ? -dd : dd;
+        int b = tab[64 * ad + 16 * (ng ? fneg : fpos) + L.k];
+        b = (ng && L.row == 2) ? -b : b;
+        if (jj != 0 || m != 7) {
+          acc = r16::dbl(acc, L);
+          acc = r16::dbl(acc, L);
+          acc = r16::dbl(acc, L);
+          acc = r16::dbl(acc, L);
+        }
+        acc = r16::add_b(acc, b, L);
+      }
+    }
+    if (isR) sh.part[w][L.row][L.k] = r16::sel4(acc.X, acc.Y, acc.Z, acc.T, L);
+    if (w == 0) CPZ_WIDE_STAMP(4);
+  } else {
+    // ---- wave 4: challenge, response checks, split, digits; then [s'] B per equation ----------
+    uint32_t dg[16], meta;
+#if defined(CPZ_CLOCK_PROBE)
+    proof_digits<true>(dg, meta, a, ca, i, l == 0, sh.sponge, 0, 1, stamps ? stamps + 12 : nullptr);
+#else
+    proof_digits<true>(dg, meta, a, ca, i, l == 0, sh.sponge, 0, 1);
+#endif
+    if (l == 0) {
+#pragma unroll
+      for (int k = 0; k < 16; k++) sh.dig[k] = dg[k];
+      sh.meta = meta;
+    }
+    CPZ_WIDE_STAMP(8);
+    __syncthreads();  // A
+    if (l < 8) {
+      const int e = l >> 2, q = l & 3;
+      uint32_t sd[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) sd[k] = sh.dig[8 + k];
+      const CombTable comb{a.comb + (e ? kCombPerBase : 0)};
+      ge_p3 B = ge_identity();
+#pragma unroll 1
+      for (int k = 0; k < 16; k++) {
+        const int dgt = (int32_t)(sd[k >> 1] << (16 - 16 * (k & 1))) >> 16;
+        const ge_niels nl = comb.lookup(k, dgt);
+        ge_cached cc;
+        cc.YpX = nl.ypx;
+        cc.YmX = nl.ymx;
+        cc.T2d = nl.xy2d;
+        cc.Z = fe_one();
+        B = ge_add_quad(B, cc, q);
+      }
+      if (q == 0) {
+        fe_towords(sh.sB[e][0], B.X);
+        fe_towords(sh.sB[e][1], B.Y);
+        fe_towords(sh.sB[e][2], B.Z);
+        fe_towords(sh.sB[e][3], B.T);
+      }
+    }
+    CPZ_WIDE_STAMP(9);
+  }
+  __syncthreads();  // B: the R chains' sums, [s'] B
+  if (w == 0) CPZ_WIDE_STAMP(5);
+  if (w == 0 || w == 2) {
+    // Q_e = [u] (-Y_e) + (-[v] R_e) + [s'] B_e, identity (mod E[4])
+    const int e = w >> 1;
+    r16::P4 R;
+    R.X = sh.part[w + 1][0][L.k];
+    R.Y = sh.part[w + 1][1][L.k];
+    R.Z = sh.part[w + 1][2][L.k];
+    R.T = sh.part[w + 1][3][L.k];
+    acc = r16::add_b(acc, r16::cached_b(r16::to_cached(R, L), false, L), L);
+    r16::P4 S;
+    S.X = r16::limb_of(sh.sB[e][0], L);
+    S.Y = r16::limb_of(sh.sB[e][1], L);
+    S.Z = r16::limb_of(sh.sB[e][2], L);
+    S.T = r16::limb_of(sh.sB[e][3], L);
+    acc = r16::add_b(acc, r16::cached_b(r16::to_cached(S, L), false, L), L);
+    const bool eq = r16::is_identity(acc);
+    if (l == 0) sh.eq[e] = eq ? 1u : 0u;
+    if (w == 0) CPZ_WIDE_STAMP(6);
+  }
+  __syncthreads();  // C
+  if (threadIdx.x != 0) return;
+  const bool bad = (sh.bad[0] | sh.bad[1] | sh.bad[2] | sh.bad[3]) != 0;
+  const bool rid = (sh.rid[0] | sh.rid[1]) != 0;
+  const uint8_t st_s = (uint8_t)(sh.meta >> 8);
+  uint8_t st;
+  if (bad) st = kStBadPoint;
+  else if (st_s == kStBadScalar) st = kStBadScalar;
+  else if (rid && !a.eq_only) st = kStIdentity;
+  else if (st_s == kStZeroS) st = kStZeroS;
+  else if (st_s == kStBadChallenge) st = kStBadScalar;
+  else st = (sh.eq[0] & sh.eq[1]) ? kStOk : kStEqFail;
+  a.status[i] = st;
+#if defined(CPZ_CLOCK_PROBE)
+  CPZ_WIDE_STAMP(7);
+  if (stamps) stamps[11] = __builtin_amdgcn_s_memrealtime();
+#endif
+#undef CPZ_WIDE_STAMP
+}
+
+hipError_t launch_verify_wide(const VerifyArgs& a, const ChallengeArgs& ca, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  if (a.pre || a.blocks || a.vtab) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_verify_wide, dim3((unsigned)a.n), dim3(64 * 5), 0, st, a, ca);
   return hipGetLastError();
 }
 

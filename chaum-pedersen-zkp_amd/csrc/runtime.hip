@@ -70,25 +70,27 @@ struct DevBuf {
   }
 };
 
-// Page-locked host memory (hipHostMalloc), grown on demand.
+// Page-locked host memory (hipHostMalloc), grown on demand; dp = its device view.
 struct PinnedBuf {
   void* p = nullptr;
+  void* dp = nullptr;
   size_t cap = 0;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
     if (p) {
       hipError_t e = hipHostFree(p);
-      p = nullptr;
+      p = dp = nullptr;
       cap = 0;
       if (e != hipSuccess) return e;
     }
     hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&dp, p, 0);
     if (e == hipSuccess) cap = bytes;
     return e;
   }
   void release() {
     if (p) (void)hipHostFree(p);
-    p = nullptr;
+    p = dp = nullptr;
     cap = 0;
   }
 };
@@ -489,6 +491,29 @@ int verify_grid(cpz_ctx* ctx, size_t n) {
 #define CPZ_SMALL_MAX 2048
 #endif
 constexpr int64_t kSmallMax = CPZ_SMALL_MAX;
+// Launches of at most wide_max() proofs (default CPZ_WIDE_MAX, environment CPZ_WIDE_MAX for
+// measurement) take k_verify_wide: a workgroup of five waves per proof, field products on
+// 16-lane rows -- the shortest chain for a few proofs; custom generators stay on k_verify_small.
+#ifndef CPZ_WIDE_MAX
+#define CPZ_WIDE_MAX 512
+#endif
+// Synchronous host-buffer calls of at most kSmallMax proofs read their page-locked inputs and
+// write their statuses in place (PinnedBuf::dp) instead of copying both ways on the stream;
+// CPZ_ZERO_COPY=0 restores the copies.
+bool zero_copy() {
+  static const bool v = [] {
+    const char* e = std::getenv("CPZ_ZERO_COPY");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+int64_t wide_max() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("CPZ_WIDE_MAX");
+    return e ? (int64_t)std::atoll(e) : (int64_t)CPZ_WIDE_MAX;
+  }();
+  return v;
+}
 #ifndef CPZ_VERIFY_CHUNK_DIV
 #define CPZ_VERIFY_CHUNK_DIV 2
 #endif
@@ -562,7 +587,10 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
         v.c = nullptr;  // computed in the kernel
       }
       StageTimer t(ctx, stage, sc);
-      CPZ_HIP(cpz::launch_verify_small(v, cc, sc));
+      if (v.n <= wide_max() && !v.vtab)
+        CPZ_HIP(cpz::launch_verify_wide(v, cc, sc));
+      else
+        CPZ_HIP(cpz::launch_verify_small(v, cc, sc));
       continue;
     }
     if (ca) {
@@ -643,9 +671,14 @@ constexpr size_t kPinMail = 256;                  // mailbox bytes at the start 
 constexpr size_t kPinStageMax = size_t(8) << 20;  // larger inputs: one pageable copy per row
 inline size_t pad16(size_t x) { return (x + 15) & ~size_t(15); }
 
+// direct (a small synchronous call, zero_copy()): the kernels read the page-locked block
+// itself through its device view -- no copy on the stream -- and *status_dev / *status_host
+// point at n status bytes after it, which the kernels write the same way.
 int stage_inputs(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], int count, const uint8_t* ctx_bytes,
                  const uint64_t* ctx_off, const uint8_t* ctx_present, const void* dev[5], const void** dcb,
-                 const uint64_t** dco, const uint8_t** dcp) {
+                 const uint64_t** dco, const uint8_t** dcp, bool direct = false, uint8_t** status_dev = nullptr,
+                 uint8_t** status_host = nullptr) {
+  if (status_dev) *status_dev = nullptr;
   if (ctx_off)
     for (size_t i = 0; i < n; i++)
       if (ctx_off[i + 1] < ctx_off[i]) return fail(CPZ_EINVAL, "ctx_off must be non-decreasing");
@@ -667,8 +700,14 @@ int stage_inputs(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], int count
       if (ctx_present) std::memcpy(h + o_pres, ctx_present, n);
       if (nbytes) std::memcpy(h + o_ctx, ctx_bytes + ctx_off[0], nbytes);
     }
-    if (total) CPZ_HIP(hipMemcpyAsync(ctx->in_all.p, h, total, hipMemcpyHostToDevice, ctx->stream));
     uint8_t* d = static_cast<uint8_t*>(ctx->in_all.p);
+    if (direct && status_dev && status_host && ctx->pin.dp) {
+      d = static_cast<uint8_t*>(ctx->pin.dp) + kPinMail;
+      *status_dev = d + total;
+      *status_host = h + total;
+    } else if (total) {
+      CPZ_HIP(hipMemcpyAsync(ctx->in_all.p, h, total, hipMemcpyHostToDevice, ctx->stream));
+    }
     for (int k = 0; k < count; k++) dev[k] = d + (size_t)k * n * 32;
     *dcb = ctx_off ? d + o_ctx : nullptr;
     *dco = ctx_off ? reinterpret_cast<const uint64_t*>(d + o_off) : nullptr;
@@ -1566,7 +1605,7 @@ int cpz_ctx_create_timing_only(int device_ordinal, cpz_ctx** out) { return ctx_c
 // partitioned check's first pass, k_part_acc (kernel 2) launch: up to max_waves records of 5
 // words (a wave that did no work leaves zeros); *got = the launch's waves.  Kernel 3: the last
 // k_verify_quad launch's kQuadPhases phase stamps (one 72-byte record; max_waves counts 40-byte
-// records, so pass at least 2; k_verify_small's kSmallStamps words when it ran instead).  Exported by CPZ_CLOCK_PROBE builds alone
+// records, so pass at least 2; k_verify_small's or k_verify_wide's kSmallStamps words when one of them ran instead).  Exported by CPZ_CLOCK_PROBE builds alone
 // (tools/time_verify.py MODE=rlc / MODE=c5, tools/quad_phases.py).
 int cpz_ctx_clock_probe(cpz_ctx* ctx, int kernel, uint64_t* out, size_t max_waves, size_t* got) {
   if (!ctx || !out || !got || kernel < 0 || kernel > 3) return fail(CPZ_EINVAL, "bad arguments");
@@ -2050,8 +2089,17 @@ int cpz_verify_each_ex(cpz_ctx* ctx, uint32_t flags, const uint8_t g[32], const 
   const void* dcb;
   const uint64_t* dco;
   const uint8_t* dcp;
-  rc = stage_inputs(ctx, n, host, 5, ctx_bytes, ctx_off, ctx_present, dev, &dcb, &dco, &dcp);
+  uint8_t *st_dev = nullptr, *st_host = nullptr;
+  rc = stage_inputs(ctx, n, host, 5, ctx_bytes, ctx_off, ctx_present, dev, &dcb, &dco, &dcp,
+                    zero_copy() && (int64_t)n <= kSmallMax, &st_dev, &st_host);
   if (rc) return rc;
+  if (st_dev) {  // zero-copy: inputs read and statuses written through the page-locked block
+    rc = enqueue_verify(ctx, n, dev[0], dev[1], dev[2], dev[3], dev[4], dcb, dco, dcp, st_dev, ctx->stream);
+    if (rc) return rc;
+    CPZ_HIP(hipStreamSynchronize(ctx->stream));
+    std::memcpy(status_out, st_host, n);
+    return CPZ_OK;
+  }
   CPZ_HIP(ctx->st.ensure(n));
   rc = enqueue_verify(ctx, n, dev[0], dev[1], dev[2], dev[3], dev[4], dcb, dco, dcp,
                       static_cast<uint8_t*>(ctx->st.p), ctx->stream);

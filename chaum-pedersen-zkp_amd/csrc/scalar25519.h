@@ -395,6 +395,12 @@ CPZ_HD void half_split_step(uint32_t r0[8], uint32_t r1[8], uint32_t t0[8], uint
 // B - R >= e1 + e2 guarantee T <= r_full < previous r_full -- the quotient is the true
 // one and the batch never passes the first remainder below T.  The last steps (and any
 // huge quotient) go through the single-step path, so (u, v) is exactly the Euclid pair.
+//
+// kSmallQ (k_verify_wide, where a wave splits one challenge): the Lehmer quotients below 4
+// (74 % of them) come from compare-and-subtract instead of the f64 division, which on one
+// lane costs ~1 us per step; the same quotients, so the same (u, v).  The per-proof kernels
+// keep the division (their lanes' quotients diverge; every lane would pay both paths).
+template <bool kSmallQ = false>
 CPZ_HD void sc_half_split(const uint32_t c[8], uint32_t u[4], uint32_t vabs[4], bool& vneg) {
   uint32_t r0[8], r1[8], t0[8], t1[8];
 #pragma unroll
@@ -413,18 +419,30 @@ CPZ_HD void sc_half_split(const uint32_t c[8], uint32_t u[4], uint32_t vabs[4], 
     int steps = 0;
 #pragma unroll 1
     while (B != 0) {
-      const double qf = (double)A / (double)B;
-      if (qf >= 0x1p30) break;
-      uint64_t q = (uint64_t)qf;
-      uint64_t qb = q * B;
-      while (qb > A) {
-        q--;
-        qb -= B;
-      }
-      uint64_t R = A - qb;
-      while (R >= B) {
-        q++;
-        R -= B;
+      uint64_t q, R;
+      if (kSmallQ && A - B < B) {  // A >= B (r0 > r1 and the same shift)
+        q = 1;
+        R = A - B;
+      } else if (kSmallQ && A - B - B < B) {
+        q = 2;
+        R = A - B - B;
+      } else if (kSmallQ && A - B - B - B < B) {
+        q = 3;
+        R = A - B - B - B;
+      } else {
+        const double qf = (double)A / (double)B;
+        if (qf >= 0x1p30) break;
+        q = (uint64_t)qf;
+        uint64_t qb = q * B;
+        while (qb > A) {
+          q--;
+          qb -= B;
+        }
+        R = A - qb;
+        while (R >= B) {
+          q++;
+          R -= B;
+        }
       }
       const int64_t u2 = u0 - (int64_t)q * u1, v2 = v0 - (int64_t)q * v1;
       const int64_t au2 = u2 < 0 ? -u2 : u2, av2 = v2 < 0 ? -v2 : v2;

@@ -199,9 +199,11 @@ def _euclid_half(c):
     return r1, t1
 
 
-def test_half_split(lib):
+@pytest.mark.parametrize("fn", ["cpzt_half_split", "cpzt_half_split_smallq"])
+def test_half_split(lib, fn):
     """sc_half_split (csrc/scalar25519.h): v c = u (mod l), u, |v| < 3 * 2^125, and equal
-    to the exact Euclid values -- incl. huge partial quotients (the shifted-divisor path)."""
+    to the exact Euclid values -- incl. huge partial quotients (the shifted-divisor path) --
+    with the f64 quotients and with k_verify_wide's compare-and-subtract small quotients."""
     rng = random.Random(7)
     cases = [0, 1, 2, (3 << 125) - 1, 3 << 125, L - 1, L - 2, L // 2, L // 3, (L >> 70), (L >> 140) + 5,
              (L >> 126), (L >> 127) + 1, 2**252, (2**128 + 1) % L]
@@ -214,7 +216,7 @@ def test_half_split(lib):
             cases += [(base + d) % L for d in (-2, -1, 0, 1, 2, 1 << 20, rng.randrange(1 << 60))]
     u, v, neg = buf(16), buf(16), ctypes.c_int()
     for c in cases:
-        lib.cpzt_half_split(u, v, ctypes.byref(neg), c.to_bytes(32, "little"))
+        getattr(lib, fn)(u, v, ctypes.byref(neg), c.to_bytes(32, "little"))
         uu = fi(u.raw)
         vv = -fi(v.raw) if neg.value else fi(v.raw)
         assert (uu, vv) == _euclid_half(c), c
