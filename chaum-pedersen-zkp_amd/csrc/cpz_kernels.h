@@ -142,6 +142,8 @@ struct VerifyArgs {
                                     // runtime: kQuadVerifyMax, bounded by the slab's size)
   uint64_t* clock_probe = nullptr;  // CPZ_CLOCK_PROBE builds only: k_verify_quad's phase stamps
                                     // (kQuadPhases shader-clock words of block 0's first proof)
+  const int32_t* vtab16 = nullptr;  // the same tables as 16-bit limbs for k_verify_wide (fe16.h):
+                                    // [4 bases][128 entries][Y+X, Y-X, 2dxy][16 limbs]
   const ge_niels* vtab = nullptr;   // variable-base generators (no comb built for this (g, h)):
                                     // Niels multiples 1..128 of g, h, 2^128 g, 2^128 h
                                     // (k_build_niels), [s'] B from them inside the Straus loop;
@@ -172,6 +174,8 @@ bool challenge_prefix_is_ctx32(const StrobeSnap& snap);  // prefix[0]: the 32-by
 // Niels tables of 2 * nbases bases (nbases <= 8); `bases` is scratch for 2 * nbases ge_p3.
 hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, ge_p3* bases,
                               hipStream_t st);
+// The Niels tables' fields as canonical 16-bit limbs (VerifyArgs::vtab16): n entries.
+hipError_t launch_niels_r16(const ge_niels* tab, int32_t* out, int n, hipStream_t st);
 hipError_t launch_parse_proofs(const ParseArgs& a, hipStream_t st);
 // Fixed-base combs of 2 bases (g, h): bases_scratch holds 2 * kCombWindows ge_p3.
 hipError_t launch_build_comb(const uint32_t* gh_words, ge_p3* bases_scratch, ge_niels* comb, hipStream_t st);
@@ -179,7 +183,7 @@ hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st);
 // k_verify_small (kernels.hip): three waves per 8 proofs, the drop-in's latency path.  a.c null:
 // the challenges and response statuses are computed in the kernel from ca (k_challenge's inputs).
 hipError_t launch_verify_small(const VerifyArgs& a, const ChallengeArgs& ca, hipStream_t st);
-// one proof per workgroup of five waves, field products on 16-lane rows (fe16.h); no vtab
+// one proof per workgroup of five waves (six with vtab16), field products on 16-lane rows (fe16.h)
 hipError_t launch_verify_wide(const VerifyArgs& a, const ChallengeArgs& ca, hipStream_t st);
 int verify_each_blocks_per_cu();  // resident k_verify_each blocks per CU (occupancy API)
 hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st);

@@ -109,8 +109,12 @@ __device__ __forceinline__ void col_step_half(int64_t (&a)[4], int x, int y, int
 // the halves: 8 column steps per lane instead of 16.  Same bounds and result as mul.
 __device__ __forceinline__ int mul_pair(int x, int y, const Lane& L) {
   const bool hi = (L.row & 1) != 0;
-  const int xs = hi ? dpp0<0x128>(x) : x;                // row_ror:8: lane j holds x_(j+8)
-  const int ys = hi ? shifted<8>(y, y * 38) : y;
+  // DPP moves are convergent: computed on every lane, then selected (a conditional DPP
+  // becomes a divergent branch)
+  const int xr = dpp0<0x128>(x);                         // row_ror:8: lane j holds x_(j+8)
+  const int yr = shifted<8>(y, y * 38);
+  const int xs = hi ? xr : x;
+  const int ys = hi ? yr : y;
   int64_t a[4] = {0, 0, 0, 0};
   col_step_half<0>(a, xs, ys, ys * 38);
   const int64_t h = (a[0] + a[1]) + (a[2] + a[3]);

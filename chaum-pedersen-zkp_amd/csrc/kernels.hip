@@ -590,6 +590,23 @@ hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* 
   return hipGetLastError();
 }
 
+__global__ void k_niels_r16(const ge_niels* __restrict__ tab, int32_t* __restrict__ out, int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;  // entry * 3 + field
+  if (t >= 3 * n) return;
+  const ge_niels& e = tab[t / 3];
+  const int f = t % 3;
+  uint32_t w[8];
+  fe_towords(w, f == 0 ? e.ypx : (f == 1 ? e.ymx : e.xy2d));
+#pragma unroll
+  for (int k = 0; k < 16; k++) out[16 * t + k] = (int32_t)((w[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+}
+
+hipError_t launch_niels_r16(const ge_niels* tab, int32_t* out, int n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_niels_r16, dim3((3 * n + 255) / 256), dim3(256), 0, st, tab, out, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_build_comb(const uint32_t* gh_words, ge_p3* bases_scratch, ge_niels* comb, hipStream_t st) {
   hipLaunchKernelGGL(k_comb_bases, dim3(1), dim3(64), 0, st, gh_words, bases_scratch);
   hipLaunchKernelGGL(k_comb_fill, dim3((unsigned)((2 * kCombPerBase + 255) / 256)), dim3(256), 0, st,
@@ -904,13 +921,15 @@ __device__ __forceinline__ void proof_digits(uint32_t dig[16], uint32_t& meta, c
                              ((reinterpret_cast<uintptr_t>(ca.ctx_bytes) + b0) & 3) == 0;
     sc c;
     if (fixed_noctx) {
-      c = challenge_fixed(reinterpret_cast<const uint32_t*>(ca.prefix[1].state), ca.k1, ca.k2, y1, y2, r1, r2);
+      c = challenge_fixed(reinterpret_cast<const uint32_t*>(ca.prefix[1].state), ca.k1, ca.k2, y1, y2, r1,
+                                    r2);
     } else if (fixed_ctx32) {
       uint32_t cx[8];
       const uint32_t* cp = reinterpret_cast<const uint32_t*>(ca.ctx_bytes + b0);
 #pragma unroll
       for (int k = 0; k < 8; k++) cx[k] = cp[k];
-      c = challenge_fixed_ctx32(reinterpret_cast<const uint32_t*>(ca.prefix[0].state), ca.c32, cx, y1, y2, r1, r2);
+      c = challenge_fixed_ctx32(reinterpret_cast<const uint32_t*>(ca.prefix[0].state), ca.c32, cx, y1, y2,
+                                          r1, r2);
     } else {
       for (int k = 0; k < 8; k++) c.w[k] = 0;
       if (sponge_lane) {
@@ -933,7 +952,10 @@ __device__ __forceinline__ void proof_digits(uint32_t dig[16], uint32_t& meta, c
   if (stamp_challenge) *stamp_challenge = __builtin_amdgcn_s_memtime();  // timing builds only
   bool vneg;
   uint32_t u[4], va[4];
-  sc_half_split<kWave>(cw, u, va, vneg);
+  if (kWave)
+    sc_half_split32(cw, u, va, vneg);
+  else
+    sc_half_split(cw, u, va, vneg);
   sc_recode_radix16_half(dig, u);
   sc_recode_radix16_half(dig + 4, va);
   sc vs, ss;
@@ -1113,7 +1135,9 @@ hipError_t launch_verify_small(const VerifyArgs& a, const ChallengeArgs& ca, hip
 //               [s'] B of both equations from the comb on two quads, as canonical words
 // Barrier A: the digits.  Barrier B: the R chains' sums and [s'] B; waves 0 and 2 add their
 // equation's three sums and test the identity.  Barrier C: wave 0 writes the status with
-// verify_proof's precedence.  Custom generators (VerifyArgs::vtab) take k_verify_small.
+// verify_proof's precedence.  Custom generators (VerifyArgs::vtab16, the pair's Niels tables
+// as 16-bit limbs): waves 4 and 5 compute [s'] g and [s'] h on rows instead of the comb --
+// 16 radix-256 windows of s' on B and of s' >> 128 on 2^128 B, 120 doublings + 32 additions.
 // ---------------------------------------------------------------------------------------
 struct WideShared {
   uint32_t dig[16];            // u (0..3), |v| (4..7), s' (8..15) digit words
@@ -1121,13 +1145,51 @@ struct WideShared {
   int32_t tab[4][9][4][16];    // chain, multiple 0..8, field (Y+X, Y-X, Z, 2dT), limb
   int32_t part[4][4][16];      // the R chains' sums: X, Y, Z, T limbs
   uint32_t sB[2][4][8];        // [s'] B of each equation: canonical words of X, Y, Z, T
+  int32_t sBv[2][4][16];       // the same from the variable-base waves: X, Y, Z, T limbs
   uint32_t bad[4];             // decode failure per chain
   uint32_t rid[2];             // R_e encodes the identity
   uint32_t eq[2];              // equation e holds
   uint32_t sponge[50];         // byte-wise transcript image (contexts off the fixed schedules)
 };
 
-__global__ void __launch_bounds__(64 * 5) k_verify_wide(VerifyArgs a, ChallengeArgs ca) {
+__device__ __forceinline__ int niels16_b(const int32_t* t16, int d, const r16::Lane& L);
+
+// [s'] B_e on the rows from the pair's R16 Niels tables: 16 radix-256 windows of s' on B_e and
+// of s' >> 128 on 2^128 B_e (k_verify_small's wave-2 loop), sum to sh.sBv[e].
+template <class Shared>
+__device__ __forceinline__ void wide_varbase(Shared& sh, const VerifyArgs& a, int e, const r16::Lane& L) {
+  uint32_t sd[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) sd[k] = sh.dig[8 + k];
+  const int32_t* gt = a.vtab16 + (size_t)e * kNielsEntries * 48;
+  const int32_t* gt2 = a.vtab16 + (size_t)(2 + e) * kNielsEntries * 48;
+  r16::P4 acc = r16::identity(L);
+#pragma unroll 1
+  for (int b = 15; b >= 0; b--) {
+    const int dg = (int32_t)(sd[b >> 2] << (24 - 8 * (b & 3))) >> 24;
+    const int dg2 = (int32_t)(sd[4 + (b >> 2)] << (24 - 8 * (b & 3))) >> 24;
+    const int b1 = niels16_b(gt, dg, L), b2 = niels16_b(gt2, dg2, L);
+    if (b != 15) {
+#pragma unroll 1
+      for (int k = 0; k < 8; k++) acc = r16::dbl(acc, L);
+    }
+    acc = r16::add_b(acc, b1, L);
+    acc = r16::add_b(acc, b2, L);
+  }
+  sh.sBv[e][L.row][L.k] = r16::sel4(acc.X, acc.Y, acc.Z, acc.T, L);
+}
+
+// row r's first-stage operand for the Niels entry d (|d| <= 128) of an R16 table (k_niels_r16):
+// +: Y-X, Y+X, 2dxy, Z = 1;  -: Y+X, Y-X, -2dxy, 1;  0: the identity (1, 1, 0, 1)
+__device__ __forceinline__ int niels16_b(const int32_t* t16, int d, const r16::Lane& L) {
+  const bool ng = d < 0;
+  const int ad = ng ? -d : d;
+  const int f = L.row == 0 ? (ng ? 0 : 1) : (L.row == 1 ? (ng ? 1 : 0) : 2);
+  int v = (ad == 0 || L.row == 3) ? (L.row == 2 ? 0 : r16::one(L)) : t16[((ad - 1) * 3 + f) * 16 + L.k];
+  return (ng && L.row == 2 && ad != 0) ? -v : v;
+}
+
+__global__ void __launch_bounds__(64 * 6) k_verify_wide(VerifyArgs a, ChallengeArgs ca) {
   __shared__ WideShared sh;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int64_t i = blockIdx.x;
@@ -1204,7 +1266,7 @@ __global__ void __launch_bounds__(64 * 5) k_verify_wide(VerifyArgs a, ChallengeA
     }
     if (isR) sh.part[w][L.row][L.k] = r16::sel4(acc.X, acc.Y, acc.Z, acc.T, L);
     if (w == 0) CPZ_WIDE_STAMP(4);
-  } else {
+  } else if (w == 4) {
     // ---- wave 4: challenge, response checks, split, digits; then [s'] B per equation ----------
     uint32_t dg[16], meta;
 #if defined(CPZ_CLOCK_PROBE)
@@ -1219,7 +1281,9 @@ __global__ void __launch_bounds__(64 * 5) k_verify_wide(VerifyArgs a, ChallengeA
     }
     CPZ_WIDE_STAMP(8);
     __syncthreads();  // A
-    if (l < 8) {
+    if (a.vtab16) {
+      wide_varbase(sh, a, 0, L);
+    } else if (l < 8) {
       const int e = l >> 2, q = l & 3;
       uint32_t sd[8];
 #pragma unroll
@@ -1245,6 +1309,10 @@ __global__ void __launch_bounds__(64 * 5) k_verify_wide(VerifyArgs a, ChallengeA
       }
     }
     CPZ_WIDE_STAMP(9);
+  } else {
+    // ---- wave 5 (variable bases): [s'] h of equation 1 ------------------------------------------
+    __syncthreads();  // A
+    wide_varbase(sh, a, 1, L);
   }
   __syncthreads();  // B: the R chains' sums, [s'] B
   if (w == 0) CPZ_WIDE_STAMP(5);
@@ -1258,10 +1326,17 @@ __global__ void __launch_bounds__(64 * 5) k_verify_wide(VerifyArgs a, ChallengeA
     R.T = sh.part[w + 1][3][L.k];
     acc = r16::add_b(acc, r16::cached_b(r16::to_cached(R, L), false, L), L);
     r16::P4 S;
-    S.X = r16::limb_of(sh.sB[e][0], L);
-    S.Y = r16::limb_of(sh.sB[e][1], L);
-    S.Z = r16::limb_of(sh.sB[e][2], L);
-    S.T = r16::limb_of(sh.sB[e][3], L);
+    if (a.vtab16) {
+      S.X = sh.sBv[e][0][L.k];
+      S.Y = sh.sBv[e][1][L.k];
+      S.Z = sh.sBv[e][2][L.k];
+      S.T = sh.sBv[e][3][L.k];
+    } else {
+      S.X = r16::limb_of(sh.sB[e][0], L);
+      S.Y = r16::limb_of(sh.sB[e][1], L);
+      S.Z = r16::limb_of(sh.sB[e][2], L);
+      S.T = r16::limb_of(sh.sB[e][3], L);
+    }
     acc = r16::add_b(acc, r16::cached_b(r16::to_cached(S, L), false, L), L);
     const bool eq = r16::is_identity(acc);
     if (l == 0) sh.eq[e] = eq ? 1u : 0u;
@@ -1289,8 +1364,8 @@ __global__ void __launch_bounds__(64 * 5) k_verify_wide(VerifyArgs a, ChallengeA
 
 hipError_t launch_verify_wide(const VerifyArgs& a, const ChallengeArgs& ca, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;
-  if (a.pre || a.blocks || a.vtab) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_verify_wide, dim3((unsigned)a.n), dim3(64 * 5), 0, st, a, ca);
+  if (a.pre || a.blocks || (a.vtab && !a.vtab16) || (!a.vtab && !a.comb)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_verify_wide, dim3((unsigned)a.n), dim3(64 * (a.vtab16 ? 6 : 5)), 0, st, a, ca);
   return hipGetLastError();
 }
 

@@ -175,6 +175,7 @@ struct GenSet {
   uint64_t used = 0;  // LRU stamp
   uint8_t gh[64];
   DevBuf tab;       // 4 x 128 ge_niels (g, h, 2^128 g, 2^128 h)
+  DevBuf tab16;     // the same as 16-bit limbs (k_verify_wide's variable bases)
   DevBuf comb;      // fixed-base combs of g and h: 2 x 16 x 2^15 ge_niels (128 MiB)
   DevBuf comb_q;    // 32 ge_p3: 2^(16 k) g, 2^(16 k) h
   DevBuf prefix;    // 2 StrobeSnap
@@ -184,7 +185,7 @@ struct GenSet {
   bool ctx32_fixed = false;   // prefix[0] at the fixed position: 32-byte contexts' fast path
   uint32_t chal_c32[3][50];   // its framing masks (g and h folded in)
   void release() {
-    for (DevBuf* b : {&tab, &comb, &comb_q, &prefix, &gh_words}) b->release();
+    for (DevBuf* b : {&tab, &tab16, &comb, &comb_q, &prefix, &gh_words}) b->release();
     valid = false;
   }
 };
@@ -368,6 +369,9 @@ int build_niels_prefix(cpz_ctx* ctx, GenSet& e, const uint8_t both[64]) {
   CPZ_HIP(cpz::launch_build_niels(static_cast<const uint32_t*>(e.gh_words.p), 2, static_cast<cpz::ge_niels*>(e.tab.p),
                                   static_cast<int*>(ctx->ok_flags.p), static_cast<cpz::ge_p3*>(ctx->gen_bases.p),
                                   ctx->stream));
+  CPZ_HIP(e.tab16.ensure(4 * cpz::kNielsEntries * 48 * sizeof(int32_t)));
+  CPZ_HIP(cpz::launch_niels_r16(static_cast<const cpz::ge_niels*>(e.tab.p), static_cast<int32_t*>(e.tab16.p),
+                                4 * cpz::kNielsEntries, ctx->stream));
   CPZ_HIP(cpz::launch_transcript_prefix(static_cast<const uint32_t*>(e.gh_words.p),
                                         static_cast<cpz::StrobeSnap*>(e.prefix.p), ctx->stream));
   int ok[2] = {0, 0};
@@ -587,7 +591,7 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
         v.c = nullptr;  // computed in the kernel
       }
       StageTimer t(ctx, stage, sc);
-      if (v.n <= wide_max() && !v.vtab)
+      if (v.n <= wide_max() && (!v.vtab || v.vtab16))
         CPZ_HIP(cpz::launch_verify_wide(v, cc, sc));
       else
         CPZ_HIP(cpz::launch_verify_small(v, cc, sc));
@@ -656,6 +660,7 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
     if ((int64_t)n > cpz::kVarBaseMax) return fail(CPZ_EINVAL, "internal: variable-base call above kVarBaseMax");
     va.comb = nullptr;
     va.vtab = static_cast<const cpz::ge_niels*>(ctx->gs->tab.p);
+    va.vtab16 = static_cast<const int32_t*>(ctx->gs->tab16.p);
   }
   va.scratch = nullptr;  // set per launch
   va.eq_only = ca.eq_only;
@@ -2336,6 +2341,7 @@ int verify_response_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2,
     if ((int64_t)n > cpz::kVarBaseMax) return fail(CPZ_EINVAL, "internal: variable-base call above kVarBaseMax");
     va.comb = nullptr;
     va.vtab = static_cast<const cpz::ge_niels*>(ctx->gs->tab.p);
+    va.vtab16 = static_cast<const int32_t*>(ctx->gs->tab16.p);
   }
   va.scratch = nullptr;  // set per launch
   va.eq_only = ctx->call_eq ? 1 : 0;

@@ -395,12 +395,6 @@ CPZ_HD void half_split_step(uint32_t r0[8], uint32_t r1[8], uint32_t t0[8], uint
 // B - R >= e1 + e2 guarantee T <= r_full < previous r_full -- the quotient is the true
 // one and the batch never passes the first remainder below T.  The last steps (and any
 // huge quotient) go through the single-step path, so (u, v) is exactly the Euclid pair.
-//
-// kSmallQ (k_verify_wide, where a wave splits one challenge): the Lehmer quotients below 4
-// (74 % of them) come from compare-and-subtract instead of the f64 division, which on one
-// lane costs ~1 us per step; the same quotients, so the same (u, v).  The per-proof kernels
-// keep the division (their lanes' quotients diverge; every lane would pay both paths).
-template <bool kSmallQ = false>
 CPZ_HD void sc_half_split(const uint32_t c[8], uint32_t u[4], uint32_t vabs[4], bool& vneg) {
   uint32_t r0[8], r1[8], t0[8], t1[8];
 #pragma unroll
@@ -419,30 +413,18 @@ CPZ_HD void sc_half_split(const uint32_t c[8], uint32_t u[4], uint32_t vabs[4], 
     int steps = 0;
 #pragma unroll 1
     while (B != 0) {
-      uint64_t q, R;
-      if (kSmallQ && A - B < B) {  // A >= B (r0 > r1 and the same shift)
-        q = 1;
-        R = A - B;
-      } else if (kSmallQ && A - B - B < B) {
-        q = 2;
-        R = A - B - B;
-      } else if (kSmallQ && A - B - B - B < B) {
-        q = 3;
-        R = A - B - B - B;
-      } else {
-        const double qf = (double)A / (double)B;
-        if (qf >= 0x1p30) break;
-        q = (uint64_t)qf;
-        uint64_t qb = q * B;
-        while (qb > A) {
-          q--;
-          qb -= B;
-        }
-        R = A - qb;
-        while (R >= B) {
-          q++;
-          R -= B;
-        }
+      const double qf = (double)A / (double)B;
+      if (qf >= 0x1p30) break;
+      uint64_t q = (uint64_t)qf;
+      uint64_t qb = q * B;
+      while (qb > A) {
+        q--;
+        qb -= B;
+      }
+      uint64_t R = A - qb;
+      while (R >= B) {
+        q++;
+        R -= B;
       }
       const int64_t u2 = u0 - (int64_t)q * u1, v2 = v0 - (int64_t)q * v1;
       const int64_t au2 = u2 < 0 ? -u2 : u2, av2 = v2 < 0 ? -v2 : v2;
@@ -481,6 +463,96 @@ CPZ_HD void sc_half_split(const uint32_t c[8], uint32_t u[4], uint32_t vabs[4], 
   for (int j = 0; j < 4; j++) {
     u[j] = r1[j];
     // |t1| = vneg ? 0 - t1 : t1
+    const uint64_t d = (uint64_t)0 - t1[j] - borrow;
+    borrow = (uint32_t)(d >> 63);
+    vabs[j] = vneg ? (uint32_t)d : t1[j];
+  }
+}
+
+// 1 / x to ~1 ulp (v_rcp_f32 on the device; the correction steps below absorb the error).
+CPZ_HD float f32_rcp(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rcpf(x);
+#else
+  return 1.0f / x;
+#endif
+}
+
+// The same split with 31-bit Lehmer windows (k_verify_wide's wave 4, one challenge per wave).
+// On a lone wave sc_half_split's inner step -- 64-bit quotient, cofactor and exactness
+// arithmetic, each a chain of dependent 32-bit halves -- takes ~1000 shader cycles whatever
+// the quotient's source (tools/ubench/w4_parts.hip: 73 K cycles for ~72 steps).  Here a step is
+// 32-bit work: the quotient from an f32 reciprocal (exact after at most one correction for
+// q < 2^15), cofactors below 2^15, the same two exactness conditions (T / 2^sh rounded up),
+// so the same Euclid pair (u, v); twice the batches (~15 bits each), each batch the same four
+// 8-word rows.
+CPZ_HD void sc_half_split32(const uint32_t c[8], uint32_t u[4], uint32_t vabs[4], bool& vneg) {
+  uint32_t r0[8], r1[8], t0[8], t1[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    r0[j] = SC_L(j);
+    r1[j] = c[j];
+    t0[j] = 0;
+    t1[j] = j == 0 ? 1u : 0u;
+  }
+#pragma unroll 1
+  while (!half_below(r1)) {
+    const int sh = words8_bitlen(r0) - 31;  // r0 >= r1 >= T > 2^126: sh > 95
+    uint32_t A = (uint32_t)words8_extract64(r0, sh), B = (uint32_t)words8_extract64(r1, sh);
+    // ceil(T / 2^sh), T = 3 * 2^125
+    const uint32_t tsh = sh <= 125 ? (3u << (125 - sh)) : (sh == 126 ? 2u : 1u);
+    int32_t u0 = 1, v0 = 0, u1 = 0, v1 = 1;
+    int steps = 0;
+    // Each step is straight-line selects and ONE exit test: a lone wave pays ~40 cycles per
+    // divergent branch, and the step's five early exits were most of its time.
+#pragma unroll 1
+    for (;;) {
+      // q = floor(A / B): the f32 estimate is within one of it for q < 2^15 (relative error
+      // < 2^-21); larger quotients (and B = 0) end the batch
+      const uint32_t qe = (uint32_t)((float)A * f32_rcp((float)(B | (B == 0u))));
+      const uint32_t qb0 = qe * B;  // <= A + B < 2^32 when qe is within one of q
+      const bool over = qb0 > A;
+      const uint32_t q1 = over ? qe - 1u : qe, qb = over ? qb0 - B : qb0;
+      const uint32_t R0 = A - qb;
+      const bool under = R0 >= B;
+      const uint32_t q = under ? q1 + 1u : q1, R = under ? R0 - B : R0;
+      const int32_t u2 = u0 - (int32_t)q * u1, v2 = v0 - (int32_t)q * v1;
+      const int32_t au2 = u2 < 0 ? -u2 : u2, av2 = v2 < 0 ? -v2 : v2;
+      const int32_t au1 = u1 < 0 ? -u1 : u1, av1 = v1 < 0 ? -v1 : v1;
+      const uint32_t e2 = (uint32_t)(au2 + av2) + 1, e1 = (uint32_t)(au1 + av1) + 1;
+      const bool go = (B != 0u) & (qe < (1u << 15)) & (au2 < (1 << 15)) & (av2 < (1 << 15)) & (R >= e2 + tsh) &
+                      (B - R >= e1 + e2);
+      if (!go) break;
+      A = B;
+      B = R;
+      u0 = u1;
+      v0 = v1;
+      u1 = u2;
+      v1 = v2;
+      steps++;
+    }
+    if (steps == 0) {
+      half_split_step(r0, r1, t0, t1);
+    } else {
+      uint32_t nr0[8], nr1[8], nt0[8], nt1[8];
+      words8_row(nr0, u0, v0, r0, r1);
+      words8_row(nr1, u1, v1, r0, r1);
+      words8_row(nt0, u0, v0, t0, t1);
+      words8_row(nt1, u1, v1, t0, t1);
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        r0[j] = nr0[j];
+        r1[j] = nr1[j];
+        t0[j] = nt0[j];
+        t1[j] = nt1[j];
+      }
+    }
+  }
+  vneg = (t1[7] >> 31) != 0;
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    u[j] = r1[j];
     const uint64_t d = (uint64_t)0 - t1[j] - borrow;
     borrow = (uint32_t)(d >> 63);
     vabs[j] = vneg ? (uint32_t)d : t1[j];

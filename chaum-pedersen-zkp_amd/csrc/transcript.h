@@ -74,38 +74,41 @@ CPZ_HD uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
 constexpr int kXor3 = 0x96;   // a ^ b ^ c
 constexpr int kChi = 0xD2;    // a ^ (~b & c)
 
-// In-place Keccak-f[1600] on 25 lanes, lane index x + 5y.
-CPZ_HD void keccak_f1600(uint64_t a[25]) {
+// One Keccak-f[1600] round on 25 lanes, lane index x + 5y.
+CPZ_HD void keccak_round(uint64_t a[25], uint64_t rc) {
   // rho offsets and pi destinations in lane order.
   constexpr int rho[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43,
                            25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
-  for (int round = 0; round < 24; round++) {
-    uint64_t c[5], b[25];
+  uint64_t c[5], b[25];
 #pragma unroll
-    for (int x = 0; x < 5; x++)
-      c[x] = bitop3_64<kXor3>(bitop3_64<kXor3>(a[x], a[x + 5], a[x + 10]), a[x + 15], a[x + 20]);
+  for (int x = 0; x < 5; x++)
+    c[x] = bitop3_64<kXor3>(bitop3_64<kXor3>(a[x], a[x + 5], a[x + 10]), a[x + 15], a[x + 20]);
 #pragma unroll
-    for (int x = 0; x < 5; x++) {
-      const uint64_t d = c[(x + 4) % 5] ^ rol64(c[(x + 1) % 5], 1);
+  for (int x = 0; x < 5; x++) {
+    const uint64_t d = c[(x + 4) % 5] ^ rol64(c[(x + 1) % 5], 1);
 #pragma unroll
-      for (int y = 0; y < 5; y++) a[x + 5 * y] ^= d;
-    }
+    for (int y = 0; y < 5; y++) a[x + 5 * y] ^= d;
+  }
 #pragma unroll
-    for (int x = 0; x < 5; x++) {
-#pragma unroll
-      for (int y = 0; y < 5; y++) {
-        // B[y, 2x + 3y] = rot(A[x, y], r[x, y])
-        b[y + 5 * ((2 * x + 3 * y) % 5)] = rol64(a[x + 5 * y], rho[x + 5 * y]);
-      }
-    }
+  for (int x = 0; x < 5; x++) {
 #pragma unroll
     for (int y = 0; y < 5; y++) {
-#pragma unroll
-      for (int x = 0; x < 5; x++)
-        a[x + 5 * y] = bitop3_64<kChi>(b[x + 5 * y], b[(x + 1) % 5 + 5 * y], b[(x + 2) % 5 + 5 * y]);
+      // B[y, 2x + 3y] = rot(A[x, y], r[x, y])
+      b[y + 5 * ((2 * x + 3 * y) % 5)] = rol64(a[x + 5 * y], rho[x + 5 * y]);
     }
-    a[0] ^= KECCAK_RC(round);
   }
+#pragma unroll
+  for (int y = 0; y < 5; y++) {
+#pragma unroll
+    for (int x = 0; x < 5; x++)
+      a[x + 5 * y] = bitop3_64<kChi>(b[x + 5 * y], b[(x + 1) % 5 + 5 * y], b[(x + 2) % 5 + 5 * y]);
+  }
+  a[0] ^= rc;
+}
+
+// In-place Keccak-f[1600] (the compiler keeps the 24 rounds a loop: one round of code).
+CPZ_HD void keccak_f1600(uint64_t a[25]) {
+  for (int round = 0; round < 24; round++) keccak_round(a, KECCAK_RC(round));
 }
 
 // STROBE-128 restricted to the operations Merlin uses (meta-AD, AD, PRF).

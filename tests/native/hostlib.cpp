@@ -410,12 +410,12 @@ void cpzt_half_split(uint8_t* u_out, uint8_t* v_out, int* vneg, const uint8_t* c
   *vneg = neg ? 1 : 0;
 }
 
-// The same through the uniform small-quotient path (k_verify_wide's wave 4).
-void cpzt_half_split_smallq(uint8_t* u_out, uint8_t* v_out, int* vneg, const uint8_t* c) {
+// The 31-bit-window split (k_verify_wide's wave 4).
+void cpzt_half_split32(uint8_t* u_out, uint8_t* v_out, int* vneg, const uint8_t* c) {
   uint32_t cw[8], u[4], v[4];
   words_from(cw, c);
   bool neg;
-  sc_half_split<true>(cw, u, v, neg);
+  sc_half_split32(cw, u, v, neg);
   std::memcpy(u_out, u, 16);
   std::memcpy(v_out, v, 16);
   *vneg = neg ? 1 : 0;

@@ -199,11 +199,11 @@ def _euclid_half(c):
     return r1, t1
 
 
-@pytest.mark.parametrize("fn", ["cpzt_half_split", "cpzt_half_split_smallq"])
+@pytest.mark.parametrize("fn", ["cpzt_half_split", "cpzt_half_split32"])
 def test_half_split(lib, fn):
     """sc_half_split (csrc/scalar25519.h): v c = u (mod l), u, |v| < 3 * 2^125, and equal
     to the exact Euclid values -- incl. huge partial quotients (the shifted-divisor path) --
-    with the f64 quotients and with k_verify_wide's compare-and-subtract small quotients."""
+    with 63-bit Lehmer windows and f64 quotients, and with k_verify_wide's 31-bit windows."""
     rng = random.Random(7)
     cases = [0, 1, 2, (3 << 125) - 1, 3 << 125, L - 1, L - 2, L // 2, L // 3, (L >> 70), (L >> 140) + 5,
              (L >> 126), (L >> 127) + 1, 2**252, (2**128 + 1) % L]

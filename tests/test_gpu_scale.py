@@ -59,11 +59,20 @@ def test_small_batch_eight_lanes_every_forgery_kind(gpu, golden, n):
 
 @pytest.mark.parametrize("n", [1, 2, 7, 8, 9, 100, 2047, 2048, 2049])
 def test_small_kernel_every_forgery_kind_and_context_shape(gpu, golden, n):
-    """Launches of at most 2048 proofs take k_verify_small (three waves per 8 proofs, the
-    transcript challenge computed inside: fixed schedules for no context and 32-byte contexts,
-    the byte-wise sponge for Some(b"") and other lengths): on both sides of the limit and at
-    the workgroup's 8-proof edges, every status and challenge equals the C oracle's."""
+    """Launches of at most 2048 proofs compute the transcript challenge inside the verify
+    kernel (fixed schedules for no context and 32-byte contexts, the byte-wise sponge for
+    Some(b"") and other lengths): up to 512 proofs k_verify_wide (a five-wave workgroup per
+    proof), then k_verify_small (three waves per 8 proofs).  On both sides of the 2048 limit
+    and at the 8-proof workgroup edges every status and challenge equals the C oracle's."""
     _every_forgery_kind(gpu, golden, n, n, 31 + n, ctx_shapes=True)
+
+
+@pytest.mark.parametrize("n", [3, 511, 512, 513])
+def test_wide_kernel_boundary_every_forgery_kind(gpu, golden, n):
+    """k_verify_wide (field products on 16-lane rows, csrc/fe16.h) takes launches of at most
+    512 proofs, k_verify_small the next: on both sides of the limit, every forgery kind and
+    context shape, every status and challenge equals the C oracle's."""
+    _every_forgery_kind(gpu, golden, n, n, 57 + n, ctx_shapes=True)
 
 
 def _every_forgery_kind(gpu, golden, n, nsample, seed, ctx_shapes=False):

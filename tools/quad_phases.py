@@ -2,7 +2,7 @@
 build (CPZ_LIB=lib/timing/clock_probe.so) the per-proof kernel stamps the shader clock at its
 phase boundaries for block 0 (kernels.hip) and the 100 MHz clock around it, so the phases come
 out in microseconds at the kernel's own clock.  k_verify_wide (launches of <= CPZ_WIDE_MAX
-proofs, default 32): wave 0's decode, table, wait for wave 4's digits, Straus, wait, combine,
+proofs, default 512): wave 0's decode, table, wait for wave 4's digits, Straus, wait, combine,
 verdict, and wave 4's challenge + split and [s'] B.  k_verify_small (launches of <= 2048 proofs):
 wave 0's decode, table, wait for wave 2's digits, Straus, wait for the partial sums, verdict,
 and wave 2's challenge + split and [s'] B; k_verify_quad (larger launches, or a library built
@@ -46,8 +46,8 @@ def main():
     fn = lib.cpz_ctx_clock_probe
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
-    wide_max = int(os.environ.get("CPZ_WIDE_MAX", "32"))
-    kern = os.environ.get("KERNEL", "wide" if n <= wide_max and not params else ("small" if n <= 2048 else "quad"))
+    wide_max = int(os.environ.get("CPZ_WIDE_MAX", "512"))
+    kern = os.environ.get("KERNEL", "wide" if n <= wide_max else ("small" if n <= 2048 else "quad"))
     small = kern in ("small", "wide")
     table = WIDE if kern == "wide" else SMALL
     names = [x[0] for x in table] if small else list(NAMES)

@@ -18,6 +18,8 @@ def main(path):
     o16 = np.frombuffer(raw[off:off + n16 * 64], np.int32).reshape(n16, 16)       # r16b
     off += n16 * 64
     o16a = np.frombuffer(raw[off:off + n16 * 64], np.int32).reshape(n16, 16)      # r16
+    off += n16 * 64
+    o16c = np.frombuffer(raw[off:off + n16 * 64], np.int32).reshape(n16, 16)      # r16c
     e = pow(2, int(chain), P - 1)
     bad25 = bad16 = 0
     for i in range(nelem):
@@ -26,10 +28,10 @@ def main(path):
         got = sum(int(w) << (32 * j) for j, w in enumerate(o25[i]))
         bad25 += got != want
         if i < n16:
-            for o in (o16, o16a):
+            for o in (o16, o16a, o16c):
                 g16 = sum(int(l) << (16 * k) for k, l in enumerate(o[i])) % P
                 bad16 += g16 != want
-    lim = int(max(np.abs(o16).max(), np.abs(o16a).max()))
+    lim = int(max(np.abs(o16).max(), np.abs(o16a).max(), np.abs(o16c).max()))
     print('{"elements_r25": %d, "bad_r25": %d, "elements_r16": %d, "bad_r16": %d, "max_abs_limb_r16": %d}'
           % (nelem, bad25, n16, bad16, lim))
     return 1 if bad25 or bad16 else 0
