@@ -15,6 +15,8 @@ constexpr uint8_t kStatusIdentity = 4;
 constexpr uint8_t kStatusZeroS = 5;
 
 constexpr int kNielsEntries = kTableB;   // radix-256 signed digits: |d| <= 128
+// Niels table bases per generator: B, 2^128 B, 2^64 B, 2^192 B (tables [level][generator])
+constexpr int kNielsLevels = 4;
 constexpr int kCachedEntries = 2 * kTableSlots;   // y and r tables (identity + 1..8): |d| <= 8
 #ifndef CPZ_VERIFY_BLOCK
 #define CPZ_VERIFY_BLOCK 256
@@ -143,7 +145,7 @@ struct VerifyArgs {
   uint64_t* clock_probe = nullptr;  // CPZ_CLOCK_PROBE builds only: k_verify_quad's phase stamps
                                     // (kQuadPhases shader-clock words of block 0's first proof)
   const int32_t* vtab16 = nullptr;  // the same tables as 16-bit limbs for k_verify_wide (fe16.h):
-                                    // [4 bases][128 entries][Y+X, Y-X, 2dxy][16 limbs]
+                                    // [8 bases][128 entries][Y+X, Y-X, 2dxy][16 limbs]
   const ge_niels* vtab = nullptr;   // variable-base generators (no comb built for this (g, h)):
                                     // Niels multiples 1..128 of g, h, 2^128 g, 2^128 h
                                     // (k_build_niels), [s'] B from them inside the Straus loop;
@@ -171,7 +173,8 @@ hipError_t launch_challenge(const ChallengeArgs& a, hipStream_t st);
 hipError_t launch_probe_gather(const ProbeGatherArgs& a, hipStream_t st);
 bool challenge_prefix_is_fixed(const StrobeSnap& snap);  // the no-context fast path applies
 bool challenge_prefix_is_ctx32(const StrobeSnap& snap);  // prefix[0]: the 32-byte-context fast path applies
-// Niels tables of 2 * nbases bases (nbases <= 8); `bases` is scratch for 2 * nbases ge_p3.
+// Niels tables of kNielsLevels * nbases bases (nbases <= 4); `bases` is scratch for
+// kNielsLevels * nbases ge_p3.
 hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, ge_p3* bases,
                               hipStream_t st);
 // The Niels tables' fields as canonical 16-bit limbs (VerifyArgs::vtab16): n entries.

@@ -8,7 +8,7 @@
 //                        registers, any other context length on an LDS sponge image
 //                        batch.rs:188-206, gadgets.rs:466-482
 //   k_challenge_noctx    the same for batches without contexts (registers only)
-//   k_niels_bases /      (k * B) for k = 1..128, B in {g, h, 2^128 g, 2^128 h}: affine
+//   k_niels_bases /      (k * B) for k = 1..128, B in {g, h} x {1, 2^128, 2^64, 2^192}: affine
 //   k_build_niels        Niels tables
 //   k_verify_each        1 thread / proof: challenge split v c = u (mod l) with
 //                        u, |v| < 2^127 (verify.h), 4 ristretto decodes, then per equation
@@ -34,6 +34,7 @@
 #include "verify.h"
 #include "rlc_dev.h"
 #include "fe16.h"
+#include "keccak_wave.h"
 
 namespace cpz {
 
@@ -181,27 +182,32 @@ __global__ void __launch_bounds__(256) k_challenge_noctx(ChallengeArgs a) {
 // ---------------------------------------------------------------------------------------
 // Fixed-base tables: tab[b * 128 + (k - 1)] = k * base_b in affine Niels form.
 // ---------------------------------------------------------------------------------------
-// Tables for 2 * nbases bases: [b0 .. b_{n-1}, 2^128 b0 .. 2^128 b_{n-1}], 128 entries each.
+// Tables for kNielsLevels * nbases bases: [b0 .. b_{n-1}] at 1, 2^128, 2^64, 2^192 times,
+// 128 entries each.
 // k_niels_bases: quad b decodes base b % nbases (every lane; ok flags from the first nbases
-// quads) and, for b >= nbases, doubles it 128 times as quad-cooperative doublings (~0.15 ms
-// for the chain, against ~0.35 ms on one lane per thread); k_build_niels: one thread per entry,
-// [k] B_b by double-and-add and one inversion to affine Niels.  A variable-base call's cold
-// (g, h) waits for both (ensure_generators).
+// quads) and doubles it 0, 128, 64 or 192 times (level b / nbases) as quad-cooperative
+// doublings (~0.2 ms for the longest chain, against ~0.5 ms on one lane per thread):
+// B, 2^128 B (k_verify_quad's variable bases, the RLC extras), 2^64 B and 2^192 B
+// (k_verify_wide's four 64-bit windows); k_build_niels: one thread per entry, [k] B_b by
+// double-and-add and one inversion to affine Niels.  A variable-base call's cold (g, h) waits
+// for both (ensure_generators).
 __global__ void __launch_bounds__(64) k_niels_bases(const uint32_t* __restrict__ base_words, int nbases,
                                                      ge_p3* __restrict__ bases, int* __restrict__ ok) {
   const int b = threadIdx.x >> 2, q = threadIdx.x & 3;
-  if (b >= 2 * nbases) return;  // whole quads
+  if (b >= kNielsLevels * nbases) return;  // whole quads
   ge_p3 B;
   const bool dec = ristretto_decode(B, base_words + 8 * (b % nbases));
   if (b < nbases && q == 0) ok[b] = dec ? 1 : 0;
-  if (b >= nbases) B = p3_dbl_n_quad(B, 128, q);
+  const int level = b / nbases;
+  const int dbl = level == 0 ? 0 : (level == 1 ? 128 : (level == 2 ? 64 : 192));
+  if (dbl) B = p3_dbl_n_quad(B, dbl, q);
   if (q == 0) bases[b] = B;
 }
 
 __global__ void __launch_bounds__(64) k_build_niels(const ge_p3* __restrict__ bases, int nbases,
                                                     ge_niels* __restrict__ tab) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 2 * nbases * kNielsEntries) return;
+  if (t >= kNielsLevels * nbases * kNielsEntries) return;
   const int b = t / kNielsEntries;
   const int k = t % kNielsEntries + 1;
   tab[t] = p3_to_niels(small_mul(bases[b], k));
@@ -581,11 +587,11 @@ hipError_t launch_probe_gather(const ProbeGatherArgs& a, hipStream_t st) {
 
 hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, ge_p3* bases,
                               hipStream_t st) {
-  if (nbases < 1 || 2 * nbases > 16) return hipErrorInvalidValue;  // one wave of quads
+  if (nbases < 1 || kNielsLevels * nbases > 16) return hipErrorInvalidValue;  // one wave of quads
   hipLaunchKernelGGL(k_niels_bases, dim3(1), dim3(64), 0, st, base_words, nbases, bases, ok);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int total = 2 * nbases * kNielsEntries;
+  const int total = kNielsLevels * nbases * kNielsEntries;
   hipLaunchKernelGGL(k_build_niels, dim3((total + 63) / 64), dim3(64), 0, st, (const ge_p3*)bases, nbases, tab);
   return hipGetLastError();
 }
@@ -921,15 +927,21 @@ __device__ __forceinline__ void proof_digits(uint32_t dig[16], uint32_t& meta, c
                              ((reinterpret_cast<uintptr_t>(ca.ctx_bytes) + b0) & 3) == 0;
     sc c;
     if (fixed_noctx) {
-      c = challenge_fixed(reinterpret_cast<const uint32_t*>(ca.prefix[1].state), ca.k1, ca.k2, y1, y2, r1,
-                                    r2);
+      const uint32_t* pre = reinterpret_cast<const uint32_t*>(ca.prefix[1].state);
+      if constexpr (kWave)
+        c = challenge_fixed(pre, ca.k1, ca.k2, y1, y2, r1, r2, PermRows{sponge, (int)(threadIdx.x & 63)});
+      else
+        c = challenge_fixed(pre, ca.k1, ca.k2, y1, y2, r1, r2);
     } else if (fixed_ctx32) {
       uint32_t cx[8];
       const uint32_t* cp = reinterpret_cast<const uint32_t*>(ca.ctx_bytes + b0);
 #pragma unroll
       for (int k = 0; k < 8; k++) cx[k] = cp[k];
-      c = challenge_fixed_ctx32(reinterpret_cast<const uint32_t*>(ca.prefix[0].state), ca.c32, cx, y1, y2,
-                                          r1, r2);
+      const uint32_t* pre = reinterpret_cast<const uint32_t*>(ca.prefix[0].state);
+      if constexpr (kWave)
+        c = challenge_fixed_ctx32(pre, ca.c32, cx, y1, y2, r1, r2, PermRows{sponge, (int)(threadIdx.x & 63)});
+      else
+        c = challenge_fixed_ctx32(pre, ca.c32, cx, y1, y2, r1, r2);
     } else {
       for (int k = 0; k < 8; k++) c.w[k] = 0;
       if (sponge_lane) {
@@ -1137,7 +1149,7 @@ hipError_t launch_verify_small(const VerifyArgs& a, const ChallengeArgs& ca, hip
 // equation's three sums and test the identity.  Barrier C: wave 0 writes the status with
 // verify_proof's precedence.  Custom generators (VerifyArgs::vtab16, the pair's Niels tables
 // as 16-bit limbs): waves 4 and 5 compute [s'] g and [s'] h on rows instead of the comb --
-// 16 radix-256 windows of s' on B and of s' >> 128 on 2^128 B, 120 doublings + 32 additions.
+// s' in four 64-bit parts on B, 2^64 B, 2^128 B, 2^192 B: 56 doublings + 32 additions.
 // ---------------------------------------------------------------------------------------
 struct WideShared {
   uint32_t dig[16];            // u (0..3), |v| (4..7), s' (8..15) digit words
@@ -1154,27 +1166,36 @@ struct WideShared {
 
 __device__ __forceinline__ int niels16_b(const int32_t* t16, int d, const r16::Lane& L);
 
-// [s'] B_e on the rows from the pair's R16 Niels tables: 16 radix-256 windows of s' on B_e and
-// of s' >> 128 on 2^128 B_e (k_verify_small's wave-2 loop), sum to sh.sBv[e].
+// [s'] B_e on the rows from the pair's R16 Niels tables: s' in four 64-bit parts on B_e,
+// 2^64 B_e, 2^128 B_e, 2^192 B_e, 8 radix-256 windows each -- 56 doublings and 32 additions
+// (two 128-bit parts would take 120 doublings) -- sum to sh.sBv[e].
 template <class Shared>
 __device__ __forceinline__ void wide_varbase(Shared& sh, const VerifyArgs& a, int e, const r16::Lane& L) {
   uint32_t sd[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) sd[k] = sh.dig[8 + k];
-  const int32_t* gt = a.vtab16 + (size_t)e * kNielsEntries * 48;
-  const int32_t* gt2 = a.vtab16 + (size_t)(2 + e) * kNielsEntries * 48;
+  // table bases: [g, h, 2^128 g, 2^128 h, 2^64 g, 2^64 h, 2^192 g, 2^192 h] (k_niels_bases)
+  const int32_t* t0 = a.vtab16 + (size_t)e * kNielsEntries * 48;
+  const int32_t* t1 = a.vtab16 + (size_t)(4 + e) * kNielsEntries * 48;
+  const int32_t* t2 = a.vtab16 + (size_t)(2 + e) * kNielsEntries * 48;
+  const int32_t* t3 = a.vtab16 + (size_t)(6 + e) * kNielsEntries * 48;
   r16::P4 acc = r16::identity(L);
 #pragma unroll 1
-  for (int b = 15; b >= 0; b--) {
-    const int dg = (int32_t)(sd[b >> 2] << (24 - 8 * (b & 3))) >> 24;
-    const int dg2 = (int32_t)(sd[4 + (b >> 2)] << (24 - 8 * (b & 3))) >> 24;
-    const int b1 = niels16_b(gt, dg, L), b2 = niels16_b(gt2, dg2, L);
-    if (b != 15) {
+  for (int b = 7; b >= 0; b--) {
+    // digit 8 q + b of s' (radix 256, 4 per word) on 2^(64 q) B_e
+    const int sft = 24 - 8 * (b & 3);
+    const int d0 = (int32_t)(sd[b >> 2] << sft) >> 24, d1 = (int32_t)(sd[2 + (b >> 2)] << sft) >> 24;
+    const int d2 = (int32_t)(sd[4 + (b >> 2)] << sft) >> 24, d3 = (int32_t)(sd[6 + (b >> 2)] << sft) >> 24;
+    const int b0 = niels16_b(t0, d0, L), b1 = niels16_b(t1, d1, L), b2 = niels16_b(t2, d2, L),
+              b3 = niels16_b(t3, d3, L);
+    if (b != 7) {
 #pragma unroll 1
       for (int k = 0; k < 8; k++) acc = r16::dbl(acc, L);
     }
+    acc = r16::add_b(acc, b0, L);
     acc = r16::add_b(acc, b1, L);
     acc = r16::add_b(acc, b2, L);
+    acc = r16::add_b(acc, b3, L);
   }
   sh.sBv[e][L.row][L.k] = r16::sel4(acc.X, acc.Y, acc.Z, acc.T, L);
 }

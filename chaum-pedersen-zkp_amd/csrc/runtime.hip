@@ -174,7 +174,7 @@ struct GenSet {
   bool full = true;
   uint64_t used = 0;  // LRU stamp
   uint8_t gh[64];
-  DevBuf tab;       // 4 x 128 ge_niels (g, h, 2^128 g, 2^128 h)
+  DevBuf tab;       // 8 x 128 ge_niels (g, h at 1, 2^128, 2^64, 2^192 times)
   DevBuf tab16;     // the same as 16-bit limbs (k_verify_wide's variable bases)
   DevBuf comb;      // fixed-base combs of g and h: 2 x 16 x 2^15 ge_niels (128 MiB)
   DevBuf comb_q;    // 32 ge_p3: 2^(16 k) g, 2^(16 k) h
@@ -360,18 +360,19 @@ GenSet* lru_victim(GenSet* sets, int n) {
 // The Niels tables (g, h, 2^128 g, 2^128 h) and transcript prefix of (g, h) into e, and the
 // fixed-schedule masks; CPZ_EGENERATOR if an encoding does not decode.
 int build_niels_prefix(cpz_ctx* ctx, GenSet& e, const uint8_t both[64]) {
-  CPZ_HIP(e.tab.ensure(4 * cpz::kNielsEntries * sizeof(cpz::ge_niels)));  // g, h, 2^128 g, 2^128 h
+  // g, h, 2^128 g, 2^128 h, 2^64 g, 2^64 h, 2^192 g, 2^192 h
+  CPZ_HIP(e.tab.ensure(2 * cpz::kNielsLevels * cpz::kNielsEntries * sizeof(cpz::ge_niels)));
   CPZ_HIP(e.prefix.ensure(2 * sizeof(cpz::StrobeSnap)));
   CPZ_HIP(e.gh_words.ensure(64));
   CPZ_HIP(ctx->ok_flags.ensure(2 * sizeof(int)));
-  CPZ_HIP(ctx->gen_bases.ensure(4 * sizeof(cpz::ge_p3)));
+  CPZ_HIP(ctx->gen_bases.ensure(2 * cpz::kNielsLevels * sizeof(cpz::ge_p3)));
   CPZ_HIP(hipMemcpyAsync(e.gh_words.p, both, 64, hipMemcpyHostToDevice, ctx->stream));
   CPZ_HIP(cpz::launch_build_niels(static_cast<const uint32_t*>(e.gh_words.p), 2, static_cast<cpz::ge_niels*>(e.tab.p),
                                   static_cast<int*>(ctx->ok_flags.p), static_cast<cpz::ge_p3*>(ctx->gen_bases.p),
                                   ctx->stream));
-  CPZ_HIP(e.tab16.ensure(4 * cpz::kNielsEntries * 48 * sizeof(int32_t)));
+  CPZ_HIP(e.tab16.ensure(2 * cpz::kNielsLevels * cpz::kNielsEntries * 48 * sizeof(int32_t)));
   CPZ_HIP(cpz::launch_niels_r16(static_cast<const cpz::ge_niels*>(e.tab.p), static_cast<int32_t*>(e.tab16.p),
-                                4 * cpz::kNielsEntries, ctx->stream));
+                                2 * cpz::kNielsLevels * cpz::kNielsEntries, ctx->stream));
   CPZ_HIP(cpz::launch_transcript_prefix(static_cast<const uint32_t*>(e.gh_words.p),
                                         static_cast<cpz::StrobeSnap*>(e.prefix.p), ctx->stream));
   int ok[2] = {0, 0};
@@ -510,23 +511,6 @@ bool zero_copy() {
     return !(e && e[0] == '0');
   }();
   return v;
-}
-// Small synchronous calls wait for their stream by polling it (hipStreamQuery) instead of
-// hipStreamSynchronize's blocking wait, whose wake-up adds microseconds to a ~0.1 ms call;
-// CPZ_SPIN_SYNC=0 restores the blocking wait.
-bool spin_sync() {
-  static const bool v = [] {
-    const char* e = std::getenv("CPZ_SPIN_SYNC");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-hipError_t sync_small_call(hipStream_t st) {
-  if (!spin_sync()) return hipStreamSynchronize(st);
-  for (;;) {
-    const hipError_t e = hipStreamQuery(st);
-    if (e != hipErrorNotReady) return e;
-  }
 }
 int64_t wide_max() {
   static const int64_t v = [] {
@@ -2118,7 +2102,7 @@ int cpz_verify_each_ex(cpz_ctx* ctx, uint32_t flags, const uint8_t g[32], const 
   if (st_dev) {  // zero-copy: inputs read and statuses written through the page-locked block
     rc = enqueue_verify(ctx, n, dev[0], dev[1], dev[2], dev[3], dev[4], dcb, dco, dcp, st_dev, ctx->stream);
     if (rc) return rc;
-    CPZ_HIP(sync_small_call(ctx->stream));
+    CPZ_HIP(hipStreamSynchronize(ctx->stream));
     std::memcpy(status_out, st_host, n);
     return CPZ_OK;
   }

@@ -114,42 +114,52 @@ CPZ_HD void keccak_words(uint32_t st[50]) {
   }
 }
 
+// The permutation the fixed-schedule tails apply to their 50-word sponge image: Keccak-f on
+// the image's registers (every lane its own sponge), or a caller's (k_verify_wide's wave 4
+// spreads one sponge over the lanes of its wave, kernels.hip PermRows).
+struct PermRegs {
+  CPZ_HD void operator()(uint32_t st[50]) const { keccak_words(st); }
+};
+
+template <class Perm = PermRegs>
 CPZ_HD sc challenge_fixed(const uint32_t prefix[50], const uint32_t k1[50], const uint32_t k2[50],
-                          const uint32_t y1[8], const uint32_t y2[8], const uint32_t r1[8], const uint32_t r2[8]) {
+                          const uint32_t y1[8], const uint32_t y2[8], const uint32_t r1[8], const uint32_t r2[8],
+                          const Perm& perm = Perm()) {
   uint32_t st[50];
 #pragma unroll
   for (int w = 0; w < 50; w++) st[w] = prefix[w] ^ k1[w];
   xor_message<kTailY1>(st, y1);
   xor_message<kTailY2>(st, y2);
   xor_message<kTailR1>(st, r1);
-  keccak_words(st);
+  perm(st);
 #pragma unroll
   for (int w = 0; w < 50; w++) st[w] ^= k2[w];
   xor_message<kTailR2>(st, r2);
-  keccak_words(st);
+  perm(st);
   return sc_reduce_wide(st);  // challenge bytes 0..63 = state words 0..15
 }
 
 // 32-byte-context tail: prefix = the state after Transcript::new, m = the three segments'
 // framing masks (challenge_masks_ctx32, g and h included), ctx = the context as 8 words.
+template <class Perm = PermRegs>
 CPZ_HD sc challenge_fixed_ctx32(const uint32_t prefix[50], const uint32_t m[3][50], const uint32_t ctx[8],
                                 const uint32_t y1[8], const uint32_t y2[8], const uint32_t r1[8],
-                                const uint32_t r2[8]) {
+                                const uint32_t r2[8], const Perm& perm = Perm()) {
   uint32_t st[50];
 #pragma unroll
   for (int w = 0; w < 50; w++) st[w] = prefix[w] ^ m[0][w];
   xor_message<kC32Ctx>(st, ctx);
-  keccak_words(st);
+  perm(st);
 #pragma unroll
   for (int w = 0; w < 50; w++) st[w] ^= m[1][w];
   xor_message<kC32Y1>(st, y1);
   xor_message<kC32Y2>(st, y2);
-  keccak_words(st);
+  perm(st);
 #pragma unroll
   for (int w = 0; w < 50; w++) st[w] ^= m[2][w];
   xor_message<kC32R1>(st, r1);
   xor_message<kC32R2>(st, r2);
-  keccak_words(st);
+  perm(st);
   return sc_reduce_wide(st);
 }
 

@@ -1,8 +1,9 @@
 // Microbenchmark: the serial work of k_verify_wide's wave 4 (the challenge and the split that
 // gate the Straus loops) timed piece by piece on a lone wave with the shader clock
 // (s_memtime), to see where its ~65 us go:
-//   challenge   challenge_fixed (two Keccak-f permutations on the register sponge + the wide
-//               reduction mod l), twice
+//   challenge   challenge_fixed (two Keccak-f permutations + the wide reduction mod l) on the
+//               register sponge, and with the permutations spread over the wave (keccak_wave.h),
+//               which must give the same challenge
 //   split       sc_half_split (63-bit Lehmer windows, f64 quotients) / sc_half_split32 (31-bit
 //               windows, f32 reciprocal) / the latter on readfirstlane'd (scalar) inputs
 //   digits      sc_mul (v s mod l) + the three recodings
@@ -19,6 +20,7 @@
 #include "../../chaum-pedersen-zkp_amd/csrc/scalar25519.h"
 #include "../../chaum-pedersen-zkp_amd/csrc/transcript.h"
 #include "../../chaum-pedersen-zkp_amd/csrc/verify.h"
+#include "../../chaum-pedersen-zkp_amd/csrc/keccak_wave.h"
 
 using namespace cpz;
 
@@ -35,13 +37,15 @@ __global__ void __launch_bounds__(64) k_parts(const uint32_t* in, uint32_t* out,
   const uint32_t* prefix = in + 64;
   const uint32_t* k1 = in + 128;
   const uint32_t* k2 = in + 192;
+  __shared__ uint32_t lds[50];
   uint64_t t[8];
   t[0] = __builtin_amdgcn_s_memtime();
-  sc c0 = challenge_fixed(prefix, k1, k2, y1, y2, r1, r2);
-  for (int k = 0; k < 8; k++) y1[k] ^= c0.w[k] & 1u;  // keep the two calls apart (uniform)
+  const sc c0 = challenge_fixed(prefix, k1, k2, y1, y2, r1, r2);
   t[1] = __builtin_amdgcn_s_memtime();
-  sc c = challenge_fixed(prefix, k1, k2, y1, y2, r1, r2);
+  const sc c = challenge_fixed(prefix, k1, k2, y1, y2, r1, r2, PermRows{lds, l});
   t[2] = __builtin_amdgcn_s_memtime();
+  bool same_c = true;
+  for (int k = 0; k < 8; k++) same_c = same_c && c.w[k] == c0.w[k];
   uint32_t u[4], va[4], u2[4], va2[4], u3[4], va3[4];
   bool vneg, vneg2, vneg3;
   sc_half_split(c.w, u, va, vneg);
@@ -72,7 +76,7 @@ __global__ void __launch_bounds__(64) k_parts(const uint32_t* in, uint32_t* out,
   // the three splits must agree
   bool same = vneg == vneg2 && vneg2 == vneg3;
   for (int k = 0; k < 4; k++) same = same && u[k] == u2[k] && u2[k] == u3[k] && va[k] == va2[k] && va2[k] == va3[k];
-  out[64 + l] = same ? 1u : 0u;
+  out[64 + l] = (same ? 1u : 0u) | (same_c ? 0u : 2u);
   if (l == 0)
     for (int k = 0; k < 7; k++) cyc[k] = t[k];
 }
@@ -90,7 +94,7 @@ int main() {
   hipMalloc(&dout, 128 * 4);
   hipMalloc(&dcyc, 8 * 8);
   hipMemcpy(din, in.data(), in.size() * 4, hipMemcpyHostToDevice);
-  const char* names[6] = {"challenge", "challenge_again", "split63", "split31", "split31_scalar",
+  const char* names[6] = {"challenge_registers", "challenge_wave_lanes", "split63", "split31", "split31_scalar",
                           "digits_scmul"};
   std::vector<std::vector<double>> per(6);
   for (int rep = 0; rep < 21; rep++) {
@@ -102,7 +106,7 @@ int main() {
     hipMemcpy(o, dout, sizeof(o), hipMemcpyDeviceToHost);
     for (int l = 0; l < 64; l++)
       if (o[64 + l] != 1) {
-        fprintf(stderr, "split variants disagree on lane %d\n", l);
+        fprintf(stderr, "lane %d: %s\n", l, (o[64 + l] & 2) ? "wave Keccak != register Keccak" : "split variants disagree");
         return 2;
       }
     if (rep == 0) continue;  // cold instruction cache
