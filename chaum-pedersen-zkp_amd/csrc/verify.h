@@ -118,7 +118,7 @@ CPZ_HD void keccak_words(uint32_t st[50]) {
 // the image's registers (every lane its own sponge), or a caller's (k_verify_wide's wave 4
 // spreads one sponge over the lanes of its wave, kernels.hip PermRows).
 struct PermRegs {
-  CPZ_HD void operator()(uint32_t st[50]) const { keccak_words(st); }
+  CPZ_HDM void operator()(uint32_t st[50]) const { keccak_words(st); }
 };
 
 template <class Perm = PermRegs>
