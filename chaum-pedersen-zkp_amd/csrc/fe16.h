@@ -11,7 +11,7 @@
 // computed by all 16 lanes at once:
 //   lane k accumulates column k = sum_i x_i * y_(k-i mod 16), with 38 y where the index
 //   wraps (2^256 = 38 mod p): x_i by a row broadcast (DPP row_newbcast:i), the shifted y by
-//   two DPP moves (row_shr:i of y, the wrapped lanes row_shl:(16-i) of 38 y), one
+//   one v_mul_i32_i24 reading y through DPP row_ror:i times the lane's wrap factor, one
 //   v_mad_i64_i32; then three rounds of a parallel carry through DPP row_ror:1.
 // 143-148 ns per squaring on a lone wave (1.5x faster than one lane, same box).
 //
@@ -36,11 +36,12 @@
 namespace cpz {
 namespace r16 {
 
-// Per-lane constants: limb index, wrap factor, row.
+// Per-lane constants: limb index, wrap factors, row.
 struct Lane {
-  int k;    // limb index (lane & 15)
-  int w;    // 38 on limb 0 (receives the wrapped carry), 1 elsewhere
-  int row;  // 0..3
+  int k;         // limb index (lane & 15)
+  int w;         // 38 on limb 0 (receives the wrapped carry), 1 elsewhere
+  int row;       // 0..3
+  int wrap[16];  // wrap[i] = 38 where a shift by i wraps (k < i), 1 elsewhere
 };
 
 __device__ __forceinline__ Lane lane_of(int lane) {
@@ -48,6 +49,8 @@ __device__ __forceinline__ Lane lane_of(int lane) {
   L.k = lane & 15;
   L.w = L.k == 0 ? 38 : 1;
   L.row = (lane >> 4) & 3;
+#pragma unroll
+  for (int i = 0; i < 16; i++) L.wrap[i] = L.k < i ? 38 : 1;
   return L;
 }
 
@@ -56,26 +59,24 @@ template <int C>
 __device__ __forceinline__ int dpp0(int x) {
   return __builtin_amdgcn_update_dpp(0, x, C, 0xf, 0xf, true);
 }
-// DPP move keeping `old` in lanes whose source is outside the row.
-template <int C>
-__device__ __forceinline__ int dppk(int old, int x) {
-  return __builtin_amdgcn_update_dpp(old, x, C, 0xf, 0xf, false);
-}
 
-// lane k of the row: y_(k-i) for k >= i, 38 y_(k-i+16) for k < i
+// lane k of the row: y_(k-i) for k >= i, 38 y_(k-i+16) for k < i -- ONE instruction,
+// v_mul_i32_i24 reading y through DPP row_ror:i (lane k <- lane k - i mod 16) times the lane's
+// wrap factor.  The 24-bit multiplier needs |y| < 2^23: operands of mul are at most four
+// tight elements (< 2^18.5); mul_pair's pre-shifted y at most 38 x two tight ones (< 2^22.3).
 template <int I>
-__device__ __forceinline__ int shifted(int y, int y38) {
+__device__ __forceinline__ int shifted(int y, const Lane& L) {
   if constexpr (I == 0) {
     return y;
   } else {
-    return dppk<0x110 + I>(dpp0<0x100 + (16 - I)>(y38), y);  // row_shr:i over row_shl:(16-i)
+    return __mul24(dpp0<0x120 + I>(y), L.wrap[I]);
   }
 }
 
 template <int I>
-__device__ __forceinline__ void col_step(int64_t (&a)[4], int x, int y, int y38) {
-  a[I & 3] += (int64_t)dpp0<0x150 + I>(x) * (int64_t)shifted<I>(y, y38);  // row_newbcast:i
-  if constexpr (I + 1 < 16) col_step<I + 1>(a, x, y, y38);
+__device__ __forceinline__ void col_step(int64_t (&a)[4], int x, int y, const Lane& L) {
+  a[I & 3] += (int64_t)dpp0<0x150 + I>(x) * (int64_t)shifted<I>(y, L);  // row_newbcast:i
+  if constexpr (I + 1 < 16) col_step<I + 1>(a, x, y, L);
 }
 
 // floor(v / 2^16) for |v| < 2^47 (bits 16..47 of the two's complement)
@@ -86,7 +87,7 @@ __device__ __forceinline__ int floor16(int64_t v) {
 // x * y mod p (both operands at most four tight elements); tight result.
 __device__ __forceinline__ int mul(int x, int y, const Lane& L) {
   int64_t a[4] = {0, 0, 0, 0};
-  col_step<0>(a, x, y, y * 38);
+  col_step<0>(a, x, y, L);
   const int64_t acc = (a[0] + a[1]) + (a[2] + a[3]);
   const int c1 = floor16(acc);
   const int64_t t = (int64_t)dpp0<0x121>(c1) * L.w + (int64_t)((uint32_t)acc & 0xffffu);  // row_ror:1
@@ -97,26 +98,27 @@ __device__ __forceinline__ int mul(int x, int y, const Lane& L) {
 }
 
 template <int I>
-__device__ __forceinline__ void col_step_half(int64_t (&a)[4], int x, int y, int y38) {
-  a[I & 3] += (int64_t)dpp0<0x150 + I>(x) * (int64_t)shifted<I>(y, y38);
-  if constexpr (I + 1 < 8) col_step_half<I + 1>(a, x, y, y38);
+__device__ __forceinline__ void col_step_half(int64_t (&a)[4], int x, int y, const Lane& L) {
+  a[I & 3] += (int64_t)dpp0<0x150 + I>(x) * (int64_t)shifted<I>(y, L);
+  if constexpr (I + 1 < 8) col_step_half<I + 1>(a, x, y, L);
 }
 
 // x * y for values that are the same on every row (the decode): the column sums are split
 // over row pairs -- even rows take i = 0..7, odd rows i = 8..15 from x rotated by 8 and y
 // shifted by 8 (lanes k < 8 then hold 38 y_(k+8); a further shift by j < 8 wraps only lanes
 // >= 9, which hold plain y, so 38 y is never taken twice) -- and one v_permlane16_swap adds
-// the halves: 8 column steps per lane instead of 16.  Same bounds and result as mul.
+// the halves: 8 column steps per lane instead of 16.  Same result as mul; operands at most
+// two tight elements (the decode's are), so the pre-shifted y fits shifted's 24-bit multiply.
 __device__ __forceinline__ int mul_pair(int x, int y, const Lane& L) {
   const bool hi = (L.row & 1) != 0;
   // DPP moves are convergent: computed on every lane, then selected (a conditional DPP
   // becomes a divergent branch)
   const int xr = dpp0<0x128>(x);                         // row_ror:8: lane j holds x_(j+8)
-  const int yr = shifted<8>(y, y * 38);
+  const int yr = shifted<8>(y, L);
   const int xs = hi ? xr : x;
   const int ys = hi ? yr : y;
   int64_t a[4] = {0, 0, 0, 0};
-  col_step_half<0>(a, xs, ys, ys * 38);
+  col_step_half<0>(a, xs, ys, L);
   const int64_t h = (a[0] + a[1]) + (a[2] + a[3]);
   const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)h, (uint32_t)h, false, false);
   const auto hw = __builtin_amdgcn_permlane16_swap((uint32_t)((uint64_t)h >> 32), (uint32_t)((uint64_t)h >> 32),

@@ -962,10 +962,15 @@ __device__ __forceinline__ void proof_digits(uint32_t dig[16], uint32_t& meta, c
     st_s = response_status(sw, ca.eq_only != 0);
   }
   if (stamp_challenge) *stamp_challenge = __builtin_amdgcn_s_memtime();  // timing builds only
+  if constexpr (kWave) {
+    // the byte-wise sponge ran on the first lane alone; the split's rows are shared by lanes
+#pragma unroll
+    for (int k = 0; k < 8; k++) cw[k] = __builtin_amdgcn_readfirstlane(cw[k]);
+  }
   bool vneg;
   uint32_t u[4], va[4];
   if (kWave)
-    sc_half_split32(cw, u, va, vneg);
+    sc_half_split32<true>(cw, u, va, vneg);
   else
     sc_half_split(cw, u, va, vneg);
   sc_recode_radix16_half(dig, u);

@@ -486,6 +486,11 @@ CPZ_HD float f32_rcp(float x) {
 // q < 2^15), cofactors below 2^15, the same two exactness conditions (T / 2^sh rounded up),
 // so the same Euclid pair (u, v); twice the batches (~15 bits each), each batch the same four
 // 8-word rows.
+//
+// kLanes (device, every lane of the wave splitting the same challenge): a batch's four 8-word
+// rows are computed on lanes 0..3 at once and read back with v_readlane, instead of one after
+// another on every lane.
+template <bool kLanes = false>
 CPZ_HD void sc_half_split32(const uint32_t c[8], uint32_t u[4], uint32_t vabs[4], bool& vneg) {
   uint32_t r0[8], r1[8], t0[8], t1[8];
 #pragma unroll
@@ -534,6 +539,32 @@ CPZ_HD void sc_half_split32(const uint32_t c[8], uint32_t u[4], uint32_t vabs[4]
     if (steps == 0) {
       half_split_step(r0, r1, t0, t1);
     } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+      if constexpr (kLanes) {
+        // lane k & 3 computes row k: (u0, v0 | u1, v1) x (r0, r1 | t0, t1); branch-free form of
+        // words8_row (the rows' signs differ between lanes)
+        const int k = (int)(threadIdx.x & 3);
+        const int32_t cu = (k & 1) ? u1 : u0, cv = (k & 1) ? v1 : v0;
+        const bool pos = cu > 0 || cv < 0;
+        const uint32_t au = (uint32_t)(cu < 0 ? -cu : cu), av = (uint32_t)(cv < 0 ? -cv : cv);
+        uint32_t X[8], Y[8], out[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const uint32_t x = (k & 2) ? t0[j] : r0[j], y = (k & 2) ? t1[j] : r1[j];
+          X[j] = pos ? x : y;
+          Y[j] = pos ? y : x;
+        }
+        words8_mulsub2(out, pos ? au : av, X, pos ? av : au, Y);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          r0[j] = __builtin_amdgcn_readlane(out[j], 0);
+          r1[j] = __builtin_amdgcn_readlane(out[j], 1);
+          t0[j] = __builtin_amdgcn_readlane(out[j], 2);
+          t1[j] = __builtin_amdgcn_readlane(out[j], 3);
+        }
+        continue;
+      }
+#endif
       uint32_t nr0[8], nr1[8], nt0[8], nt1[8];
       words8_row(nr0, u0, v0, r0, r1);
       words8_row(nr1, u1, v1, r0, r1);

@@ -1,14 +1,12 @@
 #!/bin/bash
-# Round-5 GPU session Q: the split's batch rows on four lanes (sc_half_split32<true>) and the
-# row product's shifted operand as one v_mul_i32_i24 through DPP -- the wave-4 micro-benchmark,
-# latency tests on the variant, phases, small_batch A/B against HEAD, crossover.
+# Round-5 GPU session R: the row product's shifted operand as one v_mul_i32_i24 through DPP
+# (fe16.h shifted) on top of the four-lane split rows -- latency tests on the variant, phases,
+# small_batch A/B against HEAD.
 set -o pipefail
 export PYTHONDONTWRITEBYTECODE=1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 V=$PWD/chaum-pedersen-zkp_amd/lib/var
-timeout -k 10 60 tools/ubench/w4_parts > gpurun_out/w4_parts_q.json 2>&1 || { cat gpurun_out/w4_parts_q.json; exit 1; }
-cat gpurun_out/w4_parts_q.json
 CPZ_LIB=$V/shift1.so timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_scale.py tests/test_gpu_dropin.py tests/test_gpu_api.py tests/test_gpu_varbase.py > gpurun_out/gpu_r.log 2>&1 || { grep -E "FAIL|Error|assert" gpurun_out/gpu_r.log | head -20; tail -30 gpurun_out/gpu_r.log; exit 1; }
 tail -1 gpurun_out/gpu_r.log
 for lib in $V/probe_shift1.so $PWD/chaum-pedersen-zkp_amd/lib/timing/clock_probe.so $V/probe_shift1.so; do

@@ -5,7 +5,7 @@
 //               register sponge, and with the permutations spread over the wave (keccak_wave.h),
 //               which must give the same challenge
 //   split       sc_half_split (63-bit Lehmer windows, f64 quotients) / sc_half_split32 (31-bit
-//               windows, f32 reciprocal) / the latter on readfirstlane'd (scalar) inputs
+//               windows, f32 reciprocal) / the latter with each batch's four rows on four lanes
 //   digits      sc_mul (v s mod l) + the three recodings
 // One workgroup of one wave; every lane computes the same values (as in wave 4).  Prints one
 // JSON line of cycles per piece (median of the lanes' agreeing results over `reps` launches).
@@ -54,7 +54,7 @@ __global__ void __launch_bounds__(64) k_parts(const uint32_t* in, uint32_t* out,
   t[4] = __builtin_amdgcn_s_memtime();
   uint32_t cs[8];
   for (int k = 0; k < 8; k++) cs[k] = __builtin_amdgcn_readfirstlane(c.w[k]);
-  sc_half_split32(cs, u3, va3, vneg3);
+  sc_half_split32<true>(cs, u3, va3, vneg3);
   t[5] = __builtin_amdgcn_s_memtime();
   uint32_t dig[16];
   sc_recode_radix16_half(dig, u3);
@@ -94,7 +94,7 @@ int main() {
   hipMalloc(&dout, 128 * 4);
   hipMalloc(&dcyc, 8 * 8);
   hipMemcpy(din, in.data(), in.size() * 4, hipMemcpyHostToDevice);
-  const char* names[6] = {"challenge_registers", "challenge_wave_lanes", "split63", "split31", "split31_scalar",
+  const char* names[6] = {"challenge_registers", "challenge_wave_lanes", "split63", "split31", "split31_lanes",
                           "digits_scmul"};
   std::vector<std::vector<double>> per(6);
   for (int rep = 0; rep < 21; rep++) {
