@@ -15,8 +15,13 @@ constexpr uint8_t kStatusIdentity = 4;
 constexpr uint8_t kStatusZeroS = 5;
 
 constexpr int kNielsEntries = kTableB;   // radix-256 signed digits: |d| <= 128
-// Niels table bases per generator: B, 2^128 B, 2^64 B, 2^192 B (tables [level][generator])
-constexpr int kNielsLevels = 4;
+// Niels table bases per generator: 2^(32 m) B for the level order m = 0, 4, 2, 6, 1, 3, 5, 7
+// (B, 2^128 B: the eight-lane kernels' two 128-bit parts; all eight: k_verify_wide's 32-bit
+// parts), tables [level][generator]
+constexpr int kNielsLevels = 8;
+__host__ __device__ constexpr int niels_level_doublings(int level) {
+  return level == 0 ? 0 : (level == 1 ? 128 : (level == 2 ? 64 : (level == 3 ? 192 : 32 * (2 * (level - 4) + 1))));
+}
 constexpr int kCachedEntries = 2 * kTableSlots;   // y and r tables (identity + 1..8): |d| <= 8
 #ifndef CPZ_VERIFY_BLOCK
 #define CPZ_VERIFY_BLOCK 256
@@ -115,7 +120,7 @@ constexpr int64_t kVarBaseMax = kQuadVerifyMax;
 constexpr int kQuadPhases = 9;
 // k_verify_small's stamps (CPZ_CLOCK_PROBE): wave 0 start, decoded, table, barrier A, Straus,
 // barrier B, verdict; wave 2 digits, [s'] B; 100 MHz at wave 0's start / end; wave 2's start.
-constexpr int kSmallStamps = 13;
+constexpr int kSmallStamps = 16;
 constexpr int64_t kQuadProofScratch = 2 * kQuadTableInts * 4;
 
 struct VerifyArgs {
@@ -173,8 +178,8 @@ hipError_t launch_challenge(const ChallengeArgs& a, hipStream_t st);
 hipError_t launch_probe_gather(const ProbeGatherArgs& a, hipStream_t st);
 bool challenge_prefix_is_fixed(const StrobeSnap& snap);  // the no-context fast path applies
 bool challenge_prefix_is_ctx32(const StrobeSnap& snap);  // prefix[0]: the 32-byte-context fast path applies
-// Niels tables of kNielsLevels * nbases bases (nbases <= 4); `bases` is scratch for
-// kNielsLevels * nbases ge_p3.
+// Niels tables of kNielsLevels * nbases bases (nbases <= 2: one wave of quads); `bases` is
+// scratch for kNielsLevels * nbases ge_p3.
 hipError_t launch_build_niels(const uint32_t* base_words, int nbases, ge_niels* tab, int* ok, ge_p3* bases,
                               hipStream_t st);
 // The Niels tables' fields as canonical 16-bit limbs (VerifyArgs::vtab16): n entries.

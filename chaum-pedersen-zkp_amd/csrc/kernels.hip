@@ -8,7 +8,7 @@
 //                        registers, any other context length on an LDS sponge image
 //                        batch.rs:188-206, gadgets.rs:466-482
 //   k_challenge_noctx    the same for batches without contexts (registers only)
-//   k_niels_bases /      (k * B) for k = 1..128, B in {g, h} x {1, 2^128, 2^64, 2^192}: affine
+//   k_niels_bases /      (k * B) for k = 1..128, B in {g, h} x {2^(32 m): m = 0..7}: affine
 //   k_build_niels        Niels tables
 //   k_verify_each        1 thread / proof: challenge split v c = u (mod l) with
 //                        u, |v| < 2^127 (verify.h), 4 ristretto decodes, then per equation
@@ -182,13 +182,13 @@ __global__ void __launch_bounds__(256) k_challenge_noctx(ChallengeArgs a) {
 // ---------------------------------------------------------------------------------------
 // Fixed-base tables: tab[b * 128 + (k - 1)] = k * base_b in affine Niels form.
 // ---------------------------------------------------------------------------------------
-// Tables for kNielsLevels * nbases bases: [b0 .. b_{n-1}] at 1, 2^128, 2^64, 2^192 times,
-// 128 entries each.
+// Tables for kNielsLevels * nbases bases: [b0 .. b_{n-1}] at 2^0, 2^128, 2^64, 2^192, 2^32,
+// 2^96, 2^160, 2^224 times (niels_level_doublings), 128 entries each.
 // k_niels_bases: quad b decodes base b % nbases (every lane; ok flags from the first nbases
-// quads) and doubles it 0, 128, 64 or 192 times (level b / nbases) as quad-cooperative
-// doublings (~0.2 ms for the longest chain, against ~0.5 ms on one lane per thread):
-// B, 2^128 B (k_verify_quad's variable bases, the RLC extras), 2^64 B and 2^192 B
-// (k_verify_wide's four 64-bit windows); k_build_niels: one thread per entry, [k] B_b by
+// quads) and doubles it as level b / nbases says, as quad-cooperative doublings (~0.25 ms
+// for the longest chain, against ~0.6 ms on one lane per thread): B, 2^128 B (k_verify_quad's
+// variable bases, the RLC extras), and all eight (k_verify_wide's eight 32-bit parts of s');
+// k_build_niels: one thread per entry, [k] B_b by
 // double-and-add and one inversion to affine Niels.  A variable-base call's cold (g, h) waits
 // for both (ensure_generators).
 __global__ void __launch_bounds__(64) k_niels_bases(const uint32_t* __restrict__ base_words, int nbases,
@@ -198,8 +198,7 @@ __global__ void __launch_bounds__(64) k_niels_bases(const uint32_t* __restrict__
   ge_p3 B;
   const bool dec = ristretto_decode(B, base_words + 8 * (b % nbases));
   if (b < nbases && q == 0) ok[b] = dec ? 1 : 0;
-  const int level = b / nbases;
-  const int dbl = level == 0 ? 0 : (level == 1 ? 128 : (level == 2 ? 64 : 192));
+  const int dbl = niels_level_doublings(b / nbases);
   if (dbl) B = p3_dbl_n_quad(B, dbl, q);
   if (q == 0) bases[b] = B;
 }
@@ -1145,16 +1144,22 @@ hipError_t launch_verify_small(const VerifyArgs& a, const ChallengeArgs& ca, hip
 // and every field product spread over a 16-lane row (fe16.h): a lone wave's product takes
 // ~145 ns there against ~220 ns on one lane, and a point operation is two such stages
 // (the four products of each on the four rows) instead of eight products on a quad.
-//   waves 0..3  chain c = 2 e + R of equation e: decode Y_e (R_e) -- every row the same --,
-//               its table of 9 cached multiples in LDS (of -Y, or of +R), then the
-//               half-length Straus loop [u] (-Y) or [|v|] (-+R) (k_verify_small's waves 0/1)
-//   wave 4      the challenge, response checks, split and digits (proof_digits), then
-//               [s'] B of both equations from the comb on two quads, as canonical words
-// Barrier A: the digits.  Barrier B: the R chains' sums and [s'] B; waves 0 and 2 add their
-// equation's three sums and test the identity.  Barrier C: wave 0 writes the status with
+// Four chains c = 2 e + R of equation e: a table of 9 cached multiples in LDS (of -Y_e, or
+// of +R_e), then the half-length Straus loop [u] (-Y_e) or [|v|] (-+R_e) (k_verify_small's
+// waves 0/1).  Phase 1:
+//   waves 0, 1  decode Y_e on rows 0-1 and R_e on rows 2-3 of wave e (the decode's products
+//               run on row pairs anyway), hand R_e over in LDS, build Y_e's table
+//   waves 3, 4  R_1's / R_2's table once it is handed over
+//   wave 2      the challenge, response checks, split and digits (proof_digits) -- on a SIMD
+//               of its own: with one decode per chain wave it shared wave 0's, and the two
+//               serial paths slowed each other by ~6 us
+// Phase 2: waves 0, 3, 1, 2 run chains 0..3, wave 4 [s'] B of both equations from the comb
+// on two quads, as canonical words.
+// Barrier A: the digits and tables.  Barrier B: the R chains' sums and [s'] B; the Y chains'
+// waves add their equation's three sums and test the identity.  Barrier C: wave 0 writes the status with
 // verify_proof's precedence.  Custom generators (VerifyArgs::vtab16, the pair's Niels tables
 // as 16-bit limbs): waves 4 and 5 compute [s'] g and [s'] h on rows instead of the comb --
-// s' in four 64-bit parts on B, 2^64 B, 2^128 B, 2^192 B: 56 doublings + 32 additions.
+// s' in eight 32-bit parts on 2^(32 q) B: 24 doublings + 32 additions.
 // ---------------------------------------------------------------------------------------
 struct WideShared {
   uint32_t dig[16];            // u (0..3), |v| (4..7), s' (8..15) digit words
@@ -1167,40 +1172,38 @@ struct WideShared {
   uint32_t rid[2];             // R_e encodes the identity
   uint32_t eq[2];              // equation e holds
   uint32_t sponge[50];         // byte-wise transcript image (contexts off the fixed schedules)
+  int32_t pt[2][4][16];        // R_e handed from its decoding wave to its table's builder
+  uint32_t ready[2];           // ... and the flag that releases it
 };
 
 __device__ __forceinline__ int niels16_b(const int32_t* t16, int d, const r16::Lane& L);
 
-// [s'] B_e on the rows from the pair's R16 Niels tables: s' in four 64-bit parts on B_e,
-// 2^64 B_e, 2^128 B_e, 2^192 B_e, 8 radix-256 windows each -- 56 doublings and 32 additions
-// (two 128-bit parts would take 120 doublings) -- sum to sh.sBv[e].
+// [s'] B_e on the rows from the pair's R16 Niels tables: s' in eight 32-bit parts on
+// 2^(32 q) B_e, 4 radix-256 windows each -- 24 doublings and 32 additions (four 64-bit parts
+// took 56 doublings and 32 additions, ~65 us, longer than the Straus chains) -- to sh.sBv[e].
 template <class Shared>
 __device__ __forceinline__ void wide_varbase(Shared& sh, const VerifyArgs& a, int e, const r16::Lane& L) {
   uint32_t sd[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) sd[k] = sh.dig[8 + k];
-  // table bases: [g, h, 2^128 g, 2^128 h, 2^64 g, 2^64 h, 2^192 g, 2^192 h] (k_niels_bases)
-  const int32_t* t0 = a.vtab16 + (size_t)e * kNielsEntries * 48;
-  const int32_t* t1 = a.vtab16 + (size_t)(4 + e) * kNielsEntries * 48;
-  const int32_t* t2 = a.vtab16 + (size_t)(2 + e) * kNielsEntries * 48;
-  const int32_t* t3 = a.vtab16 + (size_t)(6 + e) * kNielsEntries * 48;
+  // part q's table: level m with niels_level_doublings(m) = 32 q
+  constexpr int kLevelOfPart[8] = {0, 4, 2, 5, 1, 6, 3, 7};
   r16::P4 acc = r16::identity(L);
 #pragma unroll 1
-  for (int b = 7; b >= 0; b--) {
-    // digit 8 q + b of s' (radix 256, 4 per word) on 2^(64 q) B_e
-    const int sft = 24 - 8 * (b & 3);
-    const int d0 = (int32_t)(sd[b >> 2] << sft) >> 24, d1 = (int32_t)(sd[2 + (b >> 2)] << sft) >> 24;
-    const int d2 = (int32_t)(sd[4 + (b >> 2)] << sft) >> 24, d3 = (int32_t)(sd[6 + (b >> 2)] << sft) >> 24;
-    const int b0 = niels16_b(t0, d0, L), b1 = niels16_b(t1, d1, L), b2 = niels16_b(t2, d2, L),
-              b3 = niels16_b(t3, d3, L);
-    if (b != 7) {
+  for (int b = 3; b >= 0; b--) {
+    // digit 4 q + b of s' (radix 256, 4 per word) on 2^(32 q) B_e
+    int op[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int d = (int32_t)(sd[q] << (24 - 8 * b)) >> 24;
+      op[q] = niels16_b(a.vtab16 + (size_t)(2 * kLevelOfPart[q] + e) * kNielsEntries * 48, d, L);
+    }
+    if (b != 3) {
 #pragma unroll 1
       for (int k = 0; k < 8; k++) acc = r16::dbl(acc, L);
     }
-    acc = r16::add_b(acc, b0, L);
-    acc = r16::add_b(acc, b1, L);
-    acc = r16::add_b(acc, b2, L);
-    acc = r16::add_b(acc, b3, L);
+#pragma unroll
+    for (int q = 0; q < 8; q++) acc = r16::add_b(acc, op[q], L);
   }
   sh.sBv[e][L.row][L.k] = r16::sel4(acc.X, acc.Y, acc.Z, acc.T, L);
 }
@@ -1215,85 +1218,133 @@ __device__ __forceinline__ int niels16_b(const int32_t* t16, int d, const r16::L
   return (ng && L.row == 2 && ad != 0) ? -v : v;
 }
 
+// Chain table: entry j = cached(j P), j = 0..8, of the replicated point P; row r stores field r
+// (Y+X, Y-X, Z, 2dT) of each entry at tab[64 j + 16 r + k].
+__device__ __forceinline__ void wide_table(int32_t* tab, const r16::P4& P, const r16::Lane& L) {
+  const int slot = L.row * 16 + L.k;
+  tab[slot] = L.row == 3 ? 0 : r16::one(L);  // identity: Y+X = Y-X = Z = 1, 2dT = 0
+  const r16::C4 c1 = r16::to_cached(P, L);
+  tab[64 + slot] = r16::sel4(c1.ypx, c1.ymx, c1.z, c1.t2d, L);
+  r16::P4 M = r16::dbl(P, L);
+#pragma unroll 1
+  for (int j = 2; j <= 8; j++) {
+    if (j > 2) M = r16::add_b(M, r16::cached_b(c1, false, L), L);
+    const r16::C4 cj = r16::to_cached(M, L);
+    tab[64 * j + slot] = r16::sel4(cj.ypx, cj.ymx, cj.z, cj.t2d, L);
+  }
+}
+
+// The half-length Straus loop of a chain over its table (after barrier A): [u] (-Y) for a Y
+// chain, and for an R chain [|v|] (v < 0 ? R : -R) = -[v] R from the table of +R.
+template <class Shared>
+__device__ __forceinline__ r16::P4 wide_straus(const Shared& sh, const int32_t* tab, bool isR, const r16::Lane& L) {
+  uint32_t d[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) d[k] = sh.dig[(isR ? 4 : 0) + k];
+  const bool flip = isR && !(sh.meta & 1u);
+  // the field row r reads for +C: Y-X, Y+X, 2dT, Z; for -C: Y+X, Y-X, -2dT, Z
+  const int fpos = L.row == 0 ? 1 : (L.row == 1 ? 0 : (L.row == 2 ? 3 : 2));
+  const int fneg = L.row == 0 ? 0 : (L.row == 1 ? 1 : fpos);
+  r16::P4 acc = r16::identity(L);
+#pragma unroll 1
+  for (int jj = 0; jj < 4; jj++) {
+    const uint32_t wd = d[3 - jj];
+#pragma unroll 1
+    for (int m = 7; m >= 0; m--) {
+      int dd = ((int32_t)(wd << (28 - 4 * m))) >> 28;
+      dd = flip ? -dd : dd;
+      const bool ng = dd < 0;
+      const int ad = ng ? -dd : dd;
+      int b = tab[64 * ad + 16 * (ng ? fneg : fpos) + L.k];
+      b = (ng && L.row == 2) ? -b : b;
+      if (jj != 0 || m != 7) {
+        acc = r16::dbl(acc, L);
+        acc = r16::dbl(acc, L);
+        acc = r16::dbl(acc, L);
+        acc = r16::dbl(acc, L);
+      }
+      acc = r16::add_b(acc, b, L);
+    }
+  }
+  return acc;
+}
+
 __global__ void __launch_bounds__(64 * 6) k_verify_wide(VerifyArgs a, ChallengeArgs ca) {
   __shared__ WideShared sh;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int64_t i = blockIdx.x;
   const r16::Lane L = r16::lane_of(l);
   r16::P4 acc = r16::identity(L);
+  // Straus chain of each wave (0: Y_1, 1: R_1, 2: Y_2, 3: R_2); the challenge wave
+  const int chain = w == 0 ? 0 : (w == 1 ? 2 : (w == 2 ? 3 : (w == 3 ? 1 : -1)));
+  constexpr int kDigitWave = 2;
 #if defined(CPZ_CLOCK_PROBE)
   // timing builds only: shader-clock stamps of block 0 (wave 0 lane 0: start, decoded, table,
-  // barrier A, Straus, barrier B, identity test, end; wave 4 lane 0: digits, [s'] B,
-  // challenge (12)) and the 100 MHz clock at wave 0's start and end (10, 11) -> a.clock_probe
-  uint64_t* const stamps = (a.clock_probe && blockIdx.x == 0 && l == 0 && (w == 0 || w == 4)) ? a.clock_probe : nullptr;
+  // barrier A, Straus, barrier B, identity test, end; the challenge wave's lane 0: challenge
+  // (12), digits (8); wave 4 lane 0: [s'] B (9); wave 1 lane 0: decoded, table, Straus
+  // (13..15)) and the 100 MHz clock at wave 0's start and end (10, 11) -> a.clock_probe
+  // (waves 0, 1, 2, 4 as a bit test: with `w <= 1 || w == 2 || w == 4` this compiler left the
+  // pointer null on waves 2 and 4 -- their stamps read back as 0)
+  static_assert(kDigitWave == 2, "stamp waves");
+  const bool stamp_wave = ((0x17u >> w) & 1u) != 0;
+  uint64_t* const stamps = (a.clock_probe && blockIdx.x == 0 && l == 0 && stamp_wave) ? a.clock_probe : nullptr;
 #define CPZ_WIDE_STAMP(k) do { if (stamps) stamps[k] = __builtin_amdgcn_s_memtime(); } while (0)
   if (stamps && w == 0) stamps[10] = __builtin_amdgcn_s_memrealtime();
   if (w == 0) CPZ_WIDE_STAMP(0);
 #else
 #define CPZ_WIDE_STAMP(k) (void)0
 #endif
-  if (w < 4) {
-    const int e = w >> 1;
-    const bool isR = (w & 1) != 0;
+  if (threadIdx.x == 0) {
+    sh.ready[0] = 0u;
+    sh.ready[1] = 0u;
+  }
+  __syncthreads();  // the hand-off flags
+  if (w <= 1) {
+    // ---- waves 0, 1: decode Y_e (rows 0-1) and R_e (rows 2-3); Y_e's table -------------------
+    const int e = w;
+    const bool isR = L.row >= 2;
     const uint32_t* src = isR ? (e ? a.r2 : a.r1) : (e ? a.y2 : a.y1);
     uint32_t wu[8];
     load_words8(wu, src, i);
     r16::P4 P;
     const bool ok = r16::decode(P, src + 8 * i, wu, L);
     if (w == 0) CPZ_WIDE_STAMP(1);
-    if (l == 0) {
-      sh.bad[w] = ok ? 0u : 1u;
-      if (isR) sh.rid[e] = words8_zero(wu) ? 1u : 0u;
+    if (w == 1) CPZ_WIDE_STAMP(13);
+    if (l == 0) sh.bad[2 * e] = ok ? 0u : 1u;
+    if (l == 32) {
+      sh.bad[2 * e + 1] = ok ? 0u : 1u;
+      sh.rid[e] = words8_zero(wu) ? 1u : 0u;
     }
-    if (!isR) P = r16::neg(P);
-    // table: entry j = cached(j P), j = 0..8; row r stores field r
-    int32_t* tab = &sh.tab[w][0][0][0];
-    const int slot = L.row * 16 + L.k;
-    tab[slot] = L.row == 3 ? 0 : r16::one(L);  // identity: Y+X = Y-X = Z = 1, 2dT = 0
-    const r16::C4 c1 = r16::to_cached(P, L);
-    tab[64 + slot] = r16::sel4(c1.ypx, c1.ymx, c1.z, c1.t2d, L);
-    r16::P4 M = r16::dbl(P, L);
-#pragma unroll 1
-    for (int j = 2; j <= 8; j++) {
-      if (j > 2) M = r16::add_b(M, r16::cached_b(c1, false, L), L);
-      const r16::C4 cj = r16::to_cached(M, L);
-      tab[64 * j + slot] = r16::sel4(cj.ypx, cj.ymx, cj.z, cj.t2d, L);
+    if (L.row == 2) {
+      sh.pt[e][0][L.k] = P.X;
+      sh.pt[e][1][L.k] = P.Y;
+      sh.pt[e][2][L.k] = P.Z;
+      sh.pt[e][3][L.k] = P.T;
     }
+    if (l == 32) __hip_atomic_store(&sh.ready[e], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // Y_e on every row (rows 2-3 take rows 0-1's limbs)
+    P.X = (int)__builtin_amdgcn_permlane32_swap(P.X, P.X, false, false)[0];
+    P.Y = (int)__builtin_amdgcn_permlane32_swap(P.Y, P.Y, false, false)[0];
+    P.Z = (int)__builtin_amdgcn_permlane32_swap(P.Z, P.Z, false, false)[0];
+    P.T = (int)__builtin_amdgcn_permlane32_swap(P.T, P.T, false, false)[0];
+    wide_table(&sh.tab[2 * e][0][0][0], r16::neg(P), L);
     if (w == 0) CPZ_WIDE_STAMP(2);
-    __syncthreads();  // A: digits
-    if (w == 0) CPZ_WIDE_STAMP(3);
-    uint32_t d[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) d[k] = sh.dig[(isR ? 4 : 0) + k];
-    // R chains: [|v|] (v < 0 ? R : -R) = -[v] R from the table of +R
-    const bool flip = isR && !(sh.meta & 1u);
-    // the field row r reads for +C: Y-X, Y+X, 2dT, Z; for -C: Y+X, Y-X, -2dT, Z
-    const int fpos = L.row == 0 ? 1 : (L.row == 1 ? 0 : (L.row == 2 ? 3 : 2));
-    const int fneg = L.row == 0 ? 0 : (L.row == 1 ? 1 : fpos);
+    if (w == 1) CPZ_WIDE_STAMP(14);
+  } else if (w == 3 || w == 4) {
+    // ---- waves 3, 4: R_e's table once wave e has handed R_e over -----------------------------
+    const int e = w - 3;
 #pragma unroll 1
-    for (int jj = 0; jj < 4; jj++) {
-      const uint32_t wd = d[3 - jj];
-#pragma unroll 1
-      for (int m = 7; m >= 0; m--) {
-        int dd = ((int32_t)(wd << (28 - 4 * m))) >> 28;
-        dd = flip ? -dd : dd;
-        const bool ng = dd < 0;
-        const int ad = ng ? -dd : dd;
-        int b = tab[64 * ad + 16 * (ng ? fneg : fpos) + L.k];
-        b = (ng && L.row == 2) ? -b : b;
-        if (jj != 0 || m != 7) {
-          acc = r16::dbl(acc, L);
-          acc = r16::dbl(acc, L);
-          acc = r16::dbl(acc, L);
-          acc = r16::dbl(acc, L);
-        }
-        acc = r16::add_b(acc, b, L);
-      }
-    }
-    if (isR) sh.part[w][L.row][L.k] = r16::sel4(acc.X, acc.Y, acc.Z, acc.T, L);
-    if (w == 0) CPZ_WIDE_STAMP(4);
-  } else if (w == 4) {
-    // ---- wave 4: challenge, response checks, split, digits; then [s'] B per equation ----------
+    while (__hip_atomic_load(&sh.ready[e], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+      __builtin_amdgcn_s_sleep(2);
+    r16::P4 P;
+    P.X = sh.pt[e][0][L.k];
+    P.Y = sh.pt[e][1][L.k];
+    P.Z = sh.pt[e][2][L.k];
+    P.T = sh.pt[e][3][L.k];
+    wide_table(&sh.tab[2 * e + 1][0][0][0], P, L);
+  }
+  if (w == kDigitWave) {
+    // ---- the challenge, response checks, split, digits -----------------------------------------
     uint32_t dg[16], meta;
 #if defined(CPZ_CLOCK_PROBE)
     proof_digits<true>(dg, meta, a, ca, i, l == 0, sh.sponge, 0, 1, stamps ? stamps + 12 : nullptr);
@@ -1306,7 +1357,18 @@ __global__ void __launch_bounds__(64 * 6) k_verify_wide(VerifyArgs a, ChallengeA
       sh.meta = meta;
     }
     CPZ_WIDE_STAMP(8);
-    __syncthreads();  // A
+  }
+  __syncthreads();  // A: digits, tables
+  if (w == 0) CPZ_WIDE_STAMP(3);
+  if (chain >= 0) {
+    // ---- the four Straus chains ------------------------------------------------------------------
+    const bool isR = (chain & 1) != 0;
+    acc = wide_straus(sh, &sh.tab[chain][0][0][0], isR, L);
+    if (isR) sh.part[chain][L.row][L.k] = r16::sel4(acc.X, acc.Y, acc.Z, acc.T, L);
+    if (w == 0) CPZ_WIDE_STAMP(4);
+    if (w == 1) CPZ_WIDE_STAMP(15);
+  } else if (w == 4) {
+    // ---- wave 4: [s'] B of both equations (comb on two quads, or the variable-base rows) --------
     if (a.vtab16) {
       wide_varbase(sh, a, 0, L);
     } else if (l < 8) {
@@ -1335,21 +1397,20 @@ __global__ void __launch_bounds__(64 * 6) k_verify_wide(VerifyArgs a, ChallengeA
       }
     }
     CPZ_WIDE_STAMP(9);
-  } else {
+  } else if (w == 5) {
     // ---- wave 5 (variable bases): [s'] h of equation 1 ------------------------------------------
-    __syncthreads();  // A
     wide_varbase(sh, a, 1, L);
   }
   __syncthreads();  // B: the R chains' sums, [s'] B
   if (w == 0) CPZ_WIDE_STAMP(5);
-  if (w == 0 || w == 2) {
+  if (chain == 0 || chain == 2) {
     // Q_e = [u] (-Y_e) + (-[v] R_e) + [s'] B_e, identity (mod E[4])
-    const int e = w >> 1;
+    const int e = chain >> 1;
     r16::P4 R;
-    R.X = sh.part[w + 1][0][L.k];
-    R.Y = sh.part[w + 1][1][L.k];
-    R.Z = sh.part[w + 1][2][L.k];
-    R.T = sh.part[w + 1][3][L.k];
+    R.X = sh.part[chain + 1][0][L.k];
+    R.Y = sh.part[chain + 1][1][L.k];
+    R.Z = sh.part[chain + 1][2][L.k];
+    R.T = sh.part[chain + 1][3][L.k];
     acc = r16::add_b(acc, r16::cached_b(r16::to_cached(R, L), false, L), L);
     r16::P4 S;
     if (a.vtab16) {

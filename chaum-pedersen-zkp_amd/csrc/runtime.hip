@@ -174,7 +174,7 @@ struct GenSet {
   bool full = true;
   uint64_t used = 0;  // LRU stamp
   uint8_t gh[64];
-  DevBuf tab;       // 8 x 128 ge_niels (g, h at 1, 2^128, 2^64, 2^192 times)
+  DevBuf tab;       // 16 x 128 ge_niels (g, h at 2^(32 m) times, build_niels_prefix's order)
   DevBuf tab16;     // the same as 16-bit limbs (k_verify_wide's variable bases)
   DevBuf comb;      // fixed-base combs of g and h: 2 x 16 x 2^15 ge_niels (128 MiB)
   DevBuf comb_q;    // 32 ge_p3: 2^(16 k) g, 2^(16 k) h
@@ -357,10 +357,10 @@ GenSet* lru_victim(GenSet* sets, int n) {
   return v;
 }
 
-// The Niels tables (g, h, 2^128 g, 2^128 h) and transcript prefix of (g, h) into e, and the
-// fixed-schedule masks; CPZ_EGENERATOR if an encoding does not decode.
+// The Niels tables (g, h at 2^(32 m) times, kNielsLevels levels) and transcript prefix of
+// (g, h) into e, and the fixed-schedule masks; CPZ_EGENERATOR if an encoding does not decode.
 int build_niels_prefix(cpz_ctx* ctx, GenSet& e, const uint8_t both[64]) {
-  // g, h, 2^128 g, 2^128 h, 2^64 g, 2^64 h, 2^192 g, 2^192 h
+  // [level][generator]: g, h, 2^128 g, 2^128 h, 2^64 g, 2^64 h, 2^192 g, 2^192 h, 2^32 g, ...
   CPZ_HIP(e.tab.ensure(2 * cpz::kNielsLevels * cpz::kNielsEntries * sizeof(cpz::ge_niels)));
   CPZ_HIP(e.prefix.ensure(2 * sizeof(cpz::StrobeSnap)));
   CPZ_HIP(e.gh_words.ensure(64));

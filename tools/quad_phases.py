@@ -3,7 +3,8 @@ build (CPZ_LIB=lib/timing/clock_probe.so) the per-proof kernel stamps the shader
 phase boundaries for block 0 (kernels.hip) and the 100 MHz clock around it, so the phases come
 out in microseconds at the kernel's own clock.  k_verify_wide (launches of <= CPZ_WIDE_MAX
 proofs, default 512): wave 0's decode, table, wait for wave 4's digits, Straus, wait, combine,
-verdict, and wave 4's challenge + split and [s'] B.  k_verify_small (launches of <= 2048 proofs):
+verdict, wave 4's challenge + split and [s'] B, and wave 1's decode, table and Straus (the
+wave 0 / wave 4 SIMD sharing shows against it).  k_verify_small (launches of <= 2048 proofs):
 wave 0's decode, table, wait for wave 2's digits, Straus, wait for the partial sums, verdict,
 and wave 2's challenge + split and [s'] B; k_verify_quad (larger launches, or a library built
 with CPZ_VERIFY_SMALL=0; KERNEL=quad): split, decode, tables, Straus, comb, verdict.  N proofs
@@ -22,7 +23,7 @@ sys.path.insert(0, ROOT)
 NAMES = ("split_digits", "decode", "tables", "straus", "comb", "verdict")
 WIDE = (("decode", 0, 1), ("table", 1, 2), ("wait_digits", 2, 3), ("straus", 3, 4), ("wait_partials", 4, 5),
         ("combine", 5, 6), ("verdict", 6, 7), ("w4_challenge", 0, 12), ("w4_split_digits", 12, 8),
-        ("w4_s_B", 8, 9))
+        ("w4_s_B", 8, 9), ("w1_decode", 0, 13), ("w1_table", 13, 14), ("w1_straus", 3, 15))
 SMALL = (("decode", 0, 1), ("table", 1, 2), ("wait_digits", 2, 3), ("straus", 3, 4), ("wait_partials", 4, 5),
          ("verdict", 5, 6), ("w2_challenge_split", 11, 7), ("w2_s_B", 7, 8))
 
@@ -61,7 +62,7 @@ def main():
         cp._native.check(fn(gpu._h, 3, buf.ctypes.data, 3, ctypes.byref(got)))
         if it < 3:
             continue
-        st = buf[:13].astype(np.int64)
+        st = buf[:16].astype(np.int64)
         if kern == "wide":
             real_us, ticks = (st[11] - st[10]) / 100.0, st[7] - st[0]
         elif small:
@@ -77,10 +78,12 @@ def main():
             for k, name in enumerate(NAMES):
                 per[name].append((st[k + 1] - st[k]) / (ghz * 1e3))
         wall.append(el)
+    if os.environ.get("RAW"):  # the last call's stamps, relative to wave 0's start
+        print(json.dumps({"raw_stamps_minus_start": [int(x - st[0]) if x else 0 for x in st]}))
     med = {k: round(statistics.median(v), 1) for k, v in per.items()}
     out = {"n": n, "calls": calls, "kernel": "k_verify_" + kern,
            "custom_pair": bool(params), "kernel_clock_ghz": statistics.median(clk), "phase_us": med,
-           "kernel_us": round(sum(med[k] for k in names if not k.startswith(("w2_", "w4_"))), 1),
+           "kernel_us": round(sum(med[k] for k in names if not k.startswith(("w1_", "w2_", "w4_"))), 1),
            "call_wall_us": round(statistics.median(wall), 1)}
     print(json.dumps(out))
 
