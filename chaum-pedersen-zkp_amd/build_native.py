@@ -52,10 +52,16 @@ def _run(cmd):
     return r.stdout
 
 
+# Per-unit flags: k_verify_wide's single-wave row loops ran 12 % apart with their placement
+# (Straus 46.6 against 52.7 us for identical loop code, profiles/r05_wide_align_ab.txt);
+# aligned loop heads make that independent of the code before them.
+UNIT_FLAGS = {"wide.hip": ["-falign-loops=64"]}
+
+
 def build_libcpz(force: bool = False, verbose: bool = False, out: str = LIBCPZ, defines=()) -> str:
     """Build the product library.  `out` / `defines` build a tuning variant (e.g.
     CPZ_VERIFY_WAVES=3) elsewhere, for side-by-side measurement with CPZ_LIB=<out>."""
-    units = ["kernels.hip", "rlc.hip", "part.hip", "runtime.hip"]
+    units = ["kernels.hip", "wide.hip", "rlc.hip", "part.hip", "runtime.hip"]
     srcs = [os.path.join(CSRC, u) for u in units] + _headers()
     if not force and not defines and not _newer(out, srcs):
         return out
@@ -70,7 +76,8 @@ def build_libcpz(force: bool = False, verbose: bool = False, out: str = LIBCPZ, 
     def compile_one(u):
         obj = os.path.join(objdir, u.replace(".hip", ".o"))
         if force or defines or _newer(obj, [os.path.join(CSRC, u)] + _headers()):
-            _run(common + ["-c", os.path.join(CSRC, u), "-o", obj])
+            uf = [] if defines and os.environ.get("CPZ_NO_UNIT_FLAGS") else UNIT_FLAGS.get(u, [])  # variants only
+            _run(common + uf + ["-c", os.path.join(CSRC, u), "-o", obj])
         return obj
 
     with ThreadPoolExecutor(max_workers=len(units)) as ex:

@@ -12,7 +12,7 @@ use std::env;
 use std::path::PathBuf;
 use std::process::Command;
 
-const UNITS: [&str; 4] = ["kernels.hip", "rlc.hip", "part.hip", "runtime.hip"];
+const UNITS: [&str; 5] = ["kernels.hip", "wide.hip", "rlc.hip", "part.hip", "runtime.hip"];
 
 fn main() {
     println!("cargo:rerun-if-env-changed=CPZ_LIB_DIR");
@@ -37,8 +37,11 @@ fn main() {
         let input = src.join(unit);
         println!("cargo:rerun-if-changed={}", input.display());
         let obj = out.join(unit.replace(".hip", ".o"));
+        // build_native.py's UNIT_FLAGS: aligned loop heads for the row kernels
+        let unit_flags: &[&str] = if unit == "wide.hip" { &["-falign-loops=64"] } else { &[] };
         let st = Command::new(&hipcc)
             .args([&format!("--offload-arch={arch}"), "-O3", "-std=c++17", "-fPIC", "-c"])
+            .args(unit_flags)
             .arg("-I").arg(&src)
             .arg("-I").arg(&include)
             .arg(&input).arg("-o").arg(&obj)

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "chaum-pedersen-zkp_amd", "csrc")
 LIB = os.path.join(ROOT, "chaum-pedersen-zkp_amd", "lib", "libcpz.so")
 FLAGS = ("CPZ_EXP_SLAB_MOD=4096", "CPZ_EXP_NOSPLIT", "CPZ_CLOCK_PROBE")
-UNITS = ("kernels.hip", "rlc.hip", "runtime.hip")
+UNITS = ("kernels.hip", "wide.hip", "rlc.hip", "runtime.hip")
 
 
 def _hipcc():
