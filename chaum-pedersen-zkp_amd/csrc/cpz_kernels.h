@@ -22,6 +22,14 @@ constexpr int kNielsLevels = 8;
 __host__ __device__ constexpr int niels_level_doublings(int level) {
   return level == 0 ? 0 : (level == 1 ? 128 : (level == 2 ? 64 : (level == 3 ? 192 : 32 * (2 * (level - 4) + 1))));
 }
+// the level holding 2^(32 q) B: k_verify_wide's part q of s'
+constexpr int kNielsLevelOfPart[8] = {0, 4, 2, 5, 1, 6, 3, 7};
+constexpr bool niels_parts_consistent() {
+  for (int q = 0; q < 8; q++)
+    if (niels_level_doublings(kNielsLevelOfPart[q]) != 32 * q) return false;
+  return true;
+}
+static_assert(niels_parts_consistent(), "kNielsLevelOfPart must invert niels_level_doublings");
 constexpr int kCachedEntries = 2 * kTableSlots;   // y and r tables (identity + 1..8): |d| <= 8
 #ifndef CPZ_VERIFY_BLOCK
 #define CPZ_VERIFY_BLOCK 256

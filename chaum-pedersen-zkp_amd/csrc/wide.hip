@@ -70,12 +70,10 @@ __device__ __forceinline__ void wide_varbase(Shared& sh, const VerifyArgs& a, in
   uint32_t sd[kParts];
 #pragma unroll
   for (int k = 0; k < kParts; k++) sd[k] = sh.dig[8 + kParts * h + k];
-  // part q's table: level m with niels_level_doublings(m) = 32 q
-  constexpr int kLevelOfPart[8] = {0, 4, 2, 5, 1, 6, 3, 7};
   const int32_t* tq[kParts];
 #pragma unroll
   for (int k = 0; k < kParts; k++)
-    tq[k] = a.vtab16 + (size_t)(2 * kLevelOfPart[kParts * h + k] + e) * kNielsEntries * 48;
+    tq[k] = a.vtab16 + (size_t)(2 * kNielsLevelOfPart[kParts * h + k] + e) * kNielsEntries * 48;  // 2^(32 q) B_e
   r16::P4 acc = r16::identity(L);
 #pragma unroll 1
   for (int b = 3; b >= 0; b--) {
