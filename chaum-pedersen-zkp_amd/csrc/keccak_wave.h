@@ -13,14 +13,19 @@ namespace cpz {
 // ---------------------------------------------------------------------------------------
 // The layout: state lane j = x + 5 y (0..24) on wave lane j (lanes 25..63
 // repeat lane j mod 25), 64 bits as (lo, hi).  theta's column sums, D's neighbours, pi's moves
-// and chi's two neighbours are ds_bpermute reads of other lanes (18 per round, four dependent
-// levels); rho is a per-lane rotation.  For k_verify_wide's wave 4, which computes ONE
+// and chi's two neighbours are ds_bpermute reads of other lanes (18 per round); rho is a
+// per-lane rotation.  chi's neighbours are read straight from pi's sources (B[x + 1, y] and
+// B[x + 2, y] are rotated lanes of A like B[x, y]), so a round is three dependent exchange
+// levels, not four (33.2 K against 35.2 K cycles for the challenge, profiles/r05_keccak_fused_ab.txt).  For k_verify_wide's wave 4, which computes ONE
 // transcript challenge: on a lone wave the register form's ~190 instructions a round issue one
 // after another, here each lane does ~30.
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t bperm(int src_lane_x4, uint32_t v) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane_x4, (int)v);
 }
+
+// pi's source (x 4) of B[x, y]: A[(3 (y - 3 x)) % 5, x]... as a lane: (3 (y + 5 - 3 x % 5)) % 5 + 5 x
+__device__ __forceinline__ int keccak_pi_src(int x, int y) { return 4 * ((3 * (y + 5 - (3 * x) % 5)) % 5 + 5 * x); }
 
 __device__ __forceinline__ void keccak_lanes(uint32_t& lo, uint32_t& hi, int j) {
   constexpr int rho[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43,
@@ -35,8 +40,8 @@ __device__ __forceinline__ void keccak_lanes(uint32_t& lo, uint32_t& hi, int j) 
   const int c1 = 4 * (x + 5 * ((y + 1) % 5)), c2 = 4 * (x + 5 * ((y + 2) % 5)), c3 = 4 * (x + 5 * ((y + 3) % 5)),
             c4 = 4 * (x + 5 * ((y + 4) % 5));
   const int dm = 4 * ((x + 4) % 5), dp = 4 * ((x + 1) % 5);
-  const int pi = 4 * ((3 * (y + 5 - (3 * x) % 5)) % 5 + 5 * x);  // B[X = x, Y = y] <- A[(3 (Y - 3 X)) % 5, X]
-  const int h1 = 4 * ((x + 1) % 5 + 5 * y), h2 = 4 * ((x + 2) % 5 + 5 * y);
+  const int pi = keccak_pi_src(x, y);  // B[X = x, Y = y] <- A[(3 (Y - 3 X)) % 5, X]
+  const int h1 = keccak_pi_src((x + 1) % 5, y), h2 = keccak_pi_src((x + 2) % 5, y);  // B[x+1, y], B[x+2, y]
 #pragma unroll 1
   for (int round = 0; round < 24; round++) {
     // theta: C[x] (every lane of column x), D[x] = C[x-1] ^ rot(C[x+1], 1)
@@ -62,8 +67,8 @@ __device__ __forceinline__ void keccak_lanes(uint32_t& lo, uint32_t& hi, int j) 
     const uint32_t bl = bperm(pi, nl), bh = bperm(pi, nh);
     // chi: A = B ^ (~B[x + 1] & B[x + 2]); iota on lane 0
     const uint64_t b = ((uint64_t)bh << 32) | bl;
-    const uint64_t b1 = ((uint64_t)bperm(h1, bh) << 32) | bperm(h1, bl);
-    const uint64_t b2 = ((uint64_t)bperm(h2, bh) << 32) | bperm(h2, bl);
+    const uint64_t b1 = ((uint64_t)bperm(h1, nh) << 32) | bperm(h1, nl);
+    const uint64_t b2 = ((uint64_t)bperm(h2, nh) << 32) | bperm(h2, nl);
     uint64_t na = bitop3_64<kChi>(b, b1, b2);
     if (j == 0) na ^= KECCAK_RC(round);
     lo = (uint32_t)na;
