@@ -108,13 +108,22 @@ __device__ __forceinline__ void wide_table(int32_t* tab, const r16::P4& P, const
   tab[slot] = L.row == 3 ? 0 : r16::one(L);  // identity: Y+X = Y-X = Z = 1, 2dT = 0
   const r16::C4 c1 = r16::to_cached(P, L);
   tab[64 + slot] = r16::sel4(c1.ypx, c1.ymx, c1.z, c1.t2d, L);
+  // entries 2..8: Y+X, Y-X, Z, and for now T (row 3's field); their 2 d T afterwards, row r
+  // multiplying entries 2 + r and 6 + r at once -- two products instead of seven in the chain
   r16::P4 M = r16::dbl(P, L);
 #pragma unroll 1
   for (int j = 2; j <= 8; j++) {
     if (j > 2) M = r16::add_b(M, r16::cached_b(c1, false, L), L);
-    const r16::C4 cj = r16::to_cached(M, L);
-    tab[64 * j + slot] = r16::sel4(cj.ypx, cj.ymx, cj.z, cj.t2d, L);
+    tab[64 * j + slot] = r16::sel4(M.Y + M.X, M.Y - M.X, M.Z, M.T, L);
   }
+  __builtin_amdgcn_wave_barrier();  // same-wave LDS: the T words are read back below
+  const int ja = 2 + L.row, jb = L.row < 3 ? 6 + L.row : 5;
+  const int ta = tab[64 * ja + 48 + L.k], tb = tab[64 * jb + 48 + L.k];
+  __builtin_amdgcn_wave_barrier();
+  const int d2 = r16::K_D2(L);
+  const int pa = r16::mul(ta, d2, L), pb = r16::mul(tb, d2, L);
+  tab[64 * ja + 48 + L.k] = pa;
+  if (L.row < 3) tab[64 * jb + 48 + L.k] = pb;
 }
 
 // The half-length Straus loop of a chain over its table (after barrier A): [u] (-Y) for a Y
