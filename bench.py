@@ -18,6 +18,13 @@ Multi-GPU (torchrun, one process per GPU): contiguous shards, no data-path colle
 proofs of the whole job, split over the ranks (strong scaling, configs[3]).  value = all
 ranks' proofs / max-over-ranks time.
 
+Every line, at every N, carries a "c4" object: configs[3] at this world size -- 2^26 proofs split
+over the ranks, per-rank RLC partial keyed by the global index, all-gather of the 32-byte
+partials (RCCL over xGMI at N > 1), combine, barrier-timed and max over ranks; the valid set
+must combine to the identity, and a forged variant (s + 1 in two ranks' shards) must give every
+rank exactly its forged statuses and a non-identity total.  Fewer visible GPUs than ranks is
+refused before the process group is set up.
+
 At N = 1 the same run also measures (reported beside value, never as value): the RLC batch
 check of the same proofs with per-kernel roofline fractions (configs[2]), the 2^24-proof
 batch with 0.1 % forged proofs through the batch check + fallback (configs[4]), the prover
@@ -105,17 +112,21 @@ def _cgroup_cpu_quota():
 
 
 def cpu_threads(requested: int) -> dict:
-    """Threads for the CPU baseline: every CPU this process may run on (sched_getaffinity),
-    whatever OMP_NUM_THREADS says; the cgroup quota (the box's CPU share, which bounds what
-    those threads can get) is reported beside it."""
+    """Threads for the CPU baseline: the cores the job can actually use -- the CPUs this process
+    may run on (sched_getaffinity), capped at the whole CPUs of the cgroup quota (cpu.max; the
+    GPU box gives a job 16 of its 256 affinity CPUs, profiles/r05_box_cpu.txt).  Running one
+    thread per affinity CPU past the quota only oversubscribes the share (r05: 23 K proofs/s on
+    256 threads against 33 K on 16)."""
     try:
         aff = len(os.sched_getaffinity(0))
     except AttributeError:
         aff = os.cpu_count() or 1
     omp = os.environ.get("OMP_NUM_THREADS")
-    t = requested or aff
+    quota = _cgroup_cpu_quota()
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    t = requested or usable
     return {"threads": max(1, t), "affinity_cpus": aff, "omp_num_threads": omp,
-            "cgroup_cpu_quota": _cgroup_cpu_quota()}
+            "cgroup_cpu_quota": quota, "usable_cpus": usable}
 
 
 def cpu_baseline(host_rows, seconds: float, threads: int):
@@ -491,6 +502,117 @@ def c5_extra(gpu, torch, dev, stream, n5, ctx_len):
     return out
 
 
+def c4_forged_indices(n_total: int):
+    """Global indices forged (s + 1) in configs[3]'s forged variant: two pairs, one pair in the
+    second eighth of the index space and one in the sixth, so at 2, 4 and 8 ranks they land in
+    exactly two ranks' shards (ranks 0 / 1, 0 / 2, 1 / 5), and at N = 1 all in rank 0's."""
+    e = n_total // 8
+    return sorted({e + 5, e + 4099, 5 * e + 101, 5 * e + 77777} if e > 77777 else
+                  {e + 5, e + 9, 5 * e + 1, 5 * e + 3})
+
+
+def c4_run(gpu, torch, dist, dev, stream, world, rank, n_total, steps, warmup, backend):
+    """configs[3] at this world size: n_total proofs split over the ranks (contiguous shards,
+    shard_range), each rank reducing its shard to one 32-byte RLC partial whose weights are
+    keyed by the GLOBAL index (cpz_verify_batch_device, first_index = shard start), an
+    all-gather of the partials (RCCL over xGMI with the "nccl" backend) and cpz_combine_partials
+    on every rank.  One step = the whole exchange; barrier + synchronize on both sides of the
+    timed steps, max over ranks.  A valid set must combine to the identity.  Then the forged
+    variant: s + 1 at c4_forged_indices, the batch check with fallback -- every rank's statuses
+    must be exactly its own forged entries (status 1) and the combined total must not be the
+    identity.  This replaces the reference's sequential loops (batch.rs:239-260, 279-309)."""
+    import numpy as np
+
+    from chaum_pedersen.shard import all_gather_partials, shard_range
+    lo, hi = shard_range(n_total, world, rank)
+    n = hi - lo
+    t4 = {k: torch.empty((n, 32), dtype=torch.uint8, device=dev) for k in ("y1", "y2", "r1", "r2", "s")}
+    rows = [t4[k] for k in ("y1", "y2", "r1", "r2", "s")]
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    gpu.prove_synthetic_device(n, SEED_X, SEED_K, *rows, first_index=lo, stream=stream)
+    torch.cuda.synchronize(dev)
+    state = {}
+
+    def step(fallback=False):
+        partial, ok = gpu.verify_batch_device(*rows, st, WEIGHT_SEED, first_index=lo, fallback=fallback,
+                                              stream=stream)
+        parts = all_gather_partials(partial) if world > 1 else [partial]
+        total, ident = gpu.combine_partials(parts)
+        state.update(partial=partial, ok=ok, parts=parts, total=total, ident=ident)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(warmup):
+        step()
+    st.fill_(0xFF)
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    el = time.perf_counter() - t0
+    local_el = el
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    valid_ok = bool(state["ident"] and state["total"] == bytes(32) and state["ok"]
+                    and not int((st != 0).sum().item()))
+    clean = {"total": state["total"].hex(), "identity": bool(state["ident"])}
+
+    # forged variant: s + 1 on the forged entries of this shard, batch check + fallback
+    forged = c4_forged_indices(n_total)
+    mine = [i - lo for i in forged if lo <= i < hi]
+    if mine:
+        _bump_s(torch, t4, mine)
+    st.fill_(0xFF)
+    barrier()
+    torch.cuda.synchronize(dev)
+    f0 = time.perf_counter()
+    step(fallback=True)
+    torch.cuda.synchronize(dev)
+    barrier()
+    f_el = time.perf_counter() - f0
+    got = st.cpu().numpy()
+    bad = np.nonzero(got)[0]
+    exact_local = bool(np.array_equal(bad, np.asarray(mine, dtype=bad.dtype)) and (got[bad] == 1).all())
+    forged_ok = bool((not state["ident"]) and state["total"] != bytes(32) and state["ok"] == (not mine))
+    checks = torch.tensor([int(valid_ok), int(exact_local), int(forged_ok), len(mine)], dtype=torch.int64,
+                          device=dev if backend == "nccl" else "cpu")
+    if world > 1:
+        gathered = [torch.empty_like(checks) for _ in range(world)]
+        dist.all_gather(gathered, checks)
+        per_rank = [g.cpu().tolist() for g in gathered]
+    else:
+        per_rank = [checks.cpu().tolist()]
+    del t4, rows, st
+    torch.cuda.empty_cache()
+    out = {"workload": "configs[3]: %d proofs split over %d GPU%s (contiguous shards), per-rank RLC partial keyed "
+                       "by the global index, all-gather of the 32-B partials (%s), combine on every rank"
+                       % (n_total, world, "s" if world > 1 else "", backend if world > 1 else "world of one"),
+           "proofs_total": n_total, "proofs_per_gpu_max": max(shard_range(n_total, world, r)[1] -
+                                                                shard_range(n_total, world, r)[0]
+                                                                for r in range(world)),
+           "steps": steps, "warmup": warmup, "ms_per_step": el * 1e3 / steps,
+           "proofs_per_s": n_total * steps / el, "scaling": "strong",
+           "identity": valid_ok and all(r[0] for r in per_rank),
+           "combined_total_valid": clean["total"],
+           "forged": {"indices": forged, "per_rank_forged": [r[3] for r in per_rank],
+                      "statuses_exact_every_rank": all(r[1] for r in per_rank),
+                      "combined_total_not_identity": all(r[2] for r in per_rank),
+                      "combined_total": state["total"].hex(), "ms": f_el * 1e3,
+                      "how": "s + 1 at the forged global indices; cpz_verify_batch_device with fallback on every "
+                             "rank, all-gather, combine"},
+           "local_ms_per_step_rank0": local_el * 1e3 / steps}
+    out["ok"] = bool(out["identity"] and out["forged"]["statuses_exact_every_rank"]
+                     and out["forged"]["combined_total_not_identity"])
+    return out
+
+
 def _free_port() -> int:
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -527,7 +649,13 @@ def main():
                     help="proofs of the whole job, split over the ranks (strong scaling; configs[3] = 67108864)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="CPU baseline threads (0: every CPU in the process's affinity set)")
+                    help="CPU baseline threads (0: the usable cores, min(affinity CPUs, cgroup quota))")
+    ap.add_argument("--cpu-oversubscribed", type=int, default=0,
+                    help="also time one thread per affinity CPU past the quota (reported as a note only)")
+    ap.add_argument("--c4-n", type=int, default=1 << 26,
+                    help="configs[3]: proofs of the whole job split over the ranks, per-rank RLC partial + "
+                         "all-gather + combine, measured at every N (0: skip)")
+    ap.add_argument("--c4-steps", type=int, default=None, help="timed configs[3] steps (default: --steps)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("each", "rlc"), default="each",
                     help="each: per-proof verification (configs[1], the headline); rlc: random-linear-"
@@ -573,6 +701,13 @@ def main():
 
     if args.same_device:
         local_rank = 0
+    else:
+        # one rank per GPU: refuse before any collective is set up when the node shows fewer
+        # devices than ranks (device_count does not initialise HIP on this image)
+        ndev = torch.cuda.device_count()
+        if ndev < world or local_rank >= ndev:
+            sys.exit("bench: %d rank(s) (LOCAL_RANK %d) but %d visible GPU(s); one process per GPU is required "
+                     "(--same-device only for rehearsals)" % (world, local_rank, ndev))
     torch.cuda.set_device(local_rank)  # before the process group, so RCCL binds each rank to its own GPU
     dev = torch.device("cuda", local_rank)
     if world > 1:
@@ -654,6 +789,14 @@ def main():
     oc = _load_json("bench/opcount.json") or {}
     peak_mad = oc.get("peaks", {}).get("v_mad_i64_i32_lane_ops_per_s", 28.32e12)
     solo = world == 1
+
+    # -- configs[3] at this N (every rank; N = 1 included) ---------------------------------
+    c4 = None
+    if args.c4_n:
+        c4 = c4_run(gpu, torch, dist, dev, stream, world, rank, args.c4_n,
+                    args.c4_steps if args.c4_steps is not None else args.steps, 1, args.backend)
+        if not c4["ok"]:
+            raise SystemExit("bench: configs[3] check failed: %s" % json.dumps(c4))
 
     # -- extras at N = 1 ------------------------------------------------------------------
     rlc_extra = None
@@ -797,14 +940,17 @@ def main():
             cpu["affinity_cpus"] = th["affinity_cpus"]
             cpu["omp_num_threads"] = th["omp_num_threads"]
             cpu["cgroup_cpu_quota"] = th["cgroup_cpu_quota"]
-            omp = th["omp_num_threads"]
-            if cpu.get("value") and omp and omp.isdigit() and 1 < int(omp) < th["threads"]:
-                # the box's per-job CPU share (OMP_NUM_THREADS) beside the all-core figure
+            cpu["cores_basis"] = ("min(affinity CPUs %d, whole CPUs of the cgroup quota %s) = %d threads, one per "
+                                  "usable core" % (th["affinity_cpus"], th["cgroup_cpu_quota"], th["usable_cpus"])
+                                  if not args.cpu_threads else "--cpu-threads %d" % args.cpu_threads)
+            if cpu.get("value") and th["affinity_cpus"] > th["threads"] and args.cpu_oversubscribed:
+                # note only: one thread per affinity CPU, past the quota (r05's mislabelled figure)
                 sys.path.insert(0, os.path.join(ROOT, "oracle"))
                 import coracle  # CPU baseline only (test infrastructure)
-                sub = coracle.time_verify(rows, seconds=max(2.0, args.cpu_seconds / 4), threads=int(omp))
-                cpu["at_omp_threads"] = {"threads": int(omp), "value": sub.get("value"),
-                                         "verify_one_value": sub.get("verify_one_value")}
+                sub = coracle.time_verify(rows, seconds=max(2.0, args.cpu_seconds / 4), threads=th["affinity_cpus"])
+                cpu["note_oversubscribed"] = {"threads": th["affinity_cpus"], "value": sub.get("value"),
+                                              "what": "one thread per affinity CPU, past the cgroup quota: "
+                                                      "a note, not the baseline"}
 
     if rank == 0:
         if args.mode == "each":
@@ -838,6 +984,11 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if c4:
+            if args.same_device:   # ranks sharing one GPU: correctness only, no rate
+                c4.update(proofs_per_s=None, ms_per_step=None, local_ms_per_step_rank0=None)
+                c4["forged"]["ms"] = None
+            line["c4"] = c4
         if rlc_extra:
             line["rlc"] = rlc_extra
         if c5:

@@ -776,9 +776,11 @@ class BatchVerifier:
         (batch.rs:239-240), whatever entry point each group takes -- so a caller that keeps
         using a seeded rng sees the reference's stream.  The first draw's first 32 bytes key
         the RLC weights, so `rng` must be a CSPRNG (the reference requires CryptoRngCore):
-        secrets.SystemRandom(), or None for os.urandom.  A predictable rng (random.Random)
-        would let forgeries be built whose weighted errors cancel, and is refused whenever a
-        group takes the RLC check.  A one-entry batch's RLC check (threshold lowered to 1) is
+        secrets.SystemRandom(), or None for os.urandom.  A predictable rng would let forgeries
+        be built whose weighted errors cancel.  Only one such source is detected -- a
+        random.Random (other than SystemRandom) is refused whenever a group takes the RLC
+        check; any other caller-supplied rng is trusted to be a CSPRNG, as the reference's
+        CryptoRngCore bound trusts its implementors.  A one-entry batch's RLC check (threshold lowered to 1) is
         keyed by os.urandom.  Entries are `Proof` values, which may have been built with
         Proof(...) (Proof::new: no identity / zero-s checks), so every call is equations-only:
         verify_one's equations alone decide (batch.rs:185-231).  Either entry point returns

@@ -105,11 +105,13 @@ struct ProbeGatherArgs {
   uint8_t* out_present;
 };
 
-// Launches of at most kQuadVerifyMax proofs are verified on eight lanes per proof
-// (k_verify_quad), larger ones on one lane per proof (k_verify_each).  cpz_verify_each_device
-// per call (tools/quad_crossover.py): eight lanes 0.39 / 0.40 / 0.41 / 0.42 / 0.78 / 1.52 ms at
-// 1K / 2K / 4K / 8K / 16K / 32K proofs, one lane 1.26-1.31 ms at all of them.  The scratch slab
-// holds kQuadProofScratch bytes of tables per proof for them (VerifyArgs::quad_max).
+// Launches of 2049 .. kQuadVerifyMax proofs are verified on eight lanes per proof
+// (k_verify_quad), larger ones on one lane per proof (k_verify_each); at most 512 take
+// k_verify_wide and up to 2048 k_verify_small (runtime.hip, launch_verify_chunks).  The
+// crossover was measured in r04 (tools/quad_crossover.py, cpz_verify_each_device per call:
+// eight lanes 0.78 / 1.52 ms at 16K / 32K proofs, one lane 1.26-1.31 ms).  The scratch slab
+// holds kQuadProofScratch bytes of tables per proof for them (VerifyArgs::quad_max, the
+// runtime's verify_quad_max: this constant capped by the slab, i.e. by the device's CUs).
 #ifndef CPZ_VERIFY_QUAD
 #define CPZ_VERIFY_QUAD 1
 #endif
@@ -199,7 +201,8 @@ hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st);
 // k_verify_small (kernels.hip): three waves per 8 proofs, the drop-in's latency path.  a.c null:
 // the challenges and response statuses are computed in the kernel from ca (k_challenge's inputs).
 hipError_t launch_verify_small(const VerifyArgs& a, const ChallengeArgs& ca, hipStream_t st);
-// one proof per workgroup of five waves (six with vtab16), field products on 16-lane rows (fe16.h)
+// one proof per workgroup of six waves (4 + CPZ_WIDE_VB_WAVES = eight with vtab16), field products
+// on 16-lane rows (fe16.h)
 hipError_t launch_verify_wide(const VerifyArgs& a, const ChallengeArgs& ca, hipStream_t st);
 int verify_each_blocks_per_cu();  // resident k_verify_each blocks per CU (occupancy API)
 hipError_t launch_prove_points(const ProveArgs& a, hipStream_t st);

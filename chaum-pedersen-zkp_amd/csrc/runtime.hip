@@ -196,7 +196,9 @@ struct GenSet {
 #define CPZ_GEN_CACHE 4
 #endif
 constexpr int kGenCache = CPZ_GEN_CACHE;
-// Light sets (64 KB of Niels tables + the transcript prefix each) a context keeps.
+// Light sets a context keeps: each holds the pair's Niels tables (16 bases x 128 ge_niels, 245 KB)
+// and their 16-bit-limb copy (16 x 128 x 48 int32, 196 KB) -- ~440 KB per set, ~28 MB for all 64 --
+// plus the transcript prefix.
 constexpr int kLightCache = 64;
 
 }  // namespace
@@ -389,7 +391,7 @@ int build_niels_prefix(cpz_ctx* ctx, GenSet& e, const uint8_t both[64]) {
 }
 
 // Make the tables of (g, h) current.  A cached full set (combs) is reused.  need_comb false (a
-// per-proof call of at most kVarBaseMax proofs on a pair other than the default one): a cached
+// per-proof call of at most var_base_max(ctx) proofs on a pair other than the default one): a cached
 // light set is reused, or one is built -- k_build_niels and k_transcript_prefix only, ~0.5 ms
 // instead of the combs' ~3 ms, timed as stage 13 -- and the call verifies with variable bases.
 // Otherwise the least recently used full set (an unused one first) is rebuilt: k_build_niels,
@@ -434,8 +436,9 @@ int ensure_generators(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32], bo
     const size_t comb_bytes = (size_t)2 * cpz::kCombPerBase * sizeof(cpz::ge_niels);
     if (e.comb.ensure(comb_bytes) != hipSuccess) {
       (void)hipGetLastError();
-      for (int k = 0; k < ctx->gen_cap; k++)  // trim: every other full set
+      for (int k = 0; k < ctx->gen_cap; k++)  // trim: every other full set ...
         if (&ctx->gen[k] != &e) ctx->gen[k].release();
+      for (GenSet& l : ctx->light) l.release();  // ... and every light set
       CPZ_HIP(e.comb.ensure(comb_bytes));
     }
     CPZ_HIP(e.comb_q.ensure((size_t)2 * cpz::kCombWindows * sizeof(cpz::ge_p3)));
@@ -497,8 +500,9 @@ int verify_grid(cpz_ctx* ctx, size_t n) {
 #endif
 constexpr int64_t kSmallMax = CPZ_SMALL_MAX;
 // Launches of at most wide_max() proofs (default CPZ_WIDE_MAX, environment CPZ_WIDE_MAX for
-// measurement) take k_verify_wide: a workgroup of five waves per proof, field products on
-// 16-lane rows -- the shortest chain for a few proofs; custom generators stay on k_verify_small.
+// measurement) take k_verify_wide: a workgroup of six waves per proof (eight with a light set's
+// variable-base generators), field products on 16-lane rows -- the shortest chain for a few
+// proofs.  Light-set calls take it too (its variable-base waves read VerifyArgs::vtab16).
 #ifndef CPZ_WIDE_MAX
 #define CPZ_WIDE_MAX 512
 #endif
@@ -522,6 +526,24 @@ int64_t wide_max() {
 #ifndef CPZ_VERIFY_CHUNK_DIV
 #define CPZ_VERIFY_CHUNK_DIV 2
 #endif
+// Blocks per verify launch (half the occupancy grid) and the bytes of one verify stream's table
+// slab, which every stream owns at a fixed offset whatever a call's grid.
+int verify_full_grid(const cpz_ctx* ctx) {
+  return (occupancy_grid(ctx) + CPZ_VERIFY_CHUNK_DIV - 1) / CPZ_VERIFY_CHUNK_DIV;
+}
+size_t verify_slab_bytes(const cpz_ctx* ctx) {
+  return (size_t)verify_full_grid(ctx) * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached);
+}
+// Launches of at most this many proofs take the eight-lane kernel (k_verify_quad): kQuadVerifyMax,
+// bounded by the tables one slab holds -- full * 128 proofs, which depends on the device's CUs
+// (16384 on the 256-CU MI355X, 14080 on a 110-CU part).
+int64_t verify_quad_max(const cpz_ctx* ctx) {
+  return std::min<int64_t>(cpz::kQuadVerifyMax, (int64_t)(verify_slab_bytes(ctx) / cpz::kQuadProofScratch));
+}
+// Per-proof calls of at most this many proofs on a pair without cached combs verify with
+// variable bases (light sets), which only the eight-lane and latency kernels support: the same
+// bound as verify_quad_max, so a light-set call never reaches k_verify_each.
+int64_t var_base_max(const cpz_ctx* ctx) { return std::min<int64_t>(cpz::kVarBaseMax, verify_quad_max(ctx)); }
 // Round-robin position of the verify launches of one call that enqueues several batches
 // (the host-buffer pipeline): launches keep alternating streams across batches, and the
 // streams are joined once at the end.
@@ -543,10 +565,10 @@ int join_verify_streams(cpz_ctx* ctx, hipStream_t st) {
 int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hipStream_t st, VerifyRR* rr,
                          bool join, const cpz::ChallengeArgs* ca = nullptr) {
   static_assert(CPZ_VERIFY_STREAMS >= 1 && CPZ_VERIFY_STREAMS <= 4, "1..4 verify streams");
-  const int full = (occupancy_grid(ctx) + CPZ_VERIFY_CHUNK_DIV - 1) / CPZ_VERIFY_CHUNK_DIV;
+  const int full = verify_full_grid(ctx);
   const int grid = std::min(full, verify_grid(ctx, (size_t)va.n));
   // every stream owns a full-size slab at a fixed offset, whatever this call's grid
-  const size_t slab = (size_t)full * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached);
+  const size_t slab = verify_slab_bytes(ctx);
   const int64_t per = (int64_t)grid * cpz::kVerifyBlock;
   const int64_t chunks = (va.n + per - 1) / per;
   const int nst = rr ? CPZ_VERIFY_STREAMS : (int)std::min<int64_t>(CPZ_VERIFY_STREAMS, chunks);
@@ -572,7 +594,7 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
     v.c = va.c + 8 * a;
     if (va.pre) v.pre = va.pre + 4 * a;
     v.status = va.status + a;
-    v.quad_max = std::min<int64_t>(cpz::kQuadVerifyMax, (int64_t)(slab / cpz::kQuadProofScratch));
+    v.quad_max = verify_quad_max(ctx);
 #if defined(CPZ_CLOCK_PROBE)
     CPZ_HIP(ctx->clk[3].ensure(cpz::kSmallStamps * sizeof(uint64_t)));
     ctx->clk_waves[3] = 1;
@@ -592,7 +614,7 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
         v.c = nullptr;  // computed in the kernel
       }
       StageTimer t(ctx, stage, sc);
-      if (v.n <= wide_max() && (!v.vtab || v.vtab16))
+      if (v.n <= wide_max())  // a light set always carries vtab16 beside vtab (build_niels_prefix)
         CPZ_HIP(cpz::launch_verify_wide(v, cc, sc));
       else
         CPZ_HIP(cpz::launch_verify_small(v, cc, sc));
@@ -621,8 +643,10 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
   return CPZ_OK;
 }
 
-// Challenge + verify of n proofs on `st`.  c_buf: where the challenges go (default: the
-// context's buffer from offset 0); rr / join: see VerifyRR; ctx_end: see ChallengeArgs.
+// Challenge + verify of n proofs on `st`.  c_buf: where k_challenge writes the challenges
+// (default: the context's buffer from offset 0) -- launches of at most kSmallMax proofs compute
+// them inside k_verify_small / k_verify_wide and leave c_buf unwritten, so no caller may read
+// challenges back from it; rr / join: see VerifyRR; ctx_end: see ChallengeArgs.
 int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
                    const void* s, const void* ctx_bytes, const uint64_t* ctx_off, const uint8_t* ctx_present,
                    uint8_t* status, hipStream_t st, uint32_t* c_buf = nullptr, VerifyRR* rr = nullptr,
@@ -657,8 +681,8 @@ int enqueue_verify(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const
   va.c = ca.c_out;
   va.status = status;
   va.comb = static_cast<const cpz::ge_niels*>(ctx->gs->comb.p);
-  if (!ctx->gs->full) {  // a light set: variable-base generators (ensure_generators, n <= kVarBaseMax)
-    if ((int64_t)n > cpz::kVarBaseMax) return fail(CPZ_EINVAL, "internal: variable-base call above kVarBaseMax");
+  if (!ctx->gs->full) {  // a light set: variable-base generators (ensure_generators, n <= var_base_max)
+    if ((int64_t)n > var_base_max(ctx)) return fail(CPZ_EINVAL, "internal: variable-base call above var_base_max");
     va.comb = nullptr;
     va.vtab = static_cast<const cpz::ge_niels*>(ctx->gs->tab.p);
     va.vtab16 = static_cast<const int32_t*>(ctx->gs->tab16.p);
@@ -1096,10 +1120,10 @@ int verify_prepared_blocks(cpz_ctx* ctx, int64_t n, const void* s, uint8_t* stat
   if (block_proofs <= 0 || cpz::kVerifyBlock % block_proofs != 0) return CPZ_EINVAL;
   const int64_t G = cpz::kVerifyBlock / block_proofs;
   if (nb <= 0) return CPZ_OK;
-  const int full = (occupancy_grid(ctx) + CPZ_VERIFY_CHUNK_DIV - 1) / CPZ_VERIFY_CHUNK_DIV;
-  const size_t slab = (size_t)full * cpz::kVerifyBlock * cpz::kCachedEntries * sizeof(cpz::ge_cached);
+  const int full = verify_full_grid(ctx);
+  const size_t slab = verify_slab_bytes(ctx);
   CPZ_HIP(ctx->scratch.ensure((size_t)CPZ_VERIFY_STREAMS * slab));
-  const int64_t quad_max = std::min<int64_t>(cpz::kQuadVerifyMax, (int64_t)(slab / cpz::kQuadProofScratch));
+  const int64_t quad_max = verify_quad_max(ctx);
   if (CPZ_VERIFY_QUAD && nb * block_proofs <= quad_max) {  // one eight-lanes-per-proof launch (k_verify_quad)
     cpz::VerifyArgs v;
     v.n = n;
@@ -1575,6 +1599,12 @@ int ctx_create(int device_ordinal, cpz_ctx** out) {
     return fail(CPZ_EHIP, std::string("context setup: ") + hipGetErrorString(e));
   }
   ctx->cus = prop.multiProcessorCount;
+  // CPZ_CUS (tests): size grids and slabs as on a part with fewer CUs, e.g. the 110-CU case whose
+  // eight-lane bound (verify_quad_max) is 14080 rather than 16384
+  if (const char* v = std::getenv("CPZ_CUS")) {
+    const int k = std::atoi(v);
+    if (k >= 1 && k < ctx->cus) ctx->cus = k;
+  }
   ctx->verify_blocks_per_cu = cpz::verify_each_blocks_per_cu();  // the grid-stride verify grid fills the chip once
   // full (g, h) sets (128 MiB of combs each) this context may keep: CPZ_GEN_CACHE=1..4
   if (const char* v = std::getenv("CPZ_GEN_CACHE")) {
@@ -2059,7 +2089,7 @@ int cpz_verify_each_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t h[32
   if (d_ctx_off && !d_ctx_bytes) return fail(CPZ_EINVAL, "ctx_off given without ctx_bytes");
   CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
-  int rc = ensure_generators(ctx, g, h, (int64_t)n > cpz::kVarBaseMax);
+  int rc = ensure_generators(ctx, g, h, (int64_t)n > var_base_max(ctx));
   if (rc) return rc;
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   if ((rc = order_after_last(ctx, st))) return rc;
@@ -2086,7 +2116,7 @@ int cpz_verify_each_ex(cpz_ctx* ctx, uint32_t flags, const uint8_t g[32], const 
   if (ctx_off && !ctx_bytes && ctx_off[n] != ctx_off[0]) return fail(CPZ_EINVAL, "ctx_off given without ctx_bytes");
   CallLock lock(ctx, flags);
   CPZ_HIP(hipSetDevice(ctx->device));
-  int rc = ensure_generators(ctx, g, h, (int64_t)n > cpz::kVarBaseMax);
+  int rc = ensure_generators(ctx, g, h, (int64_t)n > var_base_max(ctx));
   if (rc) return rc;
   if ((rc = order_after_last(ctx, ctx->stream))) return rc;
   const uint8_t* host[5] = {y1, y2, r1, r2, s};
@@ -2338,8 +2368,8 @@ int verify_response_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2,
   va.c = static_cast<const uint32_t*>(ctx->c.p);
   va.status = status;
   va.comb = static_cast<const cpz::ge_niels*>(ctx->gs->comb.p);
-  if (!ctx->gs->full) {  // a light set: variable-base generators (ensure_generators, n <= kVarBaseMax)
-    if ((int64_t)n > cpz::kVarBaseMax) return fail(CPZ_EINVAL, "internal: variable-base call above kVarBaseMax");
+  if (!ctx->gs->full) {  // a light set: variable-base generators (ensure_generators, n <= var_base_max)
+    if ((int64_t)n > var_base_max(ctx)) return fail(CPZ_EINVAL, "internal: variable-base call above var_base_max");
     va.comb = nullptr;
     va.vtab = static_cast<const cpz::ge_niels*>(ctx->gs->tab.p);
     va.vtab16 = static_cast<const int32_t*>(ctx->gs->tab16.p);
@@ -2430,7 +2460,7 @@ int cpz_verify_response_device(cpz_ctx* ctx, const uint8_t g[32], const uint8_t 
   if (!rows_aligned(rows, 6)) return fail(CPZ_EINVAL, "device inputs must be 16-byte aligned");
   CallLock lock(ctx);
   CPZ_HIP(hipSetDevice(ctx->device));
-  int rc = ensure_generators(ctx, g, h, (int64_t)n > cpz::kVarBaseMax);
+  int rc = ensure_generators(ctx, g, h, (int64_t)n > var_base_max(ctx));
   if (rc) return rc;
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   if ((rc = order_after_last(ctx, st))) return rc;
@@ -2453,7 +2483,7 @@ int cpz_verify_response_ex(cpz_ctx* ctx, uint32_t flags, const uint8_t g[32], co
   if (!y1 || !y2 || !r1 || !r2 || !s || !c || !status_out) return fail(CPZ_EINVAL, "null input pointer");
   CallLock lock(ctx, flags);
   CPZ_HIP(hipSetDevice(ctx->device));
-  int rc = ensure_generators(ctx, g, h, (int64_t)n > cpz::kVarBaseMax);
+  int rc = ensure_generators(ctx, g, h, (int64_t)n > var_base_max(ctx));
   if (rc) return rc;
   if ((rc = order_after_last(ctx, ctx->stream))) return rc;
   const uint8_t* host[5] = {y1, y2, r1, r2, s};

@@ -50,9 +50,9 @@ constexpr std::size_t MAX_BATCH_SIZE = 1000;  // batch.rs:48
 // Smallest Parameters group that takes the RLC batch check rather than per-proof
 // verification (both return verify_one's outcome per entry).  The same threshold as
 // rust/reference-patch/gpu.rs (RLC_MIN_GROUP), from the per-call latency table
-// profiles/r04_small_batch.json: one synchronous host-buffer call takes 0.39-0.48 ms per proof
-// (eight lanes each, k_verify_quad) at every n from 1 to 1000, against 0.54-0.59 ms through the
-// RLC check at n <= 100 and 0.74 ms at 1000, so no group of at most MAX_BATCH_SIZE entries takes
+// bench.py's small_batch (profiles/r05_bench_i.json): one synchronous host-buffer call takes
+// 0.112-0.118 ms per proof at n = 1 .. 100 (k_verify_wide) and 0.265 ms at 1000 (k_verify_small),
+// against 0.54-0.59 ms through the RLC check at n <= 100 and 0.73 ms at 1000, so no group of at most MAX_BATCH_SIZE entries takes
 // the RLC check (set_rlc_min_group lowers it; a one-entry batch is then keyed by the OS's
 // randomness, not the caller's).
 constexpr std::size_t RLC_MIN_GROUP = 1001;

@@ -23,8 +23,8 @@ impl BatchVerifier {
     /// Verifies all proofs in the batch (batch.rs:171-183): `Err` for an empty batch,
     /// otherwise one `Result` per entry in entry order.  With the `gpu` feature the
     /// verification runs on the MI355X (gpu.rs: every `Parameters` group of this API's
-    /// batches, at most 1000 entries, is verified per proof, `verify_one` on eight GPU lanes
-    /// per entry; a group of at least RLC_MIN_GROUP entries would take the
+    /// batches, at most 1000 entries, is verified per proof, `verify_one` by k_verify_wide
+    /// (a six-wave workgroup per proof) or k_verify_small (three waves per 8 proofs); a group of at least RLC_MIN_GROUP entries would take the
     /// random-linear-combination check keyed by `rng`, with an exact per-entry fallback);
     /// the per-entry results are those of `verify_one`, and `rng` is drawn as the reference
     /// draws it (64 bytes per entry for n >= 2, nothing for n == 1).

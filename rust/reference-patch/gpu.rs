@@ -10,7 +10,9 @@
 //! appearance):
 //!   * a group of fewer than RLC_MIN_GROUP entries -- every group of this API's batches (at
 //!     most 1000 entries), from the measured latencies -- runs cpz_verify_each: `verify_one`
-//!     per entry (batch.rs:185-231), eight GPU lanes per proof;
+//!     per entry (batch.rs:185-231): up to 512 proofs one proof per six-wave workgroup with
+//!     its field products on 16-lane rows (k_verify_wide), up to 2048 three waves per 8
+//!     proofs (k_verify_small);
 //!   * a larger group takes the random-linear-combination check (cpz_verify_batch: the batch
 //!     equation with the weights on every term, one Pippenger MSM), keyed by the first 32
 //!     bytes `rng` yields -- or, for a one-entry batch, which the reference verifies with
@@ -60,10 +62,10 @@ const CONTEXTS_PER_DEVICE: usize = 2;
 /// Smallest `Parameters` group sent to the RLC batch check; smaller groups are verified per
 /// proof (cpz_verify_each).  Both return `verify_one`'s outcome; the threshold only picks the
 /// faster entry point at the batch sizes this API carries (n <= 1000, batch.rs:48), from the
-/// per-call latency table profiles/r04_small_batch.json (bench.py small_batch): per proof on
-/// eight lanes each (k_verify_quad) 0.39-0.48 ms at every n from 1 to 1000, the RLC check
-/// 0.54-0.59 ms at n <= 100 and 0.74 ms at 1000, so no group of this API (at most 1000
-/// entries, batch.rs:48) takes the RLC check; the path stays for callers that lower it.
+/// per-call latency table of bench.py's small_batch (profiles/r05_bench_i.json): per proof
+/// 0.112-0.118 ms at n = 1 .. 100 (k_verify_wide) and 0.265 ms at 1000 (k_verify_small), the
+/// RLC check 0.54-0.59 ms at n <= 100 and 0.73 ms at 1000, so no group of this API (at most
+/// 1000 entries, batch.rs:48) takes the RLC check; the path stays for callers that lower it.
 const RLC_MIN_GROUP: usize = 1001;
 
 /// The process's verifier contexts (see above).

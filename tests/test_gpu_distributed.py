@@ -203,7 +203,8 @@ def test_bench_rlc_four_rank_rehearsal(launcher):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.pop("WORLD_SIZE", None)
     args = ["--gpus", "4", "--mode", "rlc", "--n-total", str(1 << 20), "--same-device", "--backend", "gloo",
-            "--steps", "1", "--warmup", "1", "--extras", "0", "--no-cpu-baseline"]
+            "--steps", "1", "--warmup", "1", "--extras", "0", "--no-cpu-baseline", "--c4-n", str(1 << 21),
+            "--c4-steps", "1"]
     if launcher == "torchrun":
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py")] + args
@@ -217,3 +218,14 @@ def test_bench_rlc_four_rank_rehearsal(launcher):
     assert d["value"] is None and d["ms_per_step"] is None and d["n_gpus"] == 4
     assert d["rehearsal"]["combined_total_identity"] is True
     assert d["rehearsal"]["combined_total"] == "00" * 32
+    # configs[3]'s object at this world size: shards of 2^21 proofs over 4 ranks, identity on the
+    # valid set; the forged variant lands in two ranks' shards (ranks 0 and 2), every rank's
+    # statuses are exactly its forged entries, and the combined total is not the identity
+    c4 = d["c4"]
+    assert c4["ok"] is True and c4["identity"] is True and c4["combined_total_valid"] == "00" * 32
+    assert c4["proofs_total"] == 1 << 21 and c4["proofs_per_gpu_max"] == 1 << 19
+    f = c4["forged"]
+    assert f["per_rank_forged"] == [2, 0, 2, 0]
+    assert f["statuses_exact_every_rank"] is True and f["combined_total_not_identity"] is True
+    assert f["combined_total"] != "00" * 32
+    assert c4["proofs_per_s"] is None   # ranks sharing one GPU: no rate

@@ -61,7 +61,7 @@ def test_small_batch_eight_lanes_every_forgery_kind(gpu, golden, n):
 def test_small_kernel_every_forgery_kind_and_context_shape(gpu, golden, n):
     """Launches of at most 2048 proofs compute the transcript challenge inside the verify
     kernel (fixed schedules for no context and 32-byte contexts, the byte-wise sponge for
-    Some(b"") and other lengths): up to 512 proofs k_verify_wide (a five-wave workgroup per
+    Some(b"") and other lengths): up to 512 proofs k_verify_wide (a six-wave workgroup per
     proof), then k_verify_small (three waves per 8 proofs).  On both sides of the 2048 limit
     and at the 8-proof workgroup edges every status and challenge equals the C oracle's."""
     _every_forgery_kind(gpu, golden, n, n, 31 + n, ctx_shapes=True)

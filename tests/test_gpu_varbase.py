@@ -1,10 +1,11 @@
 """Custom `Parameters` without the fixed-base combs: every BatchVerifier entry
 carries its own (g, h) (batch.rs:52, gadgets.rs:77-103), and a per-proof call of at most
-kVarBaseMax (16384) proofs on a pair whose combs are not cached verifies [s'] g and [s'] h from
-the pair's 128-entry Niels tables inside the Straus loop (k_verify_quad<kVar>) instead of
-building 128 MiB of combs.  Every status is compared with the oracle's verify_one under the
-entry's own generators; the context's stage 13 counts the light table builds and stage 7 (the
-comb builds) stays at zero."""
+var_base_max proofs (the eight-lane bound: 16384 on MI355X) on a pair whose combs are not cached
+verifies [s'] g and [s'] h from the pair's 128-entry Niels tables -- k_verify_wide's
+variable-base waves up to 512 proofs, k_verify_small up to 2048, k_verify_quad<kVar> above --
+instead of building 128 MiB of combs.  Every status is compared with the oracle's verify_one
+under the entry's own generators; the context's stage 13 counts the light table builds and
+stage 7 (the comb builds) stays at zero."""
 import hashlib
 
 import numpy as np
@@ -143,3 +144,35 @@ def test_varbase_statuses_equal_comb_path_on_malformed_entries(gpu, golden):
     assert light_eq[13] == 1 and light_eq[14] == 1 and light_eq[12] == cp.STATUS_BAD_SCALAR
     # caller challenges = the transcript's own (Verifier::verify_response): the same statuses
     assert np.array_equal(resp, light)
+
+
+def test_light_set_bound_follows_the_devices_slab(gpu, monkeypatch):
+    """the light-set threshold is the runtime's eight-lane bound (verify_quad_max:
+    kQuadVerifyMax capped by one verify slab's tables, full * 128 proofs), not the constant
+    16384.  A context sized as on a 110-CU part (CPZ_CUS=110: bound 14080) verifies a custom
+    pair's call of 14080 proofs from the light set and one of 14081 .. 16384 proofs (which
+    used to fail with hipErrorInvalidValue) by building the pair's combs; every status equals
+    the forged set."""
+    pair = _pairs(1, tag=b"cus110")[0]
+    n = 15000
+    rng = np.random.default_rng(110)
+    x = rng.integers(0, 256, (n, 32), dtype=np.uint8)   # taken mod l by cpz_prove
+    k = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    rows = gpu.prove(x, k, params=pair)
+    forged = list(range(5, n, 997))
+    for i in forged:
+        v = (int.from_bytes(rows["s"][i].tobytes(), "little") + 1) % O.L
+        rows["s"][i] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)
+    monkeypatch.setenv("CPZ_CUS", "110")
+    for m, light in ((14080, True), (14081, False), (n, False)):
+        cols = [np.ascontiguousarray(rows[q][:m]) for q in ("y1", "y2", "r1", "r2", "s")]
+        with cp.Gpu(0) as small:
+            small.set_timing(True)
+            small.stage_times()
+            st = small.verify_each(*cols, params=pair)
+            stg = small.stage_times()
+        exp = np.zeros(m, np.uint8)
+        exp[[i for i in forged if i < m]] = 1
+        assert np.array_equal(st, exp), (m, np.nonzero(st != exp)[0][:8])
+        assert stg.get("generators_varbase", (0.0, 0))[1] == (1 if light else 0), (m, stg)
+        assert stg.get("generators", (0.0, 0))[1] == (0 if light else 1), (m, stg)
