@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-6 GPU session A: the new tests (light-set bound at 110 CUs, the world-4 rehearsal's c4
-# object), then the default bench line with configs[3] measured at N = 1.
+# object), the default bench line with configs[3] measured at N = 1, then the f64-limb
+# microbenchmark (tools/ubench/fe_f64.hip).
 set -o pipefail
 export PYTHONDONTWRITEBYTECODE=1
 export TMPDIR=/tmp
@@ -13,3 +14,7 @@ import json; d=json.load(open('gpurun_out/bench_a.json'))
 print('value', d['value'], 'frac', d['roofline']['frac'], 'cpu', d['cpu_baseline']['value'], d['cpu_baseline']['cores'], d['cpu_baseline'].get('cores_basis'))
 c=d['c4']; print('c4', c['proofs_per_s'], c['ms_per_step'], c['identity'], c['forged'])
 print('c5', d['c5']['ratio_to_per_proof'], d['c5_ctx']['ratio_to_per_proof'], 'rlc', d['rlc']['proofs_per_s'])"
+# f64 limbs against radix 2^25.5 (ISA VALU counts per call from profiles/r06_fe_f64_isa.txt)
+timeout -k 10 120 tools/ubench/fe_f64 20 149 214 118 175 > gpurun_out/fe_f64_a.jsonl 2>&1; rc=$?
+cat gpurun_out/fe_f64_a.jsonl
+exit $rc
