@@ -207,8 +207,12 @@ void rlc_sort_geometry(RlcMsmArgs& a, int64_t npts);
 // (start | sort: extra, hist, bscan, scan, coarse, fine | bucket | bucket fix | segment + window
 // | final).
 constexpr int kRlcMsmMarks = 6;
+// final_wait / final_done (overlapped spans, runtime.hip rlc_range_launch): the stream waits for
+// final_wait before k_rlc_final (the previous span's final, which owns RlcMsmArgs::total) and
+// records final_done after it; everything before the final overlaps freely.
 hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0, int64_t b1, const ge_niels* tab,
-                          hipStream_t st, hipEvent_t* marks = nullptr);
+                          hipStream_t st, hipEvent_t* marks = nullptr, hipEvent_t final_wait = nullptr,
+                          hipEvent_t final_done = nullptr);
 hipError_t launch_msm_load(int64_t n, const uint32_t* pts_enc, const uint32_t* scalars, ge_niels* pts,
                            int16_t* digits, int64_t dstride, int* bad, hipStream_t st);
 hipError_t launch_rlc_combine(const uint32_t* parts, int k, uint32_t* out, int* flags, hipStream_t st);

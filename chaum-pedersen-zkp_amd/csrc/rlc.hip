@@ -963,7 +963,7 @@ void rlc_sort_geometry(RlcMsmArgs& a, int64_t npts) {
 }
 
 hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0, int64_t b1, const ge_niels* tab,
-                          hipStream_t st, hipEvent_t* marks) {
+                          hipStream_t st, hipEvent_t* marks, hipEvent_t final_wait, hipEvent_t final_done) {
   hipError_t e;
   auto mark = [&](int k) -> hipError_t { return marks ? hipEventRecord(marks[k], st) : hipSuccess; };
   if ((e = mark(0)) != hipSuccess) return e;
@@ -1015,8 +1015,10 @@ hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0,
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   if ((e = mark(4)) != hipSuccess) return e;
+  if (final_wait && (e = hipStreamWaitEvent(st, final_wait, 0)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_rlc_final, dim3(1), dim3(64), 0, st, a2);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (final_done && (e = hipEventRecord(final_done, st)) != hipSuccess) return e;
   return mark(5);
 }
 

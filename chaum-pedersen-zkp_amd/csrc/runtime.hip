@@ -248,6 +248,11 @@ struct cpz_ctx {
   // decode / identity flags at [0..1]) and the combine's inputs
   RlcPrepared rl_prep;
   RlcMsmSet rl_msm;
+  // overlapped spans (rlc_range_launch): the second MSM set, its stream, and the events that
+  // start it after the prepare ([0]) and chain the spans' finals ([1 + set])
+  RlcMsmSet rl_msm2;
+  hipStream_t span_stream = nullptr;
+  hipEvent_t span_ev[3] = {nullptr, nullptr, nullptr};
   DevBuf rl_flags, rl_parts;
   // partitioned batch check (part.hip): sorted lists / offsets / window sums of one chunk of
   // blocks, every block's partial and fail flag, the sum's scratch, the failing-block list
@@ -777,7 +782,9 @@ int stage_inputs(cpz_ctx* ctx, size_t n, const uint8_t* const host[5], int count
 // ---- RLC batch path --------------------------------------------------------------------
 // digits row stride: 4 points per proof + g, h, rounded to 8 so that every window row starts
 // 16-byte aligned (k_rlc_hist reads 8 digits per load)
-int64_t rlc_dstride(int64_t cap) { return (4 * cap + 2 + 7) & ~(int64_t)7; }
+// digit rows: 4 cap points + two MSM sets' extra points (g, h) each (kRlcExtraSlots)
+constexpr int64_t kRlcExtraSlots = 4;
+int64_t rlc_dstride(int64_t cap) { return (4 * cap + kRlcExtraSlots + 7) & ~(int64_t)7; }
 // sorted-entry row stride: whole 4096-entry groups
 int64_t rlc_istride(int64_t cap) { return (4 * cap + 2 + 4095) & ~(int64_t)4095; }
 // bucket-head slots per window: one per k_rlc_bucket thread of any MSM the set can hold
@@ -789,7 +796,7 @@ int64_t rlc_hstride(int64_t cap) {
 // The prepared set for a batch of n proofs.
 int rlc_reserve_prepared(RlcPrepared& P, int64_t n) {
   if (n <= P.cap) return CPZ_OK;
-  const int64_t npts = 4 * n + 2;
+  const int64_t npts = 4 * n + kRlcExtraSlots;
   const int64_t nblk = (n + cpz::kRlcPrepBlock - 1) / cpz::kRlcPrepBlock;
   P.cap = 0;  // stays 0 unless every buffer is in place
   CPZ_HIP(P.pts.ensure((size_t)npts * sizeof(cpz::ge_niels)));
@@ -876,19 +883,54 @@ int rlc_msm_args(const RlcPrepared& P, RlcMsmSet& S, int64_t lo, int64_t hi, cpz
 // device (RlcMsmArgs::total).  Random 128-byte gathers run at ~7 TB/s over a 512 MiB array
 // but ~1.8 TB/s over 4 GiB (translation misses, tools/ubench/gather_bytes.hip), so a
 // 2^26-proof MSM over one 32 GiB points array spent 2.8x the per-entry bucket time of a 2^20
-// one.  Synchronises; returns the partial encoding and identity flag.
+// one.
+//
+// Several spans overlap (span_overlap(), default on): consecutive spans alternate between two
+// MSM sets and two streams, so one span's latency-bound sort and tails run beside the other's
+// VALU-bound bucket accumulation.  The only state the spans share is the running total, and
+// the finals that own it are chained by events (launch_rlc_msm's final_wait / final_done);
+// each set's two extra points (g, h with the span's summed scalars) have their own slots in
+// the prepared set (e0 = 4 cap + 2 set).  The last span runs on set 0 and `st`, which waits
+// for the other stream through that chain, so the readers of rl_msm (rlc_range and the
+// fallbacks) and the order of later work on `st` are unchanged.  Synchronises nothing.
+bool span_overlap() {
+  static const bool v = [] {
+    const char* e = std::getenv("CPZ_RLC_SPAN_OVERLAP");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 int rlc_range_launch(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st) {
   static_assert(CPZ_RLC_SPAN % cpz::kRlcPrepBlock == 0, "spans are whole weight blocks");
   static_assert(cpz::kRlcPrepBlock % cpz::kRlcSumBlock == 0, "ranges are whole block sums");
   static_assert(4ll * CPZ_RLC_SPAN + 2 <= cpz::kRlcMaxMsmPoints, "a span's MSM exceeds the sort-entry format");
-  RlcMsmSet& S = ctx->rl_msm;
   const int64_t nspan = (hi - lo + CPZ_RLC_SPAN - 1) / CPZ_RLC_SPAN;
+#if defined(CPZ_CLOCK_PROBE)
+  const bool overlap = false;  // timing-only builds: one clock-probe buffer, spans in order
+#else
+  const bool overlap = nspan > 1 && span_overlap();
+#endif
+  hipStream_t sts[2] = {st, st};
+  if (overlap) {
+    if (int rc = rlc_reserve_msm(ctx->rl_msm2, std::min<int64_t>(hi - lo, CPZ_RLC_SPAN))) return rc;
+    if (!ctx->span_stream) CPZ_HIP(stream_own_queue(&ctx->span_stream, ctx->cus, ctx->device, &ctx->own_queues));
+    for (auto& e : ctx->span_ev)
+      if (!e) CPZ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    CPZ_HIP(hipEventRecord(ctx->span_ev[0], st));  // the second stream starts after st's prior work
+    CPZ_HIP(hipStreamWaitEvent(ctx->span_stream, ctx->span_ev[0], 0));
+    sts[1] = ctx->span_stream;
+  }
   for (int64_t j = 0; j < nspan; j++) {
     const int64_t slo = lo + j * CPZ_RLC_SPAN, shi = std::min<int64_t>(hi, slo + CPZ_RLC_SPAN);
+    const int set = overlap ? (int)((nspan - 1 - j) & 1) : 0;  // the last span on set 0 / st
+    RlcMsmSet& S = set ? ctx->rl_msm2 : ctx->rl_msm;
+    hipStream_t ss = sts[set];
     cpz::RlcMsmArgs m;
     if (int rc = rlc_msm_args(ctx->rl_prep, S, slo, shi, m)) return rc;
+    m.e0 = 4 * ctx->rl_prep.cap + 2 * set;
     if (nspan > 1) {
-      m.total = static_cast<cpz::ge_p3*>(S.total.p);
+      m.total = static_cast<cpz::ge_p3*>(ctx->rl_msm.total.p);  // one running total for both sets
       m.total_first = j == 0;
       m.total_last = j == nspan - 1;
     }
@@ -899,11 +941,11 @@ int rlc_range_launch(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st) {
       const int64_t chunks = ((m.p1 - m.p0) + 2 + m.echunk - 1) / m.echunk;
       ctx->clk_waves[1] = (size_t)((chunks + 255) / 256) * cpz::kRlcWindows * 4;
       CPZ_HIP(ctx->clk[1].ensure(ctx->clk_waves[1] * 40));
-      CPZ_HIP(hipMemsetAsync(ctx->clk[1].p, 0, ctx->clk_waves[1] * 40, st));
+      CPZ_HIP(hipMemsetAsync(ctx->clk[1].p, 0, ctx->clk_waves[1] * 40, ss));
       m.clock_probe = static_cast<uint64_t*>(ctx->clk[1].p);
     }
 #endif
-    StageTimer t(ctx, 3, st);
+    StageTimer t(ctx, 3, ss);
     // phase marks (stages 8-12) when timing: sort, bucket, bucket fix, segment + window, final
     hipEvent_t marks[cpz::kRlcMsmMarks];
     bool timed = ctx->timing;
@@ -912,8 +954,12 @@ int rlc_range_launch(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st) {
     if (!timed)
       for (int k = 0; k < got; k++)
         if (marks[k]) ctx->free_events.push_back(marks[k]);
+    // overlapped: the final waits for the previous span's (the other set's event) and records its own
+    hipEvent_t fwait = overlap && j > 0 ? ctx->span_ev[1 + (1 - set)] : nullptr;
+    hipEvent_t fdone = overlap && j + 1 < nspan ? ctx->span_ev[1 + set] : nullptr;
     CPZ_HIP(cpz::launch_rlc_msm(m, static_cast<const cpz::sc*>(ctx->rl_prep.bsum.p), b0, b1,
-                                static_cast<const cpz::ge_niels*>(ctx->gs->tab.p), st, timed ? marks : nullptr));
+                                static_cast<const cpz::ge_niels*>(ctx->gs->tab.p), ss, timed ? marks : nullptr,
+                                fwait, fdone));
     if (timed)
       for (int k = 0; k + 1 < cpz::kRlcMsmMarks; k++) ctx->marks.push_back({8 + k, marks[k], marks[k + 1]});
   }
@@ -2010,8 +2056,15 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
     (void)hipStreamDestroy(ctx->copy_stream);
   }
   for (DevBuf* b : {&ctx->pz_blob, &ctx->pz_off, &ctx->pz_rows, &ctx->pz_code, &ctx->pz_aux}) b->release();
+  if (ctx->span_stream) {
+    (void)hipStreamSynchronize(ctx->span_stream);
+    (void)hipStreamDestroy(ctx->span_stream);
+  }
+  for (auto& e : ctx->span_ev)
+    if (e) (void)hipEventDestroy(e);
   ctx->rl_prep.release();
   ctx->rl_msm.release();
+  ctx->rl_msm2.release();
   for (DevBuf* b : {&ctx->pt_lists, &ctx->pt_offs, &ctx->pt_wsum, &ctx->pt_part, &ctx->pt_fail, &ctx->pt_tmp,
                     &ctx->pt_blocks, &ctx->pt_assign, &ctx->pt_ldig, &ctx->pt_lsum, &ctx->pt_lpart, &ctx->pt_lfail,
                     &ctx->pt_loc})
