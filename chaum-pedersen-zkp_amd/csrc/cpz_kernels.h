@@ -198,9 +198,6 @@ hipError_t launch_parse_proofs(const ParseArgs& a, hipStream_t st);
 // Fixed-base combs of 2 bases (g, h): bases_scratch holds 2 * kCombWindows ge_p3.
 hipError_t launch_build_comb(const uint32_t* gh_words, ge_p3* bases_scratch, ge_niels* comb, hipStream_t st);
 hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st);
-// k_verify_decode4: the decodes of a.n proofs into a.pre (4 n Niels points) and their
-// decode-level statuses into a.status (in: response statuses), 4 lanes per proof
-hipError_t launch_verify_decode(const VerifyArgs& a, hipStream_t st);
 // k_verify_small (kernels.hip): three waves per 8 proofs, the drop-in's latency path.  a.c null:
 // the challenges and response statuses are computed in the kernel from ca (k_challenge's inputs).
 hipError_t launch_verify_small(const VerifyArgs& a, const ChallengeArgs& ca, hipStream_t st);

@@ -328,44 +328,6 @@ __device__ __forceinline__ void verify_one_row(const VerifyArgs& a, int64_t i, c
                              a.eq_only != 0);
 }
 
-// Per-proof decodes as a kernel of their own (CPZ_VERIFY_SPLIT_DECODE, runtime.hip
-// launch_verify_chunks): one point per lane (lane 4 i + q: -r1, -y1, -r2, -y2 of proof i, the
-// RLC prepare's order and form), the low-register decode at 4 waves per SIMD (the decode's
-// squaring chains stall a SIMD holding only k_verify_each's 2 waves), each proof's
-// decode-level status settled across its quad as verify_proof orders it; k_verify_prepared
-// then checks the equations of the proofs still at status 0.  a.pre: 4 n negated affine Niels
-// points out; a.status: the response status in, the decode-level status out.
-__global__ void __launch_bounds__(256, 4) k_verify_decode4(VerifyArgs a) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t i = t >> 2;
-  const int q = (int)(t & 3);
-  bool ok = true, ident = false;
-  if (i < a.n) {  // whole quads
-    const uint32_t* src = q == 0 ? a.r1 : (q == 1 ? a.y1 : (q == 2 ? a.r2 : a.y2));
-    uint32_t w[8];
-    load_words8(w, src, i);
-    ident = !(q & 1) && words8_zero(w);
-    ge_p3 P;
-    ok = ristretto_decode_lowreg(P, w);
-    store_niels(const_cast<ge_niels*>(a.pre) + t, niels_from_p3_affine(P, true));
-  }
-  int okq = ok ? 1 : 0, idq = ident ? 1 : 0;
-  okq &= __shfl_xor(okq, 1);
-  okq &= __shfl_xor(okq, 2);
-  idq |= __shfl_xor(idq, 1);
-  idq |= __shfl_xor(idq, 2);
-  if (i < a.n && q == 0) {  // verify_proof's precedence (verify.h)
-    const uint8_t st_s = a.status[i];
-    uint8_t st = kStOk;
-    if (!okq) st = kStBadPoint;
-    else if (st_s == kStBadScalar) st = kStBadScalar;
-    else if (idq && !a.eq_only) st = kStIdentity;
-    else if (st_s == kStZeroS) st = kStZeroS;
-    else if (st_s == kStBadChallenge) st = kStBadScalar;
-    a.status[i] = st;
-  }
-}
-
 // The RLC fallback's per-proof pass (rlc_fallback): points, challenges and decode-level
 // statuses come from the RLC prepare of the same batch, so only the equations are checked.
 __global__ void __launch_bounds__(kVerifyBlock, CPZ_VERIFY_WAVES) k_verify_prepared(VerifyArgs a) {
@@ -1030,12 +992,6 @@ hipError_t launch_verify_small(const VerifyArgs& a, const ChallengeArgs& ca, hip
   return hipGetLastError();
 }
 
-
-hipError_t launch_verify_decode(const VerifyArgs& a, hipStream_t st) {
-  if (a.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_verify_decode4, dim3((unsigned)((4 * a.n + 255) / 256)), dim3(256), 0, st, a);
-  return hipGetLastError();
-}
 
 hipError_t launch_verify_each(const VerifyArgs& a, int grid, hipStream_t st) {
   if (a.n <= 0) return hipSuccess;

@@ -209,70 +209,6 @@ CPZ_HD bool ristretto_decode(ge_p3& out, const uint32_t w[8]) {
   return canonical && was_square && !fe_isnegative(t) && !fe_iszero(y);
 }
 
-// ristretto_decode with fewer registers live across the inverse square root's exponent chain
-// (for kernels that want 4 waves per SIMD, k_rlc_decode4): only the encoding's 8 words and the
-// chain's own state cross it; s, u1, u2, v and v u2^2 are recomputed from the words afterwards
-// (4 squarings + 3 products, ~3 % of a decode), the words passed through an empty asm so the
-// compiler cannot merge the recomputation with the first pass and keep those values live after
-// all.  127 VGPRs and no spill at 4 waves/SIMD, against 138 spilled VGPRs for
-// ristretto_decode there.  Same result as ristretto_decode.
-CPZ_HD fe ristretto_decode_v(const fe& s, fe& u1, fe& u2, fe& vu) {
-  const fe ss = fe_sq(s);
-  u1 = fe_sub(fe_one(), ss);
-  u2 = fe_add(fe_one(), ss);
-  const fe u2_sqr = fe_sq(u2);
-  const fe v = fe_sub(fe_neg(fe_mul(FE_D(), fe_sq(u1))), u2_sqr);
-  vu = fe_mul(v, u2_sqr);
-  return v;
-}
-
-CPZ_HD bool ristretto_decode_lowreg(ge_p3& out, const uint32_t w_in[8]) {
-  uint32_t w[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) w[i] = w_in[i];
-  const bool canonical = words_lt_p(w) && ((w[0] & 1) == 0);
-  fe r;
-  {
-    fe u1, u2, vu;
-    (void)ristretto_decode_v(fe_fromwords(w), u1, u2, vu);
-    const fe v3 = fe_mul(fe_sq(vu), vu);
-    r = fe_pow22523(fe_mul(fe_sq(v3), vu));  // (vu)^((p-5)/8 * 7) as fe_invsqrt_m1
-  }
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-  for (int i = 0; i < 8; i++) asm volatile("" : "+v"(w[i]));
-#endif
-  const fe s = fe_fromwords(w);
-  fe u1, u2, vu;
-  const fe v = ristretto_decode_v(s, u1, u2, vu);
-  // the rest of fe_invsqrt_m1(vu) (fe25519.h), then ristretto_decode's tail
-  r = fe_mul(fe_mul(fe_sq(vu), vu), r);
-  uint32_t cw[8];
-  fe_towords(cw, fe_mul(vu, fe_sq(r)));
-  const uint32_t kNegSqrtM1[8] = {0xb5f15f3du, 0x3b11e4d8u, 0x52d01b87u, 0xd0bce7f9u,
-                                  0xc2042858u, 0xd4b2ff66u, 0xb03e20f4u, 0x547cdb7fu};
-  uint32_t d_one = cw[0] ^ 1u, d_neg = cw[0] ^ 0xffffffecu, d_negi = cw[0] ^ kNegSqrtM1[0];
-#pragma unroll
-  for (int k = 1; k < 8; k++) {
-    d_one |= cw[k];
-    d_neg |= cw[k] ^ (k == 7 ? 0x7fffffffu : 0xffffffffu);
-    d_negi |= cw[k] ^ kNegSqrtM1[k];
-  }
-  r = fe_select(r, fe_mul(r, FE_SQRT_M1()), d_neg == 0 || d_negi == 0);
-  const fe invsqrt = fe_abs(r);
-  const bool was_square = d_one == 0 || d_neg == 0;
-  const fe den_x = fe_mul(invsqrt, u2);
-  const fe den_y = fe_mul(fe_mul(invsqrt, den_x), v);
-  const fe x = fe_abs(fe_mul(s, fe_add(den_x, den_x)));
-  const fe y = fe_mul(u1, den_y);
-  const fe t = fe_mul(x, y);
-  out.X = x;
-  out.Y = y;
-  out.Z = fe_one();
-  out.T = t;
-  return canonical && was_square && !fe_isnegative(t) && !fe_iszero(y);
-}
-
 // RFC 9496 4.3.2 ENCODE -> 8 little-endian words.
 CPZ_HD void ristretto_encode(uint32_t w[8], const ge_p3& p) {
   const fe u1 = fe_mul(fe_add(p.Z, p.Y), fe_sub(p.Z, p.Y));

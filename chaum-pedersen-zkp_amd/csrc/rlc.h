@@ -19,10 +19,6 @@ constexpr int kRlcSumBlock = 128;        // proofs per block sum (block_sums gra
 #ifndef CPZ_RLC_PREP_WIDE_MAX
 #define CPZ_RLC_PREP_WIDE_MAX (1 << 15)
 #endif
-// k_rlc_decode4 + k_rlc_scalars instead of k_rlc_prepare above kRlcPrepWideMax (rlc.hip)
-#ifndef CPZ_RLC_SPLIT_PREPARE
-#define CPZ_RLC_SPLIT_PREPARE 1
-#endif
 constexpr int64_t kRlcPrepWideMax = CPZ_RLC_PREP_WIDE_MAX;  // up to this many proofs: four lanes per proof
 constexpr int kRlcSortBlock = 1024;
 #ifndef CPZ_RLC_SORT_CHUNK

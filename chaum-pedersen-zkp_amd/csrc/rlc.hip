@@ -134,114 +134,6 @@ __global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_prepare(RlcPrepArgs a)
   }
 }
 
-// Split prepare (CPZ_RLC_SPLIT_PREPARE, the default for batches above kRlcPrepWideMax): the four
-// decodes per proof are ~90 % of k_rlc_prepare's work, dependent squaring chains whose carry
-// steps leave a SIMD idle when it holds only k_rlc_prepare's 2 waves (254 VGPRs).
-// k_rlc_decode4 runs the decodes alone, one point per lane (lane 4 i + q: point q of proof i),
-// at CPZ_RLC_DECODE_WAVES waves per SIMD -- tools/ubench/fe_f64.hip's floor-carry squaring
-// chain takes 353 SIMD cycles per squaring at 2 waves/SIMD and 283 at 4
-// (profiles/r06_fe_f64.jsonl) -- with the low-register decode (ristretto_decode_lowreg: 127
-// VGPRs, no spill), and settles each proof's decode-level status across its quad;
-// k_rlc_scalars (120 VGPRs, 4 waves/SIMD) then does the weights, digits and block-sum terms,
-// zero for a proof whose status is not 0.  (Two decodes side by side in k_rlc_prepare's lane
-// instead spilled 864 B per lane.)
-#ifndef CPZ_RLC_DECODE_WAVES
-#define CPZ_RLC_DECODE_WAVES 4
-#endif
-__global__ void __launch_bounds__(256, CPZ_RLC_DECODE_WAVES) k_rlc_decode4(RlcPrepArgs a) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;  // point 4 i + q
-  const int64_t i = t >> 2;
-  const int q = (int)(t & 3);
-  ClockStamp clk;
-  clk.start();
-  bool ok = true, ident = false;
-  if (i < a.n) {  // a quad's lanes share i: whole quads take this branch together
-    // q = 0: -r1, 1: -y1, 2: -r2, 3: -y2 (k_rlc_prepare's order)
-    const uint32_t* src = q == 0 ? a.r1 : (q == 1 ? a.y1 : (q == 2 ? a.r2 : a.y2));
-    uint32_t w[8];
-    rlc_load8(w, src, i);
-    ident = !(q & 1) && words8_zero(w);
-    ge_p3 P;
-    ok = ristretto_decode_lowreg(P, w);
-    store_niels(a.pts + t, niels_from_p3_affine(P, true));
-  }
-  // the quad's verdicts: every point decodes; r1 or r2 is the identity
-  int okq = ok ? 1 : 0, idq = ident ? 1 : 0;
-  okq &= __shfl_xor(okq, 1);
-  okq &= __shfl_xor(okq, 2);
-  idq |= __shfl_xor(idq, 1);
-  idq |= __shfl_xor(idq, 2);
-  if (i < a.n && q == 0) {
-    const uint8_t st_s = a.status[i];
-    uint8_t st;
-    if (!okq) st = kStBadPoint;
-    else if (st_s == kStBadScalar) st = kStBadScalar;
-    else if (idq && !a.eq_only) st = kStIdentity;
-    else if (st_s == kStZeroS) st = kStZeroS;
-    else st = kStOk;
-    a.status[i] = st;
-    if (st != kStOk) atomicOr(a.any_bad, 1);
-  }
-  clk.stop(a.clock_probe, t >> 6);
-}
-
-// Weights, digits and block-sum terms of every proof after k_rlc_decode4 (its status final):
-// k_rlc_prepare's scalar half.  A proof with a non-zero status gets zero digits and terms.
-__global__ void __launch_bounds__(kRlcPrepBlock, 2) k_rlc_scalars(RlcPrepArgs a) {
-  __shared__ sc red_a[kRlcPrepBlock];
-  __shared__ sc red_b[kRlcPrepBlock];
-  const int64_t i = (int64_t)blockIdx.x * kRlcPrepBlock + threadIdx.x;
-  sc zero;
-#pragma unroll
-  for (int k = 0; k < 8; k++) zero.w[k] = 0;
-  red_a[threadIdx.x] = zero;
-  red_b[threadIdx.x] = zero;
-  if (i < a.n) {
-    if (a.status[i] == kStOk) {
-      uint32_t blk[16];
-      chacha20_block(blk, a.seed, a.first_index + (uint64_t)i, 0);
-      const sc wa = rlc_weight(blk), wb = rlc_weight(blk + 4);
-      sc c, sv;
-      rlc_load8(c.w, a.c, i);
-      rlc_load8(sv.w, a.s, i);
-#pragma unroll 1
-      for (int q = 0; q < 4; q++) {
-        int16_t d[kRlcWindows];
-        if (q & 1) {
-          recode16(d, sc_mul(q == 1 ? wa : wb, c).w);
-        } else {
-          const uint32_t* u = q == 0 ? blk : blk + 4;
-#pragma unroll
-          for (int wv = 0; wv < kRlcWindows; wv++)
-            d[wv] = wv < 8 ? (int16_t)(u[wv >> 1] >> (16 * (wv & 1))) : (int16_t)0;
-        }
-#pragma unroll
-        for (int wv = 0; wv < kRlcWindows; wv++) a.digits[(int64_t)wv * a.dstride + 4 * i + q] = d[wv];
-      }
-      red_a[threadIdx.x] = sc_mul(wa, sv);
-      red_b[threadIdx.x] = sc_mul(wb, sv);
-    } else {  // zero weight: no digits, no block-sum terms
-      for (int q = 0; q < 4; q++)
-#pragma unroll
-        for (int wv = 0; wv < kRlcWindows; wv++) a.digits[(int64_t)wv * a.dstride + 4 * i + q] = 0;
-    }
-  }
-  static_assert(kRlcPrepBlock == 2 * kRlcSumBlock, "two block sums per prepare workgroup");
-  __syncthreads();
-  for (int off = kRlcSumBlock / 2; off > 0; off >>= 1) {
-    if ((threadIdx.x % kRlcSumBlock) < off) {
-      red_a[threadIdx.x] = sc_add(red_a[threadIdx.x], red_a[threadIdx.x + off]);
-      red_b[threadIdx.x] = sc_add(red_b[threadIdx.x], red_b[threadIdx.x + off]);
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x % kRlcSumBlock == 0) {
-    const int64_t sb = 2 * (int64_t)blockIdx.x + threadIdx.x / kRlcSumBlock;
-    a.block_sums[2 * sb] = red_a[threadIdx.x];
-    a.block_sums[2 * sb + 1] = red_b[threadIdx.x];
-  }
-}
-
 // Small batches (launch_rlc_prepare: n <= kRlcPrepWideMax): four lanes per proof -- lane q
 // writes point q's digits and decodes point q -- so a BatchVerifier-sized batch waits for one
 // decode per lane instead of four in sequence (on one lane per proof the prepare took 0.28 -
@@ -1048,13 +940,6 @@ hipError_t launch_rlc_prepare(const RlcPrepArgs& a, hipStream_t st) {
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_rlc_bsum4, dim3((unsigned)((4 * blocks + 63) / 64)), dim3(64), 0, st, a.quarter_sums, nq,
                        a.block_sums, 2 * blocks);
-    return hipGetLastError();
-  }
-  if (CPZ_RLC_SPLIT_PREPARE) {
-    hipLaunchKernelGGL(k_rlc_decode4, dim3((unsigned)((4 * a.n + 255) / 256)), dim3(256), 0, st, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_rlc_scalars, dim3((unsigned)blocks), dim3(kRlcPrepBlock), 0, st, a);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_rlc_prepare, dim3((unsigned)blocks), dim3(kRlcPrepBlock), 0, st, a);

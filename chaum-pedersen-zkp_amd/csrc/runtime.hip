@@ -221,7 +221,6 @@ struct cpz_ctx {
   DevBuf c;         // n x 32
   DevBuf st;        // n
   DevBuf scratch;   // per-stream table slabs (kCachedEntries ge_cached per thread)
-  DevBuf vpre;      // per-stream decoded points of one chunk (CPZ_VERIFY_SPLIT_DECODE)
   // host-API staging (y1, y2, r1, r2, s, and challenges / witnesses / nonces)
   DevBuf in[7];
   DevBuf ctxb, ctxo, ctxp;
@@ -532,12 +531,6 @@ int64_t wide_max() {
 #ifndef CPZ_VERIFY_CHUNK_DIV
 #define CPZ_VERIFY_CHUNK_DIV 2
 #endif
-// Per-proof chunks decode their points in a kernel of their own (k_verify_decode4, 4 waves per
-// SIMD) and verify from the decoded points (k_verify_prepared) instead of decoding inside
-// k_verify_each at its 2 waves.
-#ifndef CPZ_VERIFY_SPLIT_DECODE
-#define CPZ_VERIFY_SPLIT_DECODE 0
-#endif
 // Blocks per verify launch (half the occupancy grid) and the bytes of one verify stream's table
 // slab, which every stream owns at a fixed offset whatever a call's grid.
 int verify_full_grid(const cpz_ctx* ctx) {
@@ -647,14 +640,6 @@ int launch_verify_chunks(cpz_ctx* ctx, const cpz::VerifyArgs& va, int stage, hip
       if (ca->ctx_present) cc.ctx_present = ca->ctx_present + a;
       StageTimer tc(ctx, 0, sc);
       CPZ_HIP(cpz::launch_challenge(cc, sc));
-    }
-    if (CPZ_VERIFY_SPLIT_DECODE && !v.pre && !v.vtab && !v.blocks) {
-      // this stream's region of decoded points (4 per proof of a full-grid chunk)
-      const size_t pre_bytes = (size_t)full * cpz::kVerifyBlock * 4 * sizeof(cpz::ge_niels);
-      CPZ_HIP(ctx->vpre.ensure((size_t)CPZ_VERIFY_STREAMS * pre_bytes));
-      v.pre = reinterpret_cast<const cpz::ge_niels*>(static_cast<char*>(ctx->vpre.p) + (size_t)k * pre_bytes);
-      StageTimer td(ctx, 0, sc);  // timed with the chunk's challenges (stage 0)
-      CPZ_HIP(cpz::launch_verify_decode(v, sc));
     }
     StageTimer t(ctx, stage, sc);
     CPZ_HIP(cpz::launch_verify_each(v, grid, sc));
@@ -1046,9 +1031,7 @@ int rlc_prepare_points(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, c
   pa.any_bad = static_cast<int*>(ctx->rl_flags.p) + 3;
   CPZ_HIP(hipMemsetAsync(pa.any_bad, 0, sizeof(int), st));
 #if defined(CPZ_CLOCK_PROBE)
-  // one record per wave of k_rlc_prepare, or of k_rlc_decode4 (a lane per point: 4x the waves)
-  ctx->clk_waves[0] = (size_t)((n + cpz::kRlcPrepBlock - 1) / cpz::kRlcPrepBlock) * (cpz::kRlcPrepBlock / 64) *
-                      (CPZ_RLC_SPLIT_PREPARE && n > cpz::kRlcPrepWideMax ? 4 : 1);
+  ctx->clk_waves[0] = (size_t)((n + cpz::kRlcPrepBlock - 1) / cpz::kRlcPrepBlock) * (cpz::kRlcPrepBlock / 64);
   CPZ_HIP(ctx->clk[0].ensure(ctx->clk_waves[0] * 40));
   CPZ_HIP(hipMemsetAsync(ctx->clk[0].p, 0, ctx->clk_waves[0] * 40, st));
   pa.clock_probe = static_cast<uint64_t*>(ctx->clk[0].p);
@@ -2047,7 +2030,6 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
   ctx->c.release();
   ctx->st.release();
   ctx->scratch.release();
-  ctx->vpre.release();
   for (auto& b : ctx->in) b.release();
   ctx->in_all.release();
   ctx->pin.release();

@@ -119,31 +119,6 @@ int cpzt_decode_encode(uint8_t* out, const uint8_t* in) {
   return 1;
 }
 
-// The same through ristretto_decode_lowreg (k_rlc_decode4's decode); also writes the decoded
-// point's four coordinates (canonical words) so that the two decodes can be compared exactly.
-int cpzt_decode_encode_lowreg(uint8_t* out, uint8_t* coords, const uint8_t* in) {
-  uint32_t w[8], o[8];
-  words_from(w, in);
-  ge_p3 P;
-  const bool ok = ristretto_decode_lowreg(P, w);
-  const fe* c[4] = {&P.X, &P.Y, &P.Z, &P.T};
-  for (int k = 0; k < 4; k++) fe_out(coords + 32 * k, *c[k]);
-  if (!ok) return 0;
-  ristretto_encode(o, P);
-  bytes_from(out, o);
-  return 1;
-}
-
-int cpzt_decode_coords(uint8_t* coords, const uint8_t* in) {
-  uint32_t w[8];
-  words_from(w, in);
-  ge_p3 P;
-  const bool ok = ristretto_decode(P, w);
-  const fe* c[4] = {&P.X, &P.Y, &P.Z, &P.T};
-  for (int k = 0; k < 4; k++) fe_out(coords + 32 * k, *c[k]);
-  return ok ? 1 : 0;
-}
-
 // out = enc(a + b), enc(2a), enc(-a) for decodable a, b.
 int cpzt_point_ops(uint8_t* sum, uint8_t* dbl, uint8_t* neg, const uint8_t* a, const uint8_t* b) {
   uint32_t w[8], o[8];

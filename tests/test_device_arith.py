@@ -102,23 +102,6 @@ def test_ristretto_decode_encode(lib, golden):
             assert out.raw == b
 
 
-def test_ristretto_decode_lowreg_equals_decode(lib, golden):
-    """k_rlc_decode4's low-register decode (recomputes s, u1, u2, v after the exponent chain)
-    gives ristretto_decode's verdict and coordinates on valid, invalid and random encodings."""
-    rnd = random.Random(11)
-    out, c1, c2 = buf(), ctypes.create_string_buffer(128), ctypes.create_string_buffer(128)
-    encs = [bytes.fromhex(e) for e in golden["rfc9496_multiples"] + golden["rfc9496_bad"]]
-    encs += [bytes(rnd.getrandbits(8) for _ in range(32)) for _ in range(300)]
-    encs += [b"\xff" * 32, bytes(32), (2**255 - 20).to_bytes(32, "little")]
-    for b in encs:
-        ok_low = lib.cpzt_decode_encode_lowreg(out, c1, b)
-        ok = lib.cpzt_decode_coords(c2, b)
-        assert ok_low == ok and c1.raw == c2.raw, b.hex()
-        assert (ok == 1) == (O.ristretto_decode(b) is not None)
-        if ok:
-            assert out.raw == b
-
-
 def test_point_ops(lib):
     rnd = random.Random(4)
     s_, d_, n_ = buf(), buf(), buf()
