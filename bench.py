@@ -577,6 +577,7 @@ def c4_run(gpu, torch, dist, dev, stream, world, rank, n_total, steps, warmup, b
     torch.cuda.synchronize(dev)
     barrier()
     f_el = time.perf_counter() - f0
+    fb = gpu.fallback_stats()
     got = st.cpu().numpy()
     bad = np.nonzero(got)[0]
     exact_local = bool(np.array_equal(bad, np.asarray(mine, dtype=bad.dtype)) and (got[bad] == 1).all())
@@ -605,6 +606,7 @@ def c4_run(gpu, torch, dist, dev, stream, world, rank, n_total, steps, warmup, b
                       "statuses_exact_every_rank": all(r[1] for r in per_rank),
                       "combined_total_not_identity": all(r[2] for r in per_rank),
                       "combined_total": state["total"].hex(), "ms": f_el * 1e3,
+                      "rank0_fallback": fb,
                       "how": "s + 1 at the forged global indices; cpz_verify_batch_device with fallback on every "
                              "rank, all-gather, combine"},
            "local_ms_per_step_rank0": local_el * 1e3 / steps}

@@ -89,6 +89,8 @@ struct RlcMsmArgs {
   // the sum -- into partial_out / identity_out.  total == nullptr: a single MSM.
   ge_p3* total = nullptr;
   int total_first = 1, total_last = 1;
+  int* span_identity = nullptr;  // multi-span batches: 1 if this span's own P is the identity
+                                 // (the batch-fail fallback then skips the span)
   uint64_t* clock_probe = nullptr;  // CPZ_CLOCK_PROBE builds only: k_rlc_bucket, 5 words per wave
 };
 

@@ -873,6 +873,7 @@ __global__ void __launch_bounds__(64) k_rlc_final(RlcMsmArgs a) {
   }
   if (threadIdx.x >= 4) return;
   ge_p3 P = lds[0];
+  if (a.span_identity && q == 0) a.span_identity[0] = ristretto_is_identity(P) ? 1 : 0;
   if (a.total) {  // one span of a multi-span batch
     if (!a.total_first) P = ge_add_quad(load_p3(a.total), P, q);
     if (!a.total_last) {

@@ -229,3 +229,14 @@ def test_bench_rlc_four_rank_rehearsal(launcher):
     assert f["statuses_exact_every_rank"] is True and f["combined_total_not_identity"] is True
     assert f["combined_total"] != "00" * 32
     assert c4["proofs_per_s"] is None   # ranks sharing one GPU: no rate
+    # the scaling invariant: the four shard partials of the forged variant sum to the partial
+    # one process computes over the whole 2^21 proofs (weights keyed by the global index)
+    if launcher == "none":
+        one = [sys.executable, os.path.join(ROOT, "bench.py"), "--mode", "rlc", "--n-total", str(1 << 20),
+               "--steps", "1", "--warmup", "1", "--extras", "0", "--no-cpu-baseline", "--c4-n", str(1 << 21),
+               "--c4-steps", "1"]
+        r1 = subprocess.run(one, capture_output=True, text=True, timeout=360, env=env, cwd=ROOT)
+        assert r1.returncode == 0, r1.stderr[-3000:]
+        d1 = json.loads([l for l in r1.stdout.splitlines() if l.startswith("{")][0])
+        assert d1["n_gpus"] == 1 and d1["c4"]["ok"] is True and d1["c4"]["forged"]["per_rank_forged"] == [4]
+        assert d1["c4"]["forged"]["combined_total"] == f["combined_total"]

@@ -271,7 +271,8 @@ def test_spans_forged_only_in_a_later_span(gpu):
     oracle's partial of those entries (an identity partial here would accept a forged batch),
     the batch must fail, and the fallback must return exactly the forged set.  Also checked
     for the same span as a batch of its own (first_index = its global start) and for spans
-    0..1 alone (valid: identity, batch ok)."""
+    0..1 alone (valid: identity, batch ok).  The fallback is span-local: each span's final
+    records whether its own P is the identity, and only the failing span is searched."""
     torch = pytest.importorskip("torch")
     n, span = 1 << 23, 1 << 21
     t = _synthetic_device(gpu, torch, n)
@@ -287,6 +288,11 @@ def test_spans_forged_only_in_a_later_span(gpu):
     assert not ok and p == want
     got = st.cpu().numpy()
     assert np.array_equal(np.nonzero(got)[0], idx) and set(got[idx].tolist()) == {1}
+    # span-local fallback: only span 2's own P failed, so only span 2 is searched (no
+    # partitioned pass over the whole batch's blocks)
+    fb = gpu.fallback_stats()
+    assert fb["path"] == "bisection" and fb["blocks_checked"] == 0, fb
+    assert fb["per_proof"] <= span, fb
     lo, hi = 2 * span, 3 * span
     p, ok = gpu.verify_batch_device(*(t[k][lo:hi] for k in KEYS), st[lo:hi], WSEED, first_index=lo)
     assert not ok and p == want
