@@ -908,13 +908,18 @@ int rlc_range_launch(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st) {
   static_assert(4ll * CPZ_RLC_SPAN + 2 <= cpz::kRlcMaxMsmPoints, "a span's MSM exceeds the sort-entry format");
   const int64_t nspan = (hi - lo + CPZ_RLC_SPAN - 1) / CPZ_RLC_SPAN;
 #if defined(CPZ_CLOCK_PROBE)
-  const bool overlap = false;  // timing-only builds: one clock-probe buffer, spans in order
+  bool overlap = false;  // timing-only builds: one clock-probe buffer, spans in order
 #else
-  const bool overlap = nspan > 1 && span_overlap();
+  bool overlap = nspan > 1 && span_overlap();
 #endif
+  // the second MSM set (~1 GB for 2^21-proof spans): without room for it the spans run in order
+  if (overlap && rlc_reserve_msm(ctx->rl_msm2, std::min<int64_t>(hi - lo, CPZ_RLC_SPAN)) != CPZ_OK) {
+    ctx->rl_msm2.release();
+    (void)hipGetLastError();
+    overlap = false;
+  }
   hipStream_t sts[2] = {st, st};
   if (overlap) {
-    if (int rc = rlc_reserve_msm(ctx->rl_msm2, std::min<int64_t>(hi - lo, CPZ_RLC_SPAN))) return rc;
     if (!ctx->span_stream) CPZ_HIP(stream_own_queue(&ctx->span_stream, ctx->cus, ctx->device, &ctx->own_queues));
     for (auto& e : ctx->span_ev)
       if (!e) CPZ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
