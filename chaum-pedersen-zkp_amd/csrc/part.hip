@@ -413,6 +413,46 @@ __global__ void __launch_bounds__(64) k_part_combine(PartArgs a) {
   }
 }
 
+// The same with one lane per block (CPZ_PART_COMBINE_LANE, launches of at least
+// kPartLaneMinBlocks blocks: C5's first pass, 131,072 blocks = 2,048 waves): the same point
+// operations done once each instead of spread over a quad, whose product rounds pay DPP
+// exchanges and per-lane operand selects.  T_v is formed in the order that keeps the fewest
+// points live (P, the running sums and one loaded point), each A_h subtracted as it is loaded.
+__device__ __forceinline__ ge_p3 part_dbl_n(const ge_p3& p, int n) {  // n >= 1 doublings
+  ge_p1p1 t = p3_dbl(p);
+#pragma unroll 1
+  for (int k = 1; k < n; k++) t = p2_dbl(p1p1_to_p2(t));
+  return p1p1_to_p3(t);
+}
+
+__global__ void __launch_bounds__(256, 2) k_part_combine_lane(PartArgs a) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= a.nblk) return;
+  const ge_p3* ws = a.wsum + (a.blk0 + b) * kPartWsum;
+  ge_p3 P = ge_identity();
+#pragma unroll 1
+  for (int v = kPartWindows - 1; v >= 0; v--) {
+    // T_v = W (Stot + Sw) + Stot - sum_h A_h (k_part_combine), Sw = U + V + X
+    const ge_p3* w = ws + v * kPartQuarters * 2;
+    ge_p3 R = load_p3(w + 7);             // U = S_3
+    ge_p3 Sw = R;
+    R = ge_add(load_p3(w + 5), R);        // V = S_2 + U
+    Sw = ge_add(Sw, R);
+    R = ge_add(load_p3(w + 3), R);        // X = S_1 + V
+    Sw = ge_add(Sw, R);
+    R = ge_add(R, load_p3(w + 1));        // Stot = X + S_0
+    ge_p3 T = ge_add(part_dbl_n(ge_add(R, Sw), __builtin_ctz(part_width(v))), R);
+#pragma unroll 1
+    for (int hh = 0; hh < kPartQuarters; hh++) {  // the A_h are stored in cached form
+      const ge_p3 c = load_p3(w + 2 * hh);
+      T = p1p1_to_p3(ge_add_cached(T, ge_cached_cneg(*reinterpret_cast<const ge_cached*>(&c), true)));
+    }
+    P = v == kPartWindows - 1 ? T : ge_add(part_dbl_n(P, 8), T);
+  }
+  store_p3(a.part + a.blk0 + b, P);
+  a.fail[a.blk0 + b] = a.fail[a.blk0 + b] | (ristretto_is_identity(P) ? 0 : 1);  // k_part_sort's bit 1
+}
+
 // The same per block for very few blocks (the locate pass of a sparse failure: each wave of
 // k_part_combine runs ~800 dependent quad operations, 1.7 ms, whatever the block count): one
 // workgroup of 32 quads per block, quad v forming T_v, then P_b = sum_v 2^(8 v) T_v by a tree
@@ -675,6 +715,8 @@ hipError_t launch_part_combine(const PartArgs& a, hipStream_t st) {
   if (a.nblk <= 0) return hipSuccess;
   if (CPZ_PART_COMBINE_TREE && a.nblk <= kPartTreeMaxBlocks)
     hipLaunchKernelGGL(k_part_combine_tree, dim3((unsigned)a.nblk), dim3(4 * kPartWindows), 0, st, a);
+  else if (CPZ_PART_COMBINE_LANE && a.nblk >= kPartLaneMinBlocks)
+    hipLaunchKernelGGL(k_part_combine_lane, dim3((unsigned)((a.nblk + 255) / 256)), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL(k_part_combine, dim3((unsigned)((a.nblk + 15) / 16)), dim3(64), 0, st, a);
   return hipGetLastError();

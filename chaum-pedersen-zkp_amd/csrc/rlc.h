@@ -118,6 +118,11 @@ constexpr int kPartOffs = kPartWindows * (kPartBuckets + 1);
 constexpr int kPartWsum = kPartWindows * kPartQuarters * 2;  // (W, S) per window and quarter
 constexpr int kPartUnits = kPartWindows * kPartQuarters / 2;  // walk units per half (64 = lanes)
 // Combines of at most this many blocks run one workgroup per block (k_part_combine_tree).
+// k_part_combine_lane (one lane per block) for launches of at least kPartLaneMinBlocks blocks
+#ifndef CPZ_PART_COMBINE_LANE
+#define CPZ_PART_COMBINE_LANE 1
+#endif
+constexpr int64_t kPartLaneMinBlocks = 1 << 16;
 #ifndef CPZ_PART_COMBINE_TREE
 #define CPZ_PART_COMBINE_TREE 1
 #endif
