@@ -122,7 +122,10 @@ constexpr int kPartUnits = kPartWindows * kPartQuarters / 2;  // walk units per 
 #ifndef CPZ_PART_COMBINE_LANE
 #define CPZ_PART_COMBINE_LANE 1
 #endif
-constexpr int64_t kPartLaneMinBlocks = 1 << 16;
+#ifndef CPZ_PART_LANE_MIN
+#define CPZ_PART_LANE_MIN (1 << 16)
+#endif
+constexpr int64_t kPartLaneMinBlocks = CPZ_PART_LANE_MIN;
 #ifndef CPZ_PART_COMBINE_TREE
 #define CPZ_PART_COMBINE_TREE 1
 #endif
