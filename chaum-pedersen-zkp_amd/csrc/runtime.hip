@@ -253,9 +253,7 @@ struct cpz_ctx {
   RlcMsmSet rl_msm2;
   DevBuf rl_span_ident;  // per span of the last multi-span MSM: its own P is the identity
   hipStream_t span_stream = nullptr;
-  hipStream_t span_stream2 = nullptr;  // set 0's stream when the prepare is pipelined with the spans
-  // [0] start / end, [1 + set] the spans' finals, [3] a pipelined prepare chunk done
-  hipEvent_t span_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t span_ev[3] = {nullptr, nullptr, nullptr};
   DevBuf rl_flags, rl_parts;
   // partitioned batch check (part.hip): sorted lists / offsets / window sums of one chunk of
   // blocks, every block's partial and fail flag, the sum's scratch, the failing-block list
@@ -904,17 +902,7 @@ bool span_overlap() {
   return v;
 }
 
-int rlc_prepare_launch(cpz_ctx* ctx, const cpz::RlcPrepArgs& pa, int64_t lo, int64_t hi, hipStream_t st);
-
-bool prepare_pipeline() {
-  static const bool v = [] {
-    const char* e = std::getenv("CPZ_RLC_PIPELINE");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
-int rlc_range_launch(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, const cpz::RlcPrepArgs* prep) {
+int rlc_range_launch(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st) {
   static_assert(CPZ_RLC_SPAN % cpz::kRlcPrepBlock == 0, "spans are whole weight blocks");
   static_assert(cpz::kRlcPrepBlock % cpz::kRlcSumBlock == 0, "ranges are whole block sums");
   static_assert(4ll * CPZ_RLC_SPAN + 2 <= cpz::kRlcMaxMsmPoints, "a span's MSM exceeds the sort-entry format");
@@ -930,38 +918,20 @@ int rlc_range_launch(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, const
     (void)hipGetLastError();
     overlap = false;
   }
-  // prep (the batch's prepare, not yet launched): pipelined with overlapped spans -- span j's
-  // prepare chunk on `st`, its MSM on its set's stream once the chunk is done -- so the MSMs'
-  // latency-bound sorts and tails run beside the next chunk's VALU-bound prepare; otherwise
-  // the whole prepare first
-  const bool piped = prep && overlap && prepare_pipeline();
-  if (prep && !piped)
-    if (int rc = rlc_prepare_launch(ctx, *prep, lo, hi, st)) return rc;
   hipStream_t sts[2] = {st, st};
   if (overlap) {
     if (!ctx->span_stream) CPZ_HIP(stream_own_queue(&ctx->span_stream, ctx->cus, ctx->device, &ctx->own_queues));
-    if (piped && !ctx->span_stream2)
-      CPZ_HIP(stream_own_queue(&ctx->span_stream2, ctx->cus, ctx->device, &ctx->own_queues));
     for (auto& e : ctx->span_ev)
       if (!e) CPZ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    CPZ_HIP(hipEventRecord(ctx->span_ev[0], st));  // the span streams start after st's prior work
+    CPZ_HIP(hipEventRecord(ctx->span_ev[0], st));  // the second stream starts after st's prior work
     CPZ_HIP(hipStreamWaitEvent(ctx->span_stream, ctx->span_ev[0], 0));
     sts[1] = ctx->span_stream;
-    if (piped) {
-      CPZ_HIP(hipStreamWaitEvent(ctx->span_stream2, ctx->span_ev[0], 0));
-      sts[0] = ctx->span_stream2;
-    }
   }
   for (int64_t j = 0; j < nspan; j++) {
     const int64_t slo = lo + j * CPZ_RLC_SPAN, shi = std::min<int64_t>(hi, slo + CPZ_RLC_SPAN);
     const int set = overlap ? (int)((nspan - 1 - j) & 1) : 0;  // the last span on set 0 / st
     RlcMsmSet& S = set ? ctx->rl_msm2 : ctx->rl_msm;
     hipStream_t ss = sts[set];
-    if (piped) {  // this span's prepare chunk, then its MSM waits for it
-      if (int rc = rlc_prepare_launch(ctx, *prep, slo, shi, st)) return rc;
-      CPZ_HIP(hipEventRecord(ctx->span_ev[3], st));
-      CPZ_HIP(hipStreamWaitEvent(ss, ctx->span_ev[3], 0));
-    }
     cpz::RlcMsmArgs m;
     if (int rc = rlc_msm_args(ctx->rl_prep, S, slo, shi, m)) return rc;
     m.e0 = 4 * ctx->rl_prep.cap + 2 * set;
@@ -1001,16 +971,12 @@ int rlc_range_launch(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, const
     if (timed)
       for (int k = 0; k + 1 < cpz::kRlcMsmMarks; k++) ctx->marks.push_back({8 + k, marks[k], marks[k + 1]});
   }
-  if (piped) {  // the last span (set 0) ran on span_stream2 after every other final: st joins it
-    CPZ_HIP(hipEventRecord(ctx->span_ev[0], sts[0]));
-    CPZ_HIP(hipStreamWaitEvent(st, ctx->span_ev[0], 0));
-  }
   return CPZ_OK;
 }
 
 // rlc_range_launch, then the partial and identity flag read back (synchronises).
 int rlc_range(cpz_ctx* ctx, int64_t lo, int64_t hi, hipStream_t st, uint8_t partial[32], int* identity) {
-  if (int rc = rlc_range_launch(ctx, lo, hi, st, nullptr)) return rc;
+  if (int rc = rlc_range_launch(ctx, lo, hi, st)) return rc;
   RlcMsmSet& S = ctx->rl_msm;
   int flags[1];
   CPZ_HIP(hipMemcpyAsync(partial, S.partial.p, 32, hipMemcpyDeviceToHost, st));
@@ -1047,15 +1013,13 @@ int batch_challenges(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, con
 
 // Decode + weights + points/digits of the whole batch (after batch_challenges).
 // need_msm = false (the partitioned check): the span-sized MSM set is not reserved.
-// The prepare's arguments for the whole batch (buffers reserved, any-bad word cleared on st);
-// rlc_prepare_launch runs it over proofs [lo, hi) (lo a multiple of kRlcPrepBlock: its block
-// sums land at their global positions).
-int rlc_prepare_args(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
-                     const void* s, uint8_t* status, const uint8_t seed[32], uint64_t first_index, hipStream_t st,
-                     cpz::RlcPrepArgs& pa, bool need_msm = true) {
+int rlc_prepare_points(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
+                       const void* s, uint8_t* status, const uint8_t seed[32], uint64_t first_index, hipStream_t st,
+                       bool need_msm = true) {
   int rc = need_msm ? rlc_reserve(ctx, (int64_t)n) : rlc_reserve_prepared(ctx->rl_prep, (int64_t)n);
   if (rc) return rc;
   CPZ_HIP(ctx->rl_flags.ensure(4 * sizeof(int)));
+  cpz::RlcPrepArgs pa;
   pa.n = (int64_t)n;
   pa.first_index = first_index;
   std::memcpy(pa.seed, seed, 32);
@@ -1080,35 +1044,11 @@ int rlc_prepare_args(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, con
   CPZ_HIP(hipMemsetAsync(ctx->clk[0].p, 0, ctx->clk_waves[0] * 40, st));
   pa.clock_probe = static_cast<uint64_t*>(ctx->clk[0].p);
 #endif
+  {
+    StageTimer t(ctx, 2, st);
+    CPZ_HIP(cpz::launch_rlc_prepare(pa, st));
+  }
   return CPZ_OK;
-}
-
-int rlc_prepare_launch(cpz_ctx* ctx, const cpz::RlcPrepArgs& pa, int64_t lo, int64_t hi, hipStream_t st) {
-  if (lo % cpz::kRlcPrepBlock != 0 || lo < 0 || hi > pa.n || hi <= lo) return fail(CPZ_EINVAL, "internal: prepare range");
-  cpz::RlcPrepArgs q = pa;
-  q.n = hi - lo;
-  q.first_index = pa.first_index + (uint64_t)lo;
-  q.y1 = pa.y1 + 8 * lo;
-  q.y2 = pa.y2 + 8 * lo;
-  q.r1 = pa.r1 + 8 * lo;
-  q.r2 = pa.r2 + 8 * lo;
-  q.s = pa.s + 8 * lo;
-  q.c = pa.c + 8 * lo;
-  q.status = pa.status + lo;
-  q.pts = pa.pts + 4 * lo;
-  q.digits = pa.digits + 4 * lo;
-  q.block_sums = pa.block_sums + 2 * (lo / cpz::kRlcSumBlock);  // (a s, b s) per 128-proof sum block
-  StageTimer t(ctx, 2, st);
-  CPZ_HIP(cpz::launch_rlc_prepare(q, st));
-  return CPZ_OK;
-}
-
-int rlc_prepare_points(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, const void* r1, const void* r2,
-                       const void* s, uint8_t* status, const uint8_t seed[32], uint64_t first_index, hipStream_t st,
-                       bool need_msm = true) {
-  cpz::RlcPrepArgs pa;
-  if (int rc = rlc_prepare_args(ctx, n, y1, y2, r1, r2, s, status, seed, first_index, st, pa, need_msm)) return rc;
-  return rlc_prepare_launch(ctx, pa, 0, (int64_t)n, st);
 }
 
 // Prepare (challenge + decode + weights + points/digits) for the whole batch.
@@ -1619,13 +1559,11 @@ int verify_batch_impl(cpz_ctx* ctx, size_t n, const void* y1, const void* y2, co
       return CPZ_OK;
     }
   }
-  // The prepare is handed to the MSM launch, which pipelines it with the spans of a large batch.
+  if ((rc = rlc_prepare_points(ctx, n, y1, y2, r1, r2, s, d_status, seed, first_index, st))) return rc;
   // The partial, its identity flag, the any-bad word and (host-buffer calls) the statuses come
   // back with one synchronisation, into page-locked memory when it is there: a valid batch
   // needs no second round trip.  A failing one re-reads the statuses after its fallback.
-  cpz::RlcPrepArgs pa;
-  if ((rc = rlc_prepare_args(ctx, n, y1, y2, r1, r2, s, d_status, seed, first_index, st, pa))) return rc;
-  if ((rc = rlc_range_launch(ctx, 0, (int64_t)n, st, &pa))) return rc;
+  if ((rc = rlc_range_launch(ctx, 0, (int64_t)n, st))) return rc;
   const bool stage_st = host_status && n <= kPinStageMax;  // (the staged inputs there are spent)
   const bool pinned = ctx->pin.ensure(kPinMail + (stage_st ? pad16(n) : 0)) == hipSuccess;
   (void)hipGetLastError();
@@ -2153,11 +2091,10 @@ void cpz_ctx_destroy(cpz_ctx* ctx) {
     (void)hipStreamDestroy(ctx->copy_stream);
   }
   for (DevBuf* b : {&ctx->pz_blob, &ctx->pz_off, &ctx->pz_rows, &ctx->pz_code, &ctx->pz_aux}) b->release();
-  for (hipStream_t* sp : {&ctx->span_stream, &ctx->span_stream2})
-    if (*sp) {
-      (void)hipStreamSynchronize(*sp);
-      (void)hipStreamDestroy(*sp);
-    }
+  if (ctx->span_stream) {
+    (void)hipStreamSynchronize(ctx->span_stream);
+    (void)hipStreamDestroy(ctx->span_stream);
+  }
   for (auto& e : ctx->span_ev)
     if (e) (void)hipEventDestroy(e);
   ctx->rl_prep.release();
