@@ -28,12 +28,15 @@
 //                   k_rlc_bucket_fix (load-balanced whatever the bucket sizes).
 //   k_rlc_segment   1 thread / (window, 32-bucket segment): running sums.
 //   k_rlc_window    1 block / window: sum_b b * B_b from the segments (LDS tree).
-//   k_rlc_final     2^(16w) combine, encode -> 32-byte partial + identity flag.
+//   k_rlc_final16   2^(16w) combine (Horner on 16-lane rows, fe16.h), encode -> 32-byte
+//                   partial + identity flag (k_rlc_final: the quad tree form).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 
+#include "fe16.h"
 #include "rlc.h"
 #include "rlc_dev.h"
 #include "verify.h"
@@ -844,14 +847,9 @@ __global__ void __launch_bounds__(256) k_rlc_window_sparse(RlcMsmArgs a) {
   if (t == 0) store_p3(a.seg_s + (int64_t)w * kRlcSparseMaxGroups + g, red[0]);
 }
 
-// P = sum_w 2^(16 w) T_w by a tree on one wave: quad j owns window j; at level `span` the
-// active quads double their upper partner 16 span times and add it to their own (240
-// doublings deep), then the partial is encoded with its identity flag -- or, for one span of
-// a multi-span batch, added into the batch's running total (RlcMsmArgs::total).
-__global__ void __launch_bounds__(64) k_rlc_final(RlcMsmArgs a) {
-  __shared__ ge_p3 lds[kRlcWindows];
-  __builtin_amdgcn_s_setprio(3);
-  const int j = threadIdx.x >> 2, q = threadIdx.x & 3;
+// Window sums T_j of the MSM into lds[j] (quad j's lane 0): from k_rlc_window_sparse's
+// partials or k_rlc_window's sums.
+__device__ __forceinline__ void rlc_final_windows(const RlcMsmArgs& a, ge_p3* lds, int j, int q) {
   if (a.sparse) {  // window j's sum from its k_rlc_window_sparse partials
     const ge_p3* part = a.seg_s + (int64_t)j * kRlcSparseMaxGroups;
     ge_p3 T = load_p3(part);
@@ -863,16 +861,11 @@ __global__ void __launch_bounds__(64) k_rlc_final(RlcMsmArgs a) {
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  for (int span = 1; span < kRlcWindows; span <<= 1) {  // one wave: LDS traffic stays in program order
-    if ((j % (2 * span)) == 0) {
-      const ge_p3 lo = ge_add_quad(lds[j], p3_dbl_n_quad(lds[j + span], 16 * span, q), q);
-      if (q == 0) lds[j] = lo;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-  if (threadIdx.x >= 4) return;
-  ge_p3 P = lds[0];
+}
+
+// Lanes 0..3 (one quad, each holding P): the span's identity flag, the multi-span running
+// total, and the 32-byte partial with its identity flag.
+__device__ __forceinline__ void rlc_final_tail(const RlcMsmArgs& a, ge_p3 P, int q) {
   if (a.span_identity && q == 0) a.span_identity[0] = ristretto_is_identity(P) ? 1 : 0;
   if (a.total) {  // one span of a multi-span batch
     if (!a.total_first) P = ge_add_quad(load_p3(a.total), P, q);
@@ -890,6 +883,88 @@ __global__ void __launch_bounds__(64) k_rlc_final(RlcMsmArgs a) {
     for (int k = 0; k < 8; k++) a.partial_out[k] = enc[k];
     a.identity_out[0] = id ? 1 : 0;
   }
+}
+
+// P = sum_w 2^(16 w) T_w by a tree on one wave: quad j owns window j; at level `span` the
+// active quads double their upper partner 16 span times and add it to their own (240
+// doublings deep), then the partial is encoded with its identity flag -- or, for one span of
+// a multi-span batch, added into the batch's running total (RlcMsmArgs::total).
+// CPZ_RLC_FINAL16=0 selects it; k_rlc_final16 below is the default.
+__global__ void __launch_bounds__(64) k_rlc_final(RlcMsmArgs a) {
+  __shared__ ge_p3 lds[kRlcWindows];
+  __builtin_amdgcn_s_setprio(3);
+  const int j = threadIdx.x >> 2, q = threadIdx.x & 3;
+  rlc_final_windows(a, lds, j, q);
+  for (int span = 1; span < kRlcWindows; span <<= 1) {  // one wave: LDS traffic stays in program order
+    if ((j % (2 * span)) == 0) {
+      const ge_p3 lo = ge_add_quad(lds[j], p3_dbl_n_quad(lds[j + span], 16 * span, q), q);
+      if (q == 0) lds[j] = lo;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (threadIdx.x >= 4) return;
+  rlc_final_tail(a, lds[0], q);
+}
+
+// The same combine as a Horner chain on the latency layout of fe16.h: the whole wave holds
+// one point (a field element per 16-lane row, one 16-bit limb per lane), so each of the 240
+// doublings is two row-parallel product stages instead of a quad's two one-lane products.
+// The window sums arrive as canonical words (one fe_towords per lane: 16 windows x X, Y, Z,
+// T), P = (..(T_15 2^16 + T_14) 2^16 + ..) + T_0, and the result goes back to radix 2^25.5
+// for the shared tail.  The k_rlc_final tree is as deep (16 + 32 + 64 + 128 doublings).
+__global__ void __launch_bounds__(64) k_rlc_final16(RlcMsmArgs a) {
+  __shared__ ge_p3 lds[kRlcWindows];
+  __shared__ uint32_t wd[kRlcWindows * 4 * 8];
+  __builtin_amdgcn_s_setprio(3);
+  const int lane = threadIdx.x, j = lane >> 2, q = lane & 3;
+  rlc_final_windows(a, lds, j, q);
+  fe_towords(wd + (j * 4 + q) * 8, reinterpret_cast<const fe*>(&lds[j])[q]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const r16::Lane L = r16::lane_of(lane);
+  auto window = [&](int w) {
+    r16::P4 p;
+    p.X = r16::limb_of(wd + (w * 4 + 0) * 8, L);
+    p.Y = r16::limb_of(wd + (w * 4 + 1) * 8, L);
+    p.Z = r16::limb_of(wd + (w * 4 + 2) * 8, L);
+    p.T = r16::limb_of(wd + (w * 4 + 3) * 8, L);
+    return p;
+  };
+  r16::P4 P = window(kRlcWindows - 1);
+#pragma unroll 1
+  for (int w = kRlcWindows - 2; w >= 0; w--) {
+#pragma unroll 1
+    for (int i = 0; i < 16; i++) P = r16::dbl(P, L);
+    const r16::C4 c = r16::to_cached(window(w), L);
+    P = r16::add_b(P, r16::cached_b(c, false, L), L);
+  }
+  uint32_t out[8];
+  r16::to_words(out, r16::sel4(P.X, P.Y, P.Z, P.T, L));  // row r: coordinate r
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (L.k == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) wd[L.row * 8 + k] = out[k];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (lane >= 4) return;
+  // canonical words -> limbs in [0, 2^26), then one carry pass to the tight bounds the
+  // tail's sums (Y - X, Y + X) assume
+  auto tight = [](const uint32_t* w) {
+    const fe f = fe_fromwords(w);
+    int64_t h[10];
+#pragma unroll
+    for (int k = 0; k < 10; k++) h[k] = f.v[k];
+    return fe_carry_wide(h);
+  };
+  ge_p3 R;
+  R.X = tight(wd + 0);
+  R.Y = tight(wd + 8);
+  R.Z = tight(wd + 16);
+  R.T = tight(wd + 24);
+  rlc_final_tail(a, R, q);
 }
 
 // Generic MSM input: decode point j, store its Niels form and the digits of scalar j.
@@ -1017,7 +1092,14 @@ hipError_t launch_rlc_msm(const RlcMsmArgs& a, const sc* block_sums, int64_t b0,
   }
   if ((e = mark(4)) != hipSuccess) return e;
   if (final_wait && (e = hipStreamWaitEvent(st, final_wait, 0)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rlc_final, dim3(1), dim3(64), 0, st, a2);
+  static const bool final16 = [] {
+    const char* v = getenv("CPZ_RLC_FINAL16");
+    return !(v && v[0] == '0');
+  }();
+  if (final16)
+    hipLaunchKernelGGL(k_rlc_final16, dim3(1), dim3(64), 0, st, a2);
+  else
+    hipLaunchKernelGGL(k_rlc_final, dim3(1), dim3(64), 0, st, a2);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (final_done && (e = hipEventRecord(final_done, st)) != hipSuccess) return e;
   return mark(5);
