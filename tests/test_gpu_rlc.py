@@ -81,6 +81,26 @@ def test_small_msm_sparse_reduction_partials(gpu, n):
     assert live == idx.size and not ok and p == want
 
 
+@pytest.mark.parametrize("k", [1, 2, 7, 64, 65, 130])
+def test_combine_partials_many(gpu, k):
+    """cpz_combine_partials (k_rlc_combine: lane j decodes partials j, j + 64, ..., a tree over
+    the lanes, no encoding for the identity): the sum of k encoded points equals the oracle's
+    (pyoracle pt_add / ristretto_encode), a set that sums to the identity reports it with 32
+    zero bytes, and a partial that does not decode is refused wherever it sits."""
+    from chaum_pedersen._native import CpzError
+    pts = [O.pt_mul(O.BASEPOINT, O.bench_scalar(b"combine", i)) for i in range(k)]
+    enc = [O.ristretto_encode(p) for p in pts]
+    acc = pts[0]
+    for p in pts[1:]:
+        acc = O.pt_add(acc, p)
+    assert gpu.combine_partials(enc) == (O.ristretto_encode(acc), False)
+    assert gpu.combine_partials(enc + [O.ristretto_encode(O.pt_neg(acc))]) == (bytes(32), True)
+    bad = list(enc)
+    bad[(7 * k) // 8] = (1).to_bytes(32, "little")  # s odd: not a canonical encoding
+    with pytest.raises(CpzError):
+        gpu.combine_partials(bad)
+
+
 def test_rlc_scale_valid_forged_fallback_and_shards(gpu):
     torch = pytest.importorskip("torch")
     n = 1 << 17
