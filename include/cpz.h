@@ -329,7 +329,7 @@ int cpz_verify_batch_multi(cpz_ctx *const *ctxs, int nctx, const uint8_t g[32], 
  * pairs, or of CPZ_GEN_CACHE = 1..4 set in the environment when it is created, and frees the
  * others when a new pair's combs do not fit); phases of the RLC MSM (inside stage 3): 8 = bucket
  * sort, 9 = bucket accumulation (k_rlc_bucket), 10 = bucket fix-up, 11 = bucket reduction
- * (segment + window), 12 = window combine + encode (k_rlc_final); 13 = variable-base generator
+ * (segment + window), 12 = window combine + encode (k_rlc_final16); 13 = variable-base generator
  * tables (a per-proof call of at most 16384 proofs on a pair other than the default one and
  * without combs in the cache builds only the pair's Niels tables and transcript prefix, ~0.5 ms
  * instead of ~3 ms, and verifies [s'] g, [s'] h from them; a context keeps 64 such pairs);

@@ -61,7 +61,7 @@ def _bump_s(t, torch, idx):
 @pytest.mark.parametrize("n", [3, 100, 511, 512])
 def test_small_msm_sparse_reduction_partials(gpu, n):
     """MSMs of at most 2048 points (n <= 511 proofs) form each window's sum from its non-empty
-    buckets alone (k_rlc_window_sparse, summed in k_rlc_final); larger ones run the running sums over
+    buckets alone (k_rlc_window_sparse, summed in k_rlc_final16); larger ones run the running sums over
     all 2^15 buckets (k_rlc_segment + k_rlc_window).  On both sides of the threshold: a valid
     batch gives the identity; with s + 1 forgeries (first, middle, last entry) the partial equals
     the C oracle's partial of the forged entries alone, at a non-zero first index."""
