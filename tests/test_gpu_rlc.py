@@ -101,6 +101,51 @@ def test_combine_partials_many(gpu, k):
         gpu.combine_partials(bad)
 
 
+def test_final_tree_knob_same_partials(gpu, tmp_path):
+    """CPZ_RLC_FINAL16=0 keeps the quad-tree window combine (k_rlc_final) selectable: child
+    processes with the knob off and on (the default, k_rlc_final16) give the same partials on a
+    sparse-path batch (n = 100) and a running-sums batch (n = 4096), both with s + 1 forgeries.
+    (Multi-span totals on the default are covered by test_gpu_scale at 2^24 and 2^26.)"""
+    import json
+    import os
+    import subprocess
+    import sys
+    torch = pytest.importorskip("torch")
+    seed = hashlib.sha256(b"cpz-final-knob").digest()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = [os.path.join(root, "chaum-pedersen-zkp_amd"), os.path.join(root, "oracle"), root]
+    script = tmp_path / "child.py"
+    script.write_text(
+        "import hashlib, json, sys\n"
+        "sys.path[:0] = %r\n"
+        "import numpy as np, torch, chaum_pedersen as cp\n"
+        "import pyoracle as O\n"
+        "g = cp.Gpu(0)\n"
+        "out = []\n"
+        "sx = hashlib.sha256(b'cpz-bench-x').digest(); sk = hashlib.sha256(b'cpz-bench-k').digest()\n"
+        "for n in (100, 4096):\n"
+        "    t = {k: torch.empty((n, 32), dtype=torch.uint8, device='cuda:0') for k in ('y1','y2','r1','r2','s')}\n"
+        "    g.prove_synthetic_device(n, sx, sk, t['y1'], t['y2'], t['r1'], t['r2'], t['s'], first_index=77)\n"
+        "    s_host = t['s'].cpu().numpy().copy()\n"
+        "    for i in (0, n // 3, n - 1):\n"
+        "        v = (int.from_bytes(s_host[i].tobytes(), 'little') + 1) %% O.L\n"
+        "        s_host[i] = np.frombuffer(v.to_bytes(32, 'little'), np.uint8)\n"
+        "    t['s'].copy_(torch.from_numpy(s_host))\n"
+        "    st = torch.empty(n, dtype=torch.uint8, device='cuda:0')\n"
+        "    p, ok = g.verify_batch_device(t['y1'], t['y2'], t['r1'], t['r2'], t['s'], st, bytes.fromhex(%r), first_index=77)\n"
+        "    out.append([p.hex(), bool(ok)])\n"
+        "g.close()\n"
+        "print(json.dumps(out))\n" % (paths, seed.hex()))
+    runs = {}
+    for knob in ("0", "1"):
+        env = dict(os.environ, CPZ_RLC_FINAL16=knob)
+        r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        runs[knob] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert runs["0"] == runs["1"]
+    assert all(not ok and p != "00" * 32 for p, ok in runs["1"])
+
+
 def test_rlc_scale_valid_forged_fallback_and_shards(gpu):
     torch = pytest.importorskip("torch")
     n = 1 << 17
